@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""Headline benchmark: GiB/s erasure-encoded (device-resident), RS(8,3) 4 MiB
+StorageBlocks, on 1/2/4/8 MI355X (BASELINE.json ``metric``, ``configs[1]``).
+
+A "step" is one pass of the hot path over one batch: encode every block of
+the per-GPU batch (B blocks x 8 data shards x 524,288 B) into 3 parity shards,
+inputs already resident in HBM.  Multi-GPU: one process per GPU, whole blocks
+round-robin (global block b -> rank b % N), no collectives on the data path
+(only the timing barrier / max-over-ranks reduction).  ``scaling`` is weak.
+
+Prints ONE JSON line (rank 0).  ``roofline`` is computed from HIP events
+recorded on the stream the kernel runs on; ``cpu_baseline`` times the CPU
+restatement of the crate's AVX2 loop (oracle/, test infrastructure) on a
+bounded sample of the same workload and checks the GPU parity of those sampled
+blocks bit-for-bit.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+import torch  # noqa: E402  (before shmr_amd: share one HIP runtime)
+import torch.distributed as dist  # noqa: E402
+
+import shmr_amd  # noqa: E402
+
+METRIC = "GiB/s erasure-encoded (device-resident), RS(8,3) 4 MiB StorageBlocks, 1/2/4/8 GPUs"
+HBM_PEAK = 8.0e12          # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md)
+SEED = 0x53484D52          # "SHMR"
+
+CONFIGS = {
+    # name: (k, p, block_bytes, erasures or None)
+    "encode83": (8, 3, 4 << 20, None),
+    "decode83": (8, 3, 4 << 20, 1),
+    "encode104": (10, 4, 16 << 20, None),
+    "decode104": (10, 4, 16 << 20, 2),
+    "encode42": (4, 2, 1 << 20, None),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="encode83", choices=sorted(CONFIGS))
+    ap.add_argument("--blocks", type=int, default=0, help="blocks per GPU (default: 512 for 4 MiB, 64 for 16 MiB)")
+    ap.add_argument("--chunks", type=int, default=2, help="16-B chunks per lane per tile (1, 2, 4)")
+    ap.add_argument("--nt", type=int, default=0, help="nontemporal loads/stores")
+    ap.add_argument("--grid-cap", type=int, default=0)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the cpu_baseline sample")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    k, p, block_bytes, erasures = CONFIGS[args.config]
+    S = shmr_amd.calculate_shard_size(block_bytes, k)
+    B = args.blocks or (512 if block_bytes <= (4 << 20) else 64)
+    shmr_amd.set_tuning(args.chunks, bool(args.nt), args.grid_cap)
+    rs = shmr_amd.ReedSolomon(k, p)
+
+    # Synthetic blocks, generated on the GPU from a per-rank seed (inputs
+    # resident in HBM before timing).  Layout = the reference's block buffer:
+    # shard i of block b at b*k*S + i*S (S = 524,288 is 16-B aligned).
+    g = torch.Generator(device=dev)
+    g.manual_seed(SEED + rank)
+    if erasures is None:
+        data = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=dev, generator=g)
+        parity = torch.empty((B, p, S), dtype=torch.uint8, device=dev)
+
+        def step():
+            rs.encode_batch_dev(data, parity, shard_len=S)
+        algo_bytes_per_block = (k + p) * S
+        payload_bytes_per_block = k * S
+    else:
+        pitch = (S + 255) // 256 * 256
+        shards = torch.zeros((B, k + p, pitch), dtype=torch.uint8, device=dev)
+        shards[:, :k, :S] = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=dev, generator=g)
+        rs.encode_batch_dev(shards[:, :k], shards[:, k:], shard_len=S,
+                            data_shard_pitch=pitch, parity_shard_pitch=pitch)
+        present = np.ones((B, k + p), dtype=np.uint8)
+        gb = np.arange(B) * world + rank
+        if erasures == 1:
+            present[np.arange(B), gb % k] = 0
+        else:
+            present[np.arange(B), gb % 10] = 0                     # config 4: {b%10, (b+3)%10}
+            present[np.arange(B), (gb + 3) % 10] = 0
+
+        def step():
+            rs.reconstruct_batch_dev(shards, present, shard_len=S)
+        algo_bytes_per_block = (k + erasures) * S
+        payload_bytes_per_block = k * S
+    torch.cuda.synchronize(dev)
+
+    stream = torch.cuda.current_stream(dev)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    t0 = time.perf_counter()
+    evs[0].record(stream)
+    for i in range(args.steps):
+        step()
+        evs[i + 1].record(stream)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    gpu_s = sum(step_ms) / 1e3
+    elapsed = max(wall, gpu_s)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_payload = payload_bytes_per_block * B * world * args.steps
+    value = total_payload / elapsed / 2 ** 30
+    kern_s = float(np.mean(step_ms)) / 1e3          # one dominant launch per step
+    achieved = algo_bytes_per_block * B / kern_s
+    out = {
+        "metric": METRIC if args.config == "encode83" else f"GiB/s {args.config} (device-resident)",
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic uniform random bytes generated on-device (torch.randint, seeded per rank)",
+        "config": {
+            "workload": {"encode83": "RS(8,3) encode, 4 MiB StorageBlocks, device-resident",
+                         "decode83": "RS(8,3) reconstruct, 1 missing data shard (b mod 8), 4 MiB blocks",
+                         "encode104": "RS(10,4) encode, 16 MiB StorageBlocks, device-resident",
+                         "decode104": "RS(10,4) reconstruct, 2 erasures {b mod 10, (b+3) mod 10}, 16 MiB",
+                         "encode42": "RS(4,2) encode, 1 MiB StorageBlocks, device-resident"}[args.config],
+            "data_shards": k, "parity_shards": p, "shard_bytes": S, "blocks_per_gpu": B,
+            "global_batch_blocks": B * world,
+            "parallelism": f"blocks round-robin over {world} GPU(s), no collectives",
+            "tuning": {"chunks_per_lane": args.chunks, "nontemporal": bool(args.nt), "grid_cap": args.grid_cap},
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved / 1e9, 2),
+            "peak": HBM_PEAK / 1e9,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK, 4),
+            "traffic": load_traffic(args.config, B),
+            "kernel_ms_avg": round(kern_s * 1e3, 4),
+            "algorithmic_bytes_per_launch": algo_bytes_per_block * B,
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu and erasures is None:
+        out["cpu_baseline"] = cpu_baseline(k, p, S, data, parity, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def load_traffic(config: str, B: int):
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if any."""
+    path = os.path.join(HERE, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f).get(config)
+    except (OSError, ValueError):
+        return None
+    if not rec or rec.get("blocks") != B:
+        return None
+    return rec.get("hbm_bytes_per_launch")
+
+
+def cpu_baseline(k, p, S, data_t, parity_t, budget_s):
+    """CPU restatement of the crate's simd_c AVX2 loop (oracle/, "port"),
+    one block per thread as rayon does over VirtualFile blocks; bounded sample
+    of the same workload; also checks the GPU parity of the sampled blocks."""
+    from oracle import c_oracle   # cpu_baseline leg: oracle allowed here only
+    cores = min(16, os.cpu_count() or 1)
+    nb = min(64, data_t.shape[0])
+    host_data = data_t[:nb].contiguous().cpu().numpy().reshape(-1)
+    host_par = np.zeros(nb * p * S, dtype=np.uint8)
+    reps, secs = 0, 0.0
+    while secs < budget_s or reps == 0:
+        secs += c_oracle.encode_batch(k, p, host_data, host_par, nb, S, cores, variant=1)
+        reps += 1
+    gpu_par = parity_t[:nb].contiguous().cpu().numpy().reshape(-1)
+    ok = bool(np.array_equal(gpu_par, host_par))
+    gib = nb * k * S * reps / secs / 2 ** 30
+    single = c_oracle.encode_batch(k, p, host_data[: k * S], host_par[: p * S], 1, S, 1, variant=1)
+    return {
+        "value": round(gib, 3),
+        "unit": "GiB/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": f"{nb} blocks x {reps} reps of the same RS({k},{p}) workload, {cores} threads "
+                  f"(one block per thread, AVX2 nibble-pshufb loop restating reed-solomon-erasure "
+                  f"6.0.0 simd_c); encode only (erasure_encode_duration scope, block.rs:425-430)",
+        "single_core_GiBps": round(k * S / single / 2 ** 30, 3),
+        "cpu_model": platform.processor() or platform.machine(),
+        "gpu_parity_bit_exact_on_sample": ok,
+    }
+
+
+if __name__ == "__main__":
+    main()

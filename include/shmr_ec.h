@@ -1,0 +1,166 @@
+/*
+ * shmr_ec.h -- C ABI of the MI355X-native Reed-Solomon erasure path for
+ * shmr's StorageBlock (VirtualBlock) layer.
+ *
+ * Drop-in boundary: the reference binds reed_solomon_erasure::galois_8::
+ * ReedSolomon (reference src/vfs/block.rs:10) and calls exactly three
+ * entry points on the hot path:
+ *
+ *   ReedSolomon::new(data, parity)        src/vfs/block.rs:405, :531  -> shmr_ec_new
+ *   r.encode(&mut Vec<Vec<u8>>)           src/vfs/block.rs:427        -> shmr_ec_encode
+ *   r.reconstruct(&mut Vec<Option<..>>)   src/vfs/block.rs:560        -> shmr_ec_reconstruct
+ *
+ * plus the shard-size helper the callers use before every encode/decode
+ * (calculate_shard_size, src/vfs/mod.rs:16-18) -> shmr_ec_shard_size.
+ *
+ * Everything runs on AMD Instinct MI355X (gfx950) through hand-written HIP
+ * kernels.  There is no CPU compute fallback: without a usable GPU every
+ * compute entry point returns SHMR_EC_NO_DEVICE / SHMR_EC_DEVICE_ERROR.
+ *
+ * Conventions: plain pointers and sizes, 0 on success, negative status on
+ * failure, never aborts, never frees caller memory.  Thread-safe: contexts
+ * may be shared across threads or created per call (the reference creates a
+ * ReedSolomon per block from rayon workers, src/vfs/mod.rs:93-96).
+ */
+#ifndef SHMR_EC_H
+#define SHMR_EC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Status codes.  -1..-13 are 1:1 with reed_solomon_erasure::Error (6.0.0),
+ * which the reference wraps as ShmrError::EcError (src/config.rs:158,170-174). */
+typedef enum shmr_ec_status {
+    SHMR_EC_OK = 0,
+    SHMR_EC_TOO_FEW_SHARDS = -1,
+    SHMR_EC_TOO_MANY_SHARDS = -2,
+    SHMR_EC_TOO_FEW_DATA_SHARDS = -3,
+    SHMR_EC_TOO_MANY_DATA_SHARDS = -4,
+    SHMR_EC_TOO_FEW_PARITY_SHARDS = -5,
+    SHMR_EC_TOO_MANY_PARITY_SHARDS = -6,
+    SHMR_EC_TOO_FEW_BUFFER_SHARDS = -7,
+    SHMR_EC_TOO_MANY_BUFFER_SHARDS = -8,
+    SHMR_EC_INCORRECT_SHARD_SIZE = -9,
+    SHMR_EC_TOO_FEW_SHARDS_PRESENT = -10,
+    SHMR_EC_EMPTY_SHARD = -11,
+    SHMR_EC_INVALID_SHARD_FLAGS = -12,
+    SHMR_EC_INVALID_INDEX = -13,
+    /* library-level conditions (no crate equivalent) */
+    SHMR_EC_INVALID_ARGUMENT = -100,
+    SHMR_EC_NO_DEVICE = -101,
+    SHMR_EC_DEVICE_ERROR = -102,
+    SHMR_EC_OUT_OF_MEMORY = -103
+} shmr_ec_status;
+
+typedef struct shmr_ec shmr_ec_t;
+
+/* Human-readable name of a status ("TooFewShardsPresent", ...). */
+const char* shmr_ec_status_name(int status);
+
+/* Library version string. */
+const char* shmr_ec_version(void);
+
+/* ---- host logic (no GPU needed) ---------------------------------------- */
+
+/* calculate_shard_size, src/vfs/mod.rs:16-18:
+ * (length as f32 / data_shards as f32).ceil() as usize. 0 if data_shards==0. */
+size_t shmr_ec_shard_size(uint64_t length, uint32_t data_shards);
+
+/* ReedSolomon::new (src/vfs/block.rs:405,531).  Errors exactly as the crate:
+ * data==0 -> TOO_FEW_DATA_SHARDS, parity==0 -> TOO_FEW_PARITY_SHARDS,
+ * data+parity > 256 -> TOO_MANY_SHARDS.  Builds the (data+parity) x data
+ * systematic Vandermonde matrix on the host; touches no GPU. */
+int shmr_ec_new(uint32_t data_shards, uint32_t parity_shards, shmr_ec_t** out);
+void shmr_ec_free(shmr_ec_t* rs);
+
+uint32_t shmr_ec_data_shard_count(const shmr_ec_t* rs);
+uint32_t shmr_ec_parity_shard_count(const shmr_ec_t* rs);
+uint32_t shmr_ec_total_shard_count(const shmr_ec_t* rs);
+
+/* Copies the (data+parity) x data coding matrix, row-major, into out
+ * (out_len >= total*data). */
+int shmr_ec_matrix(const shmr_ec_t* rs, uint8_t* out, size_t out_len);
+
+/* Rows of the reconstruct plan the library would run for a presence
+ * pattern: out_rows[m * data + t] (m < *n_out) applied to the shards listed in
+ * in_idx[0..data) rebuilds shard out_idx[m].  Host only; for tests/tools. */
+int shmr_ec_reconstruct_plan(shmr_ec_t* rs, const uint8_t* present, size_t nshards, int data_only,
+                             uint16_t* in_idx, uint16_t* out_idx, uint8_t* out_rows,
+                             size_t out_rows_len, uint32_t* n_out);
+
+/* ---- host-buffer entry points (drop-in for the crate calls) ------------- */
+
+/* ReedSolomon::encode (src/vfs/block.rs:427).  shards[0..data) are inputs,
+ * shards[data..total) are overwritten with parity.  shard_lens[i] is the
+ * length of shards[i]; the crate's checks run first and in its order
+ * (count -> TOO_FEW/TOO_MANY_SHARDS, len 0 -> EMPTY_SHARD, unequal ->
+ * INCORRECT_SHARD_SIZE).  H2D, kernel, D2H on the context's device. */
+int shmr_ec_encode(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_lens, size_t nshards);
+
+/* ReedSolomon::reconstruct / reconstruct_data (src/vfs/block.rs:560).
+ * present[i] != 0 marks shard i as Some(..); shard_lens[i] is only read for
+ * present shards.  Absent shards must point at caller buffers of the common
+ * shard length (the crate allocates them; the Rust shim allocates
+ * vec![0; len] before calling).  data_only != 0: absent parity shards are left
+ * untouched (and may be NULL).  All present -> no-op; fewer than data present
+ * -> TOO_FEW_SHARDS_PRESENT. */
+int shmr_ec_reconstruct(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_lens,
+                        const uint8_t* present, size_t nshards, int data_only);
+
+/* ---- device-resident batched entry points ------------------------------ *
+ * All pointers are device pointers on `device`; `stream` is a hipStream_t
+ * (NULL = the null stream).  Calls are asynchronous w.r.t. the host: they
+ * enqueue kernels on `stream` and return.  Block b's shard i lives at
+ *     base + b * block_pitch + i * shard_pitch.
+ * 16-byte aligned bases/pitches take the vector path; anything else is
+ * handled byte-granularly (correct, slower). */
+
+/* Encode nblocks blocks: data shard i of block b at
+ * d_data + b*data_block_pitch + i*data_shard_pitch; parity shard r at
+ * d_parity + b*parity_block_pitch + r*parity_shard_pitch. */
+int shmr_ec_encode_batch_dev(shmr_ec_t* rs, const uint8_t* d_data, size_t data_shard_pitch,
+                             size_t data_block_pitch, uint8_t* d_parity, size_t parity_shard_pitch,
+                             size_t parity_block_pitch, size_t nblocks, size_t shard_len,
+                             int device, void* stream);
+
+/* Reconstruct nblocks blocks in place.  All total shards of block b live at
+ * d_shards + b*block_pitch + i*shard_pitch.  present is HOST memory,
+ * nblocks x total flags (row-major).  Blocks may have different presence
+ * patterns; validation of every block precedes any launch. */
+int shmr_ec_reconstruct_batch_dev(shmr_ec_t* rs, uint8_t* d_shards, size_t shard_pitch,
+                                  size_t block_pitch, const uint8_t* present, size_t nblocks,
+                                  size_t shard_len, int data_only, int device, void* stream);
+
+/* ---- multi-GPU host batch ------------------------------------------------ *
+ * Encode nblocks blocks held in HOST memory, whole blocks round-robin across
+ * `devices` (block b -> devices[b % ndev]), H2D/kernel/D2H pipelined per
+ * device.  host_shards[b * total + i] points at shard i of block b (data
+ * read, parity written), each shard_len bytes.  Synchronous. */
+int shmr_ec_encode_blocks_host(shmr_ec_t* rs, uint8_t* const* host_shards, size_t nblocks,
+                               size_t shard_len, const int* devices, int ndev);
+
+/* ---- configuration -------------------------------------------------------- */
+
+/* Device used by the host-buffer entry points (default 0). */
+int shmr_ec_set_device(shmr_ec_t* rs, int device);
+
+/* Kernel tuning knobs (process-wide): chunks of 16 B per lane per tile
+ * (1, 2 or 4), nontemporal loads/stores (0/1), grid cap (0 = occupancy). */
+int shmr_ec_set_tuning(int chunks_per_lane, int nontemporal, int grid_cap);
+
+/* Decode-matrix LRU statistics of the (data, parity) codec (crate cache
+ * semantics, capacity 254). */
+int shmr_ec_cache_stats(const shmr_ec_t* rs, uint64_t* hits, uint64_t* misses);
+
+/* Number of visible GPUs (0 when none; never fails). */
+int shmr_ec_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SHMR_EC_H */

@@ -1,0 +1,78 @@
+"""Loader for the in-tree native library ``shmr_amd/_lib/libshmr_ec.so``.
+
+There is no fallback: if the library is missing or fails to load, importing
+the compute API raises.  ``torch`` is imported first when available so that
+the library binds to the same HIP runtime instance as PyTorch (both carry the
+SONAME ``libamdhip64.so.7``; loading ours first would map a second runtime).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+try:  # share torch's HIP runtime (see module docstring)
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is part of the image
+    torch = None
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libshmr_ec.so")
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u8pp = ctypes.POINTER(_u8p)
+_sz = ctypes.c_size_t
+
+# (name, restype, argtypes) for every symbol declared in include/shmr_ec.h
+SIGNATURES = [
+    ("shmr_ec_status_name", ctypes.c_char_p, [ctypes.c_int]),
+    ("shmr_ec_version", ctypes.c_char_p, []),
+    ("shmr_ec_shard_size", _sz, [ctypes.c_uint64, ctypes.c_uint32]),
+    ("shmr_ec_new", ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),
+    ("shmr_ec_free", None, [ctypes.c_void_p]),
+    ("shmr_ec_data_shard_count", ctypes.c_uint32, [ctypes.c_void_p]),
+    ("shmr_ec_parity_shard_count", ctypes.c_uint32, [ctypes.c_void_p]),
+    ("shmr_ec_total_shard_count", ctypes.c_uint32, [ctypes.c_void_p]),
+    ("shmr_ec_matrix", ctypes.c_int, [ctypes.c_void_p, _u8p, _sz]),
+    ("shmr_ec_reconstruct_plan", ctypes.c_int,
+     [ctypes.c_void_p, _u8p, _sz, ctypes.c_int, ctypes.POINTER(ctypes.c_uint16),
+      ctypes.POINTER(ctypes.c_uint16), _u8p, _sz, ctypes.POINTER(ctypes.c_uint32)]),
+    ("shmr_ec_encode", ctypes.c_int, [ctypes.c_void_p, _u8pp, ctypes.POINTER(_sz), _sz]),
+    ("shmr_ec_reconstruct", ctypes.c_int,
+     [ctypes.c_void_p, _u8pp, ctypes.POINTER(_sz), _u8p, _sz, ctypes.c_int]),
+    ("shmr_ec_encode_batch_dev", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, _sz, _sz, ctypes.c_void_p, _sz, _sz, _sz, _sz,
+      ctypes.c_int, ctypes.c_void_p]),
+    ("shmr_ec_reconstruct_batch_dev", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, _sz, _sz, _u8p, _sz, _sz, ctypes.c_int, ctypes.c_int,
+      ctypes.c_void_p]),
+    ("shmr_ec_encode_blocks_host", ctypes.c_int,
+     [ctypes.c_void_p, _u8pp, _sz, _sz, ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    ("shmr_ec_set_device", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    ("shmr_ec_set_tuning", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    ("shmr_ec_cache_stats", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    ("shmr_ec_device_count", ctypes.c_int, []),
+]
+
+_lib = None
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def lib():
+    """Returns the loaded native library; raises if it is not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeLibraryMissing(
+                f"{LIB_PATH} is missing: build it with `make -C shmr_amd/csrc` or "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib

@@ -1,0 +1,48 @@
+// Launch interface of the gfx950 GF(2^8) matrix-apply kernel (gf_apply.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace shmr {
+namespace kern {
+
+constexpr int kThreads = 256;                          // lanes per workgroup (4 waves)
+// A tile = kThreads * 16 * U bytes of columns of one block; U (16-byte chunks
+// per lane per shard) is a launch parameter in {1, 2, 4}.
+inline uint64_t tile_bytes(int u) { return uint64_t(kThreads) * 16 * uint64_t(u); }
+constexpr unsigned kMaxRowsPerLaunch = 4;
+
+// Shard t of block b lives at in_base + b * in_bpitch + in_idx[t] * in_spitch,
+// output r of block b at out_base + b * out_bpitch + (out_idx[row0 + r] - out_bias) * out_spitch.
+// Blocks of a launch: blk_list[j] if blk_list, else blk_first + j * blk_stride.
+struct ApplyArgs {
+    const uint8_t* in_base;
+    uint8_t* out_base;
+    uint64_t in_bpitch, in_spitch;
+    uint64_t out_bpitch, out_spitch;
+    const uint32_t* blk_list;
+    uint64_t blk_first, blk_stride;
+    uint64_t nblk;
+    uint64_t len;            // shard length in bytes
+    uint64_t col_base;       // column of tile 0 (tail launches start at the last partial tile)
+    uint64_t ntiles;         // nblk * tiles_per_block
+    uint32_t tiles_per_block;
+    uint32_t k;              // inputs per block
+    uint32_t m;              // rows in the plan image
+    uint32_t row0;           // first plan row handled by this launch
+    uint32_t out_bias;       // output r at (out_idx[row0 + r] - out_bias) * out_spitch
+    const uint8_t* plan;     // device plan image (gf256.hpp Plan::image)
+    uint32_t tab_off;        // byte offset of the PermTab array in the image
+};
+
+// rows in [1, kMaxRowsPerLaunch].  mode 0: full tiles, every shard base
+// (base + b*bpitch + idx*spitch) 16-byte aligned; mode 1: one partial tail
+// tile per block (aligned); mode 2: any alignment, byte-granular.
+// grid_cap <= 0: occupancy-sized grid.
+hipError_t launch_apply(const ApplyArgs& a, unsigned rows, int u, int mode, bool nt, int grid_cap,
+                        hipStream_t stream);
+
+}  // namespace kern
+}  // namespace shmr

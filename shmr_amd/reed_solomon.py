@@ -1,0 +1,210 @@
+"""Host-side mirror of ``reed_solomon_erasure::galois_8::ReedSolomon``.
+
+The reference binds the crate at ``src/vfs/block.rs:10`` and calls
+``ReedSolomon::new`` (block.rs:405, :531), ``encode`` (block.rs:427) and
+``reconstruct`` (block.rs:560).  This class keeps those names, argument
+meanings and error behaviour (``Error.name`` is the crate variant name), and
+runs every byte of arithmetic on the MI355X through ``include/shmr_ec.h``.
+
+Device-resident batch entry points (``encode_batch_dev`` /
+``reconstruct_batch_dev``) take torch CUDA(HIP) tensors and enqueue on the
+current torch stream.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, MutableSequence, Optional, Sequence
+
+import numpy as np
+
+from ._native import _u8p, lib
+
+__all__ = ["Error", "ReedSolomon", "calculate_shard_size", "device_count", "set_tuning"]
+
+
+class Error(Exception):
+    """A non-zero status from the native library (crate variant names)."""
+
+    def __init__(self, code: int):
+        self.code = code
+        self.name = lib().shmr_ec_status_name(code).decode()
+        super().__init__(f"{self.name} ({code})")
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        raise Error(rc)
+
+
+def calculate_shard_size(length: int, data_shards: int) -> int:
+    """``calculate_shard_size`` (reference src/vfs/mod.rs:16-18), f32 ceil."""
+    return int(lib().shmr_ec_shard_size(length, data_shards))
+
+
+def device_count() -> int:
+    return int(lib().shmr_ec_device_count())
+
+
+def set_tuning(chunks_per_lane: int = 2, nontemporal: bool = False, grid_cap: int = 0) -> None:
+    _check(lib().shmr_ec_set_tuning(chunks_per_lane, int(bool(nontemporal)), grid_cap))
+
+
+def _writable_u8(buf) -> np.ndarray:
+    """A uint8 view over a writable buffer (bytearray, numpy array, memoryview)."""
+    if isinstance(buf, np.ndarray):
+        if buf.dtype != np.uint8 or not buf.flags["C_CONTIGUOUS"]:
+            raise TypeError("shards must be C-contiguous uint8 arrays")
+        return buf
+    arr = np.frombuffer(buf, dtype=np.uint8)
+    if not arr.flags["WRITEABLE"]:
+        raise TypeError("shard buffers must be writable (bytearray / numpy)")
+    return arr
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(_u8p) if a.size else ctypes.cast(ctypes.c_void_p(1), _u8p)
+
+
+class ReedSolomon:
+    """``ReedSolomon::new(data_shards, parity_shards)`` -- raises ``Error``."""
+
+    def __init__(self, data_shards: int, parity_shards: int, device: int = 0):
+        h = ctypes.c_void_p()
+        _check(lib().shmr_ec_new(data_shards, parity_shards, ctypes.byref(h)))
+        self._h = h
+        if device:
+            _check(lib().shmr_ec_set_device(self._h, device))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib().shmr_ec_free(h)
+            self._h = None
+
+    # -- crate accessors -------------------------------------------------------
+    def data_shard_count(self) -> int:
+        return int(lib().shmr_ec_data_shard_count(self._h))
+
+    def parity_shard_count(self) -> int:
+        return int(lib().shmr_ec_parity_shard_count(self._h))
+
+    def total_shard_count(self) -> int:
+        return int(lib().shmr_ec_total_shard_count(self._h))
+
+    def matrix(self) -> np.ndarray:
+        t, k = self.total_shard_count(), self.data_shard_count()
+        out = np.zeros(t * k, dtype=np.uint8)
+        _check(lib().shmr_ec_matrix(self._h, _ptr(out), out.size))
+        return out.reshape(t, k)
+
+    def set_device(self, device: int) -> None:
+        _check(lib().shmr_ec_set_device(self._h, device))
+
+    def cache_stats(self):
+        h, m = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().shmr_ec_cache_stats(self._h, ctypes.byref(h), ctypes.byref(m)))
+        return int(h.value), int(m.value)
+
+    def reconstruct_plan(self, present: Sequence[bool], data_only: bool = False):
+        """(in_idx, out_idx, rows) of the plan the GPU runs for this pattern."""
+        t, k = self.total_shard_count(), self.data_shard_count()
+        pr = np.array([1 if x else 0 for x in present], dtype=np.uint8)
+        in_idx = (ctypes.c_uint16 * k)()
+        out_idx = (ctypes.c_uint16 * t)()
+        rows = np.zeros(t * k, dtype=np.uint8)
+        n = ctypes.c_uint32()
+        _check(lib().shmr_ec_reconstruct_plan(self._h, _ptr(pr), len(pr), int(data_only), in_idx, out_idx,
+                                              _ptr(rows), rows.size, ctypes.byref(n)))
+        m = n.value
+        return list(in_idx), list(out_idx)[:m], rows[:m * k].reshape(m, k).copy()
+
+    # -- crate calls ---------------------------------------------------------------
+    def encode(self, shards: MutableSequence) -> None:
+        """``ReedSolomon::encode``: shards[k:] are overwritten with parity."""
+        arrs = [_writable_u8(s) for s in shards]
+        n = len(arrs)
+        ptrs = (_u8p * max(n, 1))(*[_ptr(a) for a in arrs])
+        lens = (ctypes.c_size_t * max(n, 1))(*[a.size for a in arrs])
+        _check(lib().shmr_ec_encode(self._h, ptrs, lens, n))
+
+    def _reconstruct(self, shards: MutableSequence[Optional[object]], data_only: bool) -> None:
+        n = len(shards)
+        k = self.data_shard_count()
+        present = np.array([s is not None for s in shards], dtype=np.uint8)
+        arrs: List[Optional[np.ndarray]] = [None if s is None else _writable_u8(s) for s in shards]
+        shard_len = next((a.size for a in arrs if a is not None), 0)
+        # The crate allocates absent shards (get_or_initialize); mirror that,
+        # but only once the crate's own checks would pass.
+        fill = [False] * n
+        if n == self.total_shard_count() and 0 < present.sum() < n and present.sum() >= k:
+            for i, a in enumerate(arrs):
+                if a is None and (i < k or not data_only):
+                    arrs[i] = np.zeros(shard_len, dtype=np.uint8)
+                    fill[i] = True
+        ptrs = (_u8p * max(n, 1))(*[(_ptr(a) if a is not None else _u8p()) for a in arrs])
+        lens = (ctypes.c_size_t * max(n, 1))(*[(a.size if a is not None else 0) for a in arrs])
+        _check(lib().shmr_ec_reconstruct(self._h, ptrs, lens, _ptr(present), n, int(data_only)))
+        for i in range(n):
+            if fill[i]:
+                shards[i] = arrs[i]
+
+    def reconstruct(self, shards: MutableSequence[Optional[object]]) -> None:
+        """``ReedSolomon::reconstruct``: None entries become rebuilt shards."""
+        self._reconstruct(shards, data_only=False)
+
+    def reconstruct_data(self, shards: MutableSequence[Optional[object]]) -> None:
+        """``ReedSolomon::reconstruct_data``: only absent data shards are rebuilt."""
+        self._reconstruct(shards, data_only=True)
+
+    def verify(self, shards: Sequence) -> bool:
+        """``ReedSolomon::verify``: recompute parity on the GPU and compare."""
+        k = self.data_shard_count()
+        arrs = [_writable_u8(s) if not isinstance(s, (bytes,)) else np.frombuffer(s, np.uint8) for s in shards]
+        tmp = [a.copy() for a in arrs[:k]] + [np.zeros_like(a) for a in arrs[k:]]
+        self.encode(tmp)
+        return all(np.array_equal(a, b) for a, b in zip(tmp[k:], arrs[k:]))
+
+    # -- device-resident batches (torch tensors on the GPU) ------------------------
+    @staticmethod
+    def _stream_and_device(t):
+        import torch
+        dev = t.device.index if t.device.index is not None else torch.cuda.current_device()
+        return dev, ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+    def encode_batch_dev(self, data, parity, shard_len: Optional[int] = None,
+                         data_shard_pitch: Optional[int] = None, parity_shard_pitch: Optional[int] = None) -> None:
+        """data: uint8 [B, k, pitch] (or [B, k*pitch]); parity: uint8 [B, p, pitch'].
+
+        Enqueued on torch's current stream of the tensors' device."""
+        B = data.shape[0]
+        dbp = data.stride(0)
+        pbp = parity.stride(0)
+        dsp = data_shard_pitch if data_shard_pitch is not None else (data.stride(1) if data.dim() == 3 else dbp // self.data_shard_count())
+        psp = parity_shard_pitch if parity_shard_pitch is not None else (parity.stride(1) if parity.dim() == 3 else pbp // self.parity_shard_count())
+        L = shard_len if shard_len is not None else dsp
+        dev, stream = self._stream_and_device(data)
+        _check(lib().shmr_ec_encode_batch_dev(self._h, ctypes.c_void_p(data.data_ptr()), dsp, dbp,
+                                              ctypes.c_void_p(parity.data_ptr()), psp, pbp, B, L, dev, stream))
+
+    def reconstruct_batch_dev(self, shards, present: np.ndarray, shard_len: Optional[int] = None,
+                              data_only: bool = False) -> None:
+        """shards: uint8 [B, total, pitch] on the GPU; present: host bool/uint8 [B, total]."""
+        B, t = shards.shape[0], shards.shape[1]
+        pr = np.ascontiguousarray(present, dtype=np.uint8).reshape(B, t)
+        L = shard_len if shard_len is not None else shards.stride(1)
+        dev, stream = self._stream_and_device(shards)
+        _check(lib().shmr_ec_reconstruct_batch_dev(self._h, ctypes.c_void_p(shards.data_ptr()), shards.stride(1),
+                                                   shards.stride(0), _ptr(pr), B, L, int(data_only), dev, stream))
+
+    def encode_blocks_host(self, blocks: Sequence[Sequence[np.ndarray]], devices: Sequence[int] = (0,)) -> None:
+        """Encode many host-resident blocks, whole blocks round-robin over devices."""
+        t = self.total_shard_count()
+        arrs = [[_writable_u8(s) for s in blk] for blk in blocks]
+        for blk in arrs:
+            if len(blk) != t:
+                raise Error(-1 if len(blk) < t else -2)
+        L = arrs[0][0].size if arrs else 0
+        flat = [a for blk in arrs for a in blk]
+        ptrs = (_u8p * max(len(flat), 1))(*[_ptr(a) for a in flat])
+        devs = (ctypes.c_int * len(devices))(*devices)
+        _check(lib().shmr_ec_encode_blocks_host(self._h, ptrs, len(arrs), L, devs, len(devices)))

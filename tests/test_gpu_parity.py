@@ -1,0 +1,275 @@
+"""GPU parity tests: the HIP path through the C ABI vs the CPU oracle, bit-exact.
+
+Reference call sites under test: ReedSolomon::encode (src/vfs/block.rs:427)
+and ReedSolomon::reconstruct (src/vfs/block.rs:560), with shard sizes from
+calculate_shard_size (src/vfs/mod.rs:16-18).
+"""
+import itertools
+
+import numpy as np
+import pytest
+
+import shmr_amd
+from oracle import c_oracle
+from oracle import rs_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def rand_shards(rng, n, L):
+    return [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(n)]
+
+
+def oracle_parity(k, p, data):
+    L = len(data[0])
+    sh = [d.copy() for d in data] + [np.zeros(L, np.uint8) for _ in range(p)]
+    c_oracle.encode(k, p, sh)
+    return sh[k:]
+
+
+# ---------------------------------------------------------------- host-buffer API
+@pytest.mark.parametrize("k,p,L", [(4, 2, 262144), (8, 3, 524288), (10, 4, 1677722), (5, 5, 2),
+                                   (1, 1, 1), (3, 2, 17), (8, 3, 4095), (8, 3, 4097), (8, 3, 8192 + 5),
+                                   (17, 3, 100003), (2, 7, 33)])
+def test_encode_host_matches_oracle(gpu, k, p, L):
+    rng = np.random.default_rng([k, p, L])
+    data = rand_shards(rng, k, L)
+    shards = [d.copy() for d in data] + [np.full(L, 0xAA, np.uint8) for _ in range(p)]
+    shmr_amd.ReedSolomon(k, p).encode(shards)
+    for a, b in zip(shards[k:], oracle_parity(k, p, data)):
+        assert np.array_equal(a, b)
+    for a, b in zip(shards[:k], data):
+        assert np.array_equal(a, b)   # inputs untouched
+
+
+def test_encode_kat_5_5(gpu):
+    """Upstream known-answer vector (JavaReedSolomon / crate test_encoding)."""
+    data = [[0, 1], [4, 5], [2, 3], [6, 7], [8, 9]]
+    shards = [np.array(d, np.uint8) for d in data] + [np.zeros(2, np.uint8) for _ in range(5)]
+    shmr_amd.ReedSolomon(5, 5).encode(shards)
+    assert [s.tolist() for s in shards[5:]] == [[12, 13], [10, 11], [14, 15], [90, 91], [94, 95]]
+
+
+@pytest.mark.parametrize("fill", [0x00, 0xFF])
+def test_encode_constant_blocks(gpu, fill):
+    k, p, L = 8, 3, 524288
+    data = [np.full(L, fill, np.uint8) for _ in range(k)]
+    shards = [d.copy() for d in data] + [np.zeros(L, np.uint8) for _ in range(p)]
+    shmr_amd.ReedSolomon(k, p).encode(shards)
+    for a, b in zip(shards[k:], oracle_parity(k, p, data)):
+        assert np.array_equal(a, b)
+
+
+def test_every_coefficient_and_byte(gpu):
+    """Exhaustive multiply check: 256 data values x every coefficient that a
+    (255, 1) code and a (1, 255) code use."""
+    for k, p in [(255, 1), (1, 255), (128, 128)]:
+        L = 256 * 3 + 7
+        rng = np.random.default_rng(k)
+        data = [np.resize(np.roll(np.arange(256, dtype=np.uint8), i), L) for i in range(k)]
+        data[0] = rng.integers(0, 256, L, dtype=np.uint8)
+        shards = [d.copy() for d in data] + [np.zeros(L, np.uint8) for _ in range(p)]
+        shmr_amd.ReedSolomon(k, p).encode(shards)
+        for a, b in zip(shards[k:], oracle_parity(k, p, data)):
+            assert np.array_equal(a, b), (k, p)
+
+
+PATTERNS_83 = [
+    [0], [7], [8], [10], [0, 8], [3, 4], [1, 9, 10], [0, 1, 2], [5, 6, 7], [2, 8, 9],
+]
+
+
+@pytest.mark.parametrize("missing", PATTERNS_83)
+@pytest.mark.parametrize("data_only", [False, True])
+def test_reconstruct_host_matches_oracle(gpu, missing, data_only):
+    k, p, L = 8, 3, 524288 + 13
+    rng = np.random.default_rng(sum(missing) + 100 * data_only)
+    full = rand_shards(rng, k, L)
+    full += oracle_parity(k, p, full)
+    got = [None if i in missing else full[i].copy() for i in range(k + p)]
+    rs = shmr_amd.ReedSolomon(k, p)
+    (rs.reconstruct_data if data_only else rs.reconstruct)(got)
+    ref = [None if i in missing else full[i].copy() for i in range(k + p)]
+    (O.ReedSolomon(k, p).reconstruct_data if data_only else O.ReedSolomon(k, p).reconstruct)(ref)
+    for i in range(k + p):
+        if data_only and i >= k and i in missing:
+            assert got[i] is None
+            continue
+        assert np.array_equal(got[i], ref[i]), i
+        assert np.array_equal(got[i], full[i]), i
+
+
+def test_reconstruct_inconsistent_shards_follow_crate(gpu):
+    """Inputs that are not a codeword: the crate uses the first k present
+    shards and then re-encodes missing parity from the rebuilt data."""
+    k, p, L = 4, 3, 4099
+    rng = np.random.default_rng(7)
+    shards = rand_shards(rng, k + p, L)      # random: not a codeword
+    for missing in itertools.combinations(range(k + p), 2):
+        got = [None if i in missing else shards[i].copy() for i in range(k + p)]
+        ref = [None if i in missing else shards[i].copy() for i in range(k + p)]
+        shmr_amd.ReedSolomon(k, p).reconstruct(got)
+        O.ReedSolomon(k, p).reconstruct(ref)
+        for i in range(k + p):
+            assert np.array_equal(got[i], ref[i]), (missing, i)
+
+
+def test_reconstruct_all_patterns_10_4(gpu):
+    k, p, L = 10, 4, 3000
+    rng = np.random.default_rng(11)
+    full = rand_shards(rng, k, L)
+    full += oracle_parity(k, p, full)
+    rs = shmr_amd.ReedSolomon(k, p)
+    for n in (1, 2, 3, 4):
+        for missing in itertools.combinations(range(k + p), n):
+            got = [None if i in missing else full[i].copy() for i in range(k + p)]
+            rs.reconstruct(got)
+            for i in missing:
+                assert np.array_equal(got[i], full[i]), (missing, i)
+
+
+# --------------------------------------------------------------- device batch API
+def _dev_encode_check(gpu, k, p, L, B, chunks=2, nt=False, pitch=None):
+    import torch
+    shmr_amd.set_tuning(chunks, nt, 0)
+    try:
+        pitch = pitch or L
+        g = torch.Generator(device=gpu)
+        g.manual_seed(k * 1000 + p * 10 + B)
+        data = torch.randint(0, 256, (B, k, pitch), dtype=torch.uint8, device=gpu, generator=g)
+        parity = torch.full((B, p, pitch), 0x5A, dtype=torch.uint8, device=gpu)
+        shmr_amd.ReedSolomon(k, p).encode_batch_dev(data, parity, shard_len=L)
+        torch.cuda.synchronize()
+        hd, hp = data.cpu().numpy(), parity.cpu().numpy()
+        for b in range(B):
+            ref = oracle_parity(k, p, [hd[b, i, :L].copy() for i in range(k)])
+            for r in range(p):
+                assert np.array_equal(hp[b, r, :L], ref[r]), (b, r)
+                assert (hp[b, r, L:] == 0x5A).all(), "wrote past shard_len"
+    finally:
+        shmr_amd.set_tuning(2, False, 0)
+
+
+@pytest.mark.parametrize("k,p,L,B", [(8, 3, 524288, 16), (4, 2, 262144, 8), (10, 4, 1677722, 3),
+                                     (6, 3, 8192 * 3 + 16, 5), (3, 5, 16, 7)])
+def test_encode_batch_dev(gpu, k, p, L, B):
+    _dev_encode_check(gpu, k, p, L, B, pitch=(L + 255) // 256 * 256)
+
+
+@pytest.mark.parametrize("chunks,nt", [(1, False), (2, True), (4, False), (4, True)])
+def test_encode_batch_dev_tuning_variants(gpu, chunks, nt):
+    _dev_encode_check(gpu, 8, 3, 524288 + 4096 + 48, 4, chunks=chunks, nt=nt,
+                      pitch=524288 + 8192)
+
+
+def test_encode_batch_dev_unaligned_reference_layout(gpu):
+    """The reference buffer layout with S = 1,677,722 (S % 4 == 2): shard i at
+    i*S, so odd shards are misaligned -> byte-granular path, same bytes."""
+    import torch
+    k, p = 10, 4
+    S = shmr_amd.calculate_shard_size(16 << 20, k)
+    assert S == 1677722
+    g = torch.Generator(device=gpu)
+    g.manual_seed(3)
+    B = 2
+    data = torch.randint(0, 256, (B, k * S), dtype=torch.uint8, device=gpu, generator=g)
+    parity = torch.empty((B, p * S), dtype=torch.uint8, device=gpu)
+    shmr_amd.ReedSolomon(k, p).encode_batch_dev(data, parity, shard_len=S, data_shard_pitch=S,
+                                                parity_shard_pitch=S)
+    torch.cuda.synchronize()
+    hd, hp = data.cpu().numpy(), parity.cpu().numpy()
+    for b in range(B):
+        ref = oracle_parity(k, p, [hd[b, i * S:(i + 1) * S].copy() for i in range(k)])
+        for r in range(p):
+            assert np.array_equal(hp[b, r * S:(r + 1) * S], ref[r])
+
+
+@pytest.mark.parametrize("k,p,erasures", [(8, 3, 1), (10, 4, 2), (8, 3, 3)])
+def test_reconstruct_batch_dev_mixed_patterns(gpu, k, p, erasures):
+    import torch
+    S = 65536 + 12
+    pitch = (S + 255) // 256 * 256
+    B = 24
+    rng = np.random.default_rng(k + erasures)
+    host = rng.integers(0, 256, (B, k + p, pitch), dtype=np.uint8)
+    for b in range(B):
+        par = oracle_parity(k, p, [host[b, i, :S].copy() for i in range(k)])
+        for r in range(p):
+            host[b, k + r, :S] = par[r]
+    present = np.ones((B, k + p), np.uint8)
+    for b in range(B):
+        miss = rng.choice(k + p, size=erasures, replace=False)
+        present[b, miss] = 0
+    present[5] = 1                 # an all-present block is a no-op
+    dev = torch.from_numpy(host.copy()).to(gpu)
+    # poison the erased shards on the device
+    for b in range(B):
+        for i in range(k + p):
+            if not present[b, i]:
+                dev[b, i, :S] = 0xEE
+    rs = shmr_amd.ReedSolomon(k, p)
+    rs.reconstruct_batch_dev(dev, present, shard_len=S)
+    torch.cuda.synchronize()
+    out = dev.cpu().numpy()
+    assert np.array_equal(out[:, :, :S], host[:, :, :S])
+
+
+def test_roundtrip_full_size_83(gpu):
+    """Size-independent property at the benchmark size: encode -> erase every
+    single data shard in turn -> reconstruct == original (512 blocks would be
+    the bench batch; 64 keeps the test quick)."""
+    import torch
+    k, p, S, B = 8, 3, 524288, 64
+    g = torch.Generator(device=gpu)
+    g.manual_seed(99)
+    shards = torch.empty((B, k + p, S), dtype=torch.uint8, device=gpu)
+    shards[:, :k] = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=gpu, generator=g)
+    rs = shmr_amd.ReedSolomon(k, p)
+    rs.encode_batch_dev(shards[:, :k], shards[:, k:], shard_len=S, data_shard_pitch=S, parity_shard_pitch=S)
+    ref = shards.clone()
+    present = np.ones((B, k + p), np.uint8)
+    present[np.arange(B), np.arange(B) % k] = 0
+    present[np.arange(B), k + np.arange(B) % p] = 0
+    shards[torch.arange(B), torch.arange(B) % k] = 0
+    shards[torch.arange(B), k + torch.arange(B) % p] = 0
+    rs.reconstruct_batch_dev(shards, present, shard_len=S)
+    torch.cuda.synchronize()
+    assert torch.equal(shards, ref)
+    # checksum of checksums: parity of the batch vs a CPU oracle sample
+    hd = ref[:2].cpu().numpy()
+    for b in range(2):
+        par = oracle_parity(k, p, [hd[b, i].copy() for i in range(k)])
+        for r in range(p):
+            assert np.array_equal(hd[b, k + r], par[r])
+
+
+def test_encode_blocks_host_round_robin(gpu):
+    k, p, S, B = 8, 3, 100000, 5
+    rng = np.random.default_rng(5)
+    blocks = [[rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)] + [np.zeros(S, np.uint8) for _ in range(p)]
+              for _ in range(B)]
+    shmr_amd.ReedSolomon(k, p).encode_blocks_host(blocks, devices=[0])
+    for blk in blocks:
+        ref = oracle_parity(k, p, blk[:k])
+        for r in range(p):
+            assert np.array_equal(blk[k + r], ref[r])
+
+
+def test_sync_data_erasure_via_gpu(gpu):
+    """VirtualBlock::sync_data Erasure arm (block.rs:404-440) on a partial
+    buffer (700,001 B of a 1 MiB RS(4,2) block -> 3 data chunks + 1 zero
+    shard), arithmetic on the GPU, layout from the oracle's glue."""
+    size, k, p = 1 << 20, 4, 2
+    rng = np.random.default_rng(0)
+    buf = rng.integers(0, 256, 700001, dtype=np.uint8)
+    S = shmr_amd.calculate_shard_size(size, k)
+    shards = []
+    for off in range(0, len(buf), S):
+        c = np.zeros(S, np.uint8)
+        c[:len(buf[off:off + S])] = buf[off:off + S]
+        shards.append(c)
+    shards += [np.zeros(S, np.uint8) for _ in range(p + k - len(shards))]
+    shmr_amd.ReedSolomon(k, p).encode(shards)
+    ref = O.sync_data_erasure(buf.tobytes(), size, k, p)
+    for a, b in zip(shards, ref):
+        assert np.array_equal(a, b)
