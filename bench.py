@@ -54,9 +54,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="encode83", choices=sorted(CONFIGS))
     ap.add_argument("--blocks", type=int, default=0, help="blocks per GPU (default: 512 for 4 MiB, 64 for 16 MiB)")
-    ap.add_argument("--chunks", type=int, default=2, help="16-B chunks per lane per tile (1, 2, 4)")
-    ap.add_argument("--nt", type=int, default=0, help="nontemporal loads/stores")
-    ap.add_argument("--grid-cap", type=int, default=0)
+    ap.add_argument("--tune", default="", help="kernel knobs, e.g. 'chunks=2,grid=0' (default: library defaults)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the cpu_baseline sample")
     return ap.parse_args()
@@ -76,24 +74,31 @@ def main():
     k, p, block_bytes, erasures = CONFIGS[args.config]
     S = shmr_amd.calculate_shard_size(block_bytes, k)
     B = args.blocks or (512 if block_bytes <= (4 << 20) else 64)
-    shmr_amd.set_tuning(args.chunks, bool(args.nt), args.grid_cap)
+    for kv in filter(None, args.tune.split(",")):
+        key, val = kv.split("=")
+        shmr_amd.set_tuning(**{key: int(val)})
+    op = "encode" if erasures is None else "decode"
+    tuning = {key: shmr_amd.get_tuning(f"{op}.{key}")
+              for key in ("chunks", "nt_load", "nt_store", "scalar_tabs", "occ8", "grid")}
     rs = shmr_amd.ReedSolomon(k, p)
 
     # Synthetic blocks, generated on the GPU from a per-rank seed (inputs
-    # resident in HBM before timing).  Layout = the reference's block buffer:
-    # shard i of block b at b*k*S + i*S (S = 524,288 is 16-B aligned).
+    # resident in HBM before timing).  HBM layout: shard i of block b at
+    # (b*k + i) * pitch with pitch = S rounded up to 256 B -- for S = 524,288
+    # this IS the reference's block buffer (shards contiguous at i*S); for
+    # S = 1,677,722 (RS(10,4) 16 MiB) it is the 16-B aligned pitched layout.
+    pitch = (S + 255) // 256 * 256
     g = torch.Generator(device=dev)
     g.manual_seed(SEED + rank)
     if erasures is None:
-        data = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=dev, generator=g)
-        parity = torch.empty((B, p, S), dtype=torch.uint8, device=dev)
+        data = torch.randint(0, 256, (B, k, pitch), dtype=torch.uint8, device=dev, generator=g)
+        parity = torch.empty((B, p, pitch), dtype=torch.uint8, device=dev)
 
         def step():
             rs.encode_batch_dev(data, parity, shard_len=S)
         algo_bytes_per_block = (k + p) * S
         payload_bytes_per_block = k * S
     else:
-        pitch = (S + 255) // 256 * 256
         shards = torch.zeros((B, k + p, pitch), dtype=torch.uint8, device=dev)
         shards[:, :k, :S] = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=dev, generator=g)
         rs.encode_batch_dev(shards[:, :k], shards[:, k:], shard_len=S,
@@ -164,7 +169,7 @@ def main():
             "data_shards": k, "parity_shards": p, "shard_bytes": S, "blocks_per_gpu": B,
             "global_batch_blocks": B * world,
             "parallelism": f"blocks round-robin over {world} GPU(s), no collectives",
-            "tuning": {"chunks_per_lane": args.chunks, "nontemporal": bool(args.nt), "grid_cap": args.grid_cap},
+            "tuning": tuning,
         },
         "roofline": {
             "bound": "hbm",
@@ -205,14 +210,14 @@ def cpu_baseline(k, p, S, data_t, parity_t, budget_s):
     of the same workload; also checks the GPU parity of the sampled blocks."""
     from oracle import c_oracle   # cpu_baseline leg: oracle allowed here only
     cores = min(16, os.cpu_count() or 1)
-    nb = min(64, data_t.shape[0])
-    host_data = data_t[:nb].contiguous().cpu().numpy().reshape(-1)
+    nb = min(256, data_t.shape[0])     # 1 GiB of RS(8,3) data: larger than the host LLC
+    host_data = data_t[:nb, :, :S].contiguous().cpu().numpy().reshape(-1)
     host_par = np.zeros(nb * p * S, dtype=np.uint8)
     reps, secs = 0, 0.0
     while secs < budget_s or reps == 0:
         secs += c_oracle.encode_batch(k, p, host_data, host_par, nb, S, cores, variant=1)
         reps += 1
-    gpu_par = parity_t[:nb].contiguous().cpu().numpy().reshape(-1)
+    gpu_par = parity_t[:nb, :, :S].contiguous().cpu().numpy().reshape(-1)
     ok = bool(np.array_equal(gpu_par, host_par))
     gib = nb * k * S * reps / secs / 2 ** 30
     single = c_oracle.encode_batch(k, p, host_data[: k * S], host_par[: p * S], 1, S, 1, variant=1)

@@ -148,9 +148,15 @@ int shmr_ec_encode_blocks_host(shmr_ec_t* rs, uint8_t* const* host_shards, size_
 /* Device used by the host-buffer entry points (default 0). */
 int shmr_ec_set_device(shmr_ec_t* rs, int device);
 
-/* Kernel tuning knobs (process-wide): chunks of 16 B per lane per tile
- * (1, 2 or 4), nontemporal loads/stores (0/1), grid cap (0 = occupancy). */
-int shmr_ec_set_tuning(int chunks_per_lane, int nontemporal, int grid_cap);
+/* Kernel tuning knobs (process-wide).  key is one of "chunks" (16-B chunks
+ * per lane per tile: 1, 2, 4), "nt_load", "nt_store" (nontemporal 0/1),
+ * "scalar_tabs" (0/1), "occ8" (0/1), "grid" (-1 one workgroup per tile,
+ * 0 balanced persistent grid, >0 capped persistent grid), "diag" (0/1:
+ * XOR-only diagnostic kernel, WRONG results, for ceiling measurements).
+ * Prefix "encode." or "decode." to set one operation class only.  Defaults
+ * are the fastest variants measured on MI355X. */
+int shmr_ec_set_tuning(const char* key, int value);
+int shmr_ec_get_tuning(const char* key);
 
 /* Decode-matrix LRU statistics of the (data, parity) codec (crate cache
  * semantics, capacity 254). */

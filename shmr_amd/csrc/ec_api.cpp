@@ -15,6 +15,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -31,9 +32,38 @@ struct shmr_ec {
 
 namespace {
 
-std::atomic<int> g_chunks{2};
-std::atomic<int> g_nt{0};
-std::atomic<int> g_grid_cap{0};
+// Kernel tuning per operation class (encode / reconstruct), process-wide.
+// Defaults are the fastest variants measured on MI355X (DESIGN.md "Tuning").
+struct Tuning {
+    std::atomic<int> u{1};
+    std::atomic<int> nt_load{0};
+    std::atomic<int> nt_store{0};
+    std::atomic<int> scalar_tabs{0};
+    std::atomic<int> occ8{0};
+    std::atomic<int> grid{-1};     // -1: one workgroup per tile
+    std::atomic<int> diag{0};
+    shmr::kern::Variant variant() const {
+        shmr::kern::Variant v;
+        v.u = u.load();
+        v.nt_load = nt_load.load() != 0;
+        v.nt_store = nt_store.load() != 0;
+        v.scalar_tabs = scalar_tabs.load() != 0;
+        v.occ8 = occ8.load() != 0;
+        v.diag = diag.load() != 0;
+        return v;
+    }
+};
+Tuning g_tune[2];   // [0] encode, [1] reconstruct
+enum OpClass { kEncode = 0, kDecode = 1 };
+
+struct TuningInit {
+    TuningInit() {
+        g_tune[kEncode].nt_load = 1;
+        g_tune[kEncode].nt_store = 1;
+        g_tune[kDecode].nt_load = 1;
+        g_tune[kDecode].nt_store = 1;
+    }
+} g_tuning_init;
 
 #define HIP_TRY(expr)                                     \
     do {                                                  \
@@ -105,15 +135,17 @@ bool aligned16(uint64_t v) { return (v & 15u) == 0; }
 // Enqueues the plan over blocks {first + j * stride, j < nblk} on the current
 // device.  Rows are processed in groups of <= 4 per launch.
 int run_plan(Plan& plan, int dev, const Layout& L, uint64_t first, uint64_t stride, uint64_t nblk,
-             uint64_t len, hipStream_t stream) {
+             uint64_t len, hipStream_t stream, OpClass op) {
     if (nblk == 0 || plan.m == 0) return SHMR_EC_OK;
     const uint8_t* dplan = nullptr;
     uint32_t tab_off = 0;
     int rc = plan_on_device(plan, dev, &dplan, &tab_off);
     if (rc) return rc;
-    const int u = g_chunks.load();
-    const bool nt = g_nt.load() != 0;
-    const int cap = g_grid_cap.load();
+    const Tuning& T = g_tune[op];
+    const shmr::kern::Variant var = T.variant();
+    shmr::kern::Variant tail;   // tail / unaligned launches: U = 1, plain loads
+    const int u = var.u;
+    const int cap = T.grid.load();
     const bool aligned = aligned16(uintptr_t(L.in_base)) && aligned16(uintptr_t(L.out_base)) &&
                          aligned16(L.in_bpitch) && aligned16(L.in_spitch) && aligned16(L.out_bpitch) &&
                          aligned16(L.out_spitch);
@@ -139,10 +171,11 @@ int run_plan(Plan& plan, int dev, const Layout& L, uint64_t first, uint64_t stri
         a.plan = dplan;
         a.tab_off = tab_off;
         if (!aligned) {
+            const uint64_t tb1 = shmr::kern::tile_bytes(1);
             a.col_base = 0;
-            a.tiles_per_block = uint32_t((len + tb - 1) / tb);
+            a.tiles_per_block = uint32_t((len + tb1 - 1) / tb1);
             a.ntiles = nblk * a.tiles_per_block;
-            HIP_TRY(shmr::kern::launch_apply(a, rows, u, 2, false, cap, stream));
+            HIP_TRY(shmr::kern::launch_apply(a, rows, tail, 2, cap, stream));
             continue;
         }
         const uint64_t full = len / tb;
@@ -150,13 +183,17 @@ int run_plan(Plan& plan, int dev, const Layout& L, uint64_t first, uint64_t stri
             a.col_base = 0;
             a.tiles_per_block = uint32_t(full);
             a.ntiles = nblk * full;
-            HIP_TRY(shmr::kern::launch_apply(a, rows, u, 0, nt, cap, stream));
+            const hipError_t e = shmr::kern::launch_apply(a, rows, var, 0, cap, stream);
+            if (e == hipErrorInvalidValue) return SHMR_EC_INVALID_ARGUMENT;   // variant not compiled
+            if (e != hipSuccess) return SHMR_EC_DEVICE_ERROR;
         }
         if (len % tb) {
+            // remaining columns [full*tb, len): U = 1 tiles, the last one partial
+            const uint64_t tb1 = shmr::kern::tile_bytes(1);
             a.col_base = full * tb;
-            a.tiles_per_block = 1;
-            a.ntiles = nblk;
-            HIP_TRY(shmr::kern::launch_apply(a, rows, u, 1, false, cap, stream));
+            a.tiles_per_block = uint32_t((len - full * tb + tb1 - 1) / tb1);
+            a.ntiles = nblk * a.tiles_per_block;
+            HIP_TRY(shmr::kern::launch_apply(a, rows, tail, 1, cap, stream));
         }
     }
     return SHMR_EC_OK;
@@ -332,13 +369,61 @@ int shmr_ec_set_device(shmr_ec_t* rs, int device) {
     return SHMR_EC_OK;
 }
 
-int shmr_ec_set_tuning(int chunks_per_lane, int nontemporal, int grid_cap) {
-    if (chunks_per_lane != 1 && chunks_per_lane != 2 && chunks_per_lane != 4) return SHMR_EC_INVALID_ARGUMENT;
-    if (grid_cap < 0) return SHMR_EC_INVALID_ARGUMENT;
-    g_chunks = chunks_per_lane;
-    g_nt = nontemporal ? 1 : 0;
-    g_grid_cap = grid_cap;
+int shmr_ec_set_tuning(const char* key, int value) {
+    if (!key) return SHMR_EC_INVALID_ARGUMENT;
+    std::string k(key);
+    int first = 0, last = 1;
+    if (k.rfind("encode.", 0) == 0) {
+        first = last = kEncode;
+        k = k.substr(7);
+    } else if (k.rfind("decode.", 0) == 0) {
+        first = last = kDecode;
+        k = k.substr(7);
+    }
+    for (int i = first; i <= last; ++i) {
+        Tuning& T = g_tune[i];
+        if (k == "chunks") {
+            if (value != 1 && value != 2 && value != 4) return SHMR_EC_INVALID_ARGUMENT;
+            T.u = value;
+        } else if (k == "nt_load") {
+            T.nt_load = value != 0;
+        } else if (k == "nt_store") {
+            T.nt_store = value != 0;
+        } else if (k == "scalar_tabs") {
+            T.scalar_tabs = value != 0;
+        } else if (k == "occ8") {
+            T.occ8 = value != 0;
+        } else if (k == "grid") {
+            if (value < -1) return SHMR_EC_INVALID_ARGUMENT;
+            T.grid = value;
+        } else if (k == "diag") {
+            T.diag = value != 0;
+        } else {
+            return SHMR_EC_INVALID_ARGUMENT;
+        }
+    }
     return SHMR_EC_OK;
+}
+
+int shmr_ec_get_tuning(const char* key) {
+    if (!key) return SHMR_EC_INVALID_ARGUMENT;
+    std::string k(key);
+    int op = kEncode;
+    if (k.rfind("encode.", 0) == 0) {
+        k = k.substr(7);
+    } else if (k.rfind("decode.", 0) == 0) {
+        op = kDecode;
+        k = k.substr(7);
+    }
+    const Tuning& T = g_tune[op];
+    if (k == "chunks") return T.u;
+    if (k == "nt_load") return T.nt_load;
+    if (k == "nt_store") return T.nt_store;
+    if (k == "scalar_tabs") return T.scalar_tabs;
+    if (k == "occ8") return T.occ8;
+    if (k == "grid") return T.grid;
+    if (k == "diag") return T.diag;
+    return SHMR_EC_INVALID_ARGUMENT;
 }
 
 int shmr_ec_cache_stats(const shmr_ec_t* rs, uint64_t* hits, uint64_t* misses) {
@@ -377,7 +462,7 @@ int shmr_ec_encode(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_le
     for (unsigned i = 0; i < k; ++i)
         HIP_TRY(hipMemcpyAsync(s.dbuf + i * pitch, shards[i], len, hipMemcpyHostToDevice, s.stream));
     Layout L{s.dbuf, s.dbuf, 0, pitch, 0, pitch, 0};
-    rc = run_plan(*c.encode_plan(), dev, L, 0, 1, 1, len, s.stream);
+    rc = run_plan(*c.encode_plan(), dev, L, 0, 1, 1, len, s.stream, kEncode);
     if (rc) return rc;
     for (unsigned r = 0; r < p; ++r)
         HIP_TRY(hipMemcpyAsync(shards[k + r], s.dbuf + (k + r) * pitch, len, hipMemcpyDeviceToHost, s.stream));
@@ -430,7 +515,7 @@ int shmr_ec_reconstruct(shmr_ec_t* rs, uint8_t* const* shards, const size_t* sha
         HIP_TRY(hipMemcpyAsync(s.dbuf + idx * pitch, shards[idx], len, hipMemcpyHostToDevice, s.stream));
     }
     Layout L{s.dbuf, s.dbuf, 0, pitch, 0, pitch, 0};
-    rc = run_plan(*plan, dev, L, 0, 1, 1, len, s.stream);
+    rc = run_plan(*plan, dev, L, 0, 1, 1, len, s.stream, kDecode);
     if (rc) return rc;
     for (unsigned m = 0; m < plan->m; ++m) {
         const unsigned idx = plan->out_idx[m];
@@ -455,7 +540,7 @@ int shmr_ec_encode_batch_dev(shmr_ec_t* rs, const uint8_t* d_data, size_t data_s
     if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
     Codec& c = *rs->codec;
     Layout L{d_data, d_parity, data_block_pitch, data_shard_pitch, parity_block_pitch, parity_shard_pitch, c.k()};
-    return run_plan(*c.encode_plan(), device, L, 0, 1, nblocks, shard_len, static_cast<hipStream_t>(stream));
+    return run_plan(*c.encode_plan(), device, L, 0, 1, nblocks, shard_len, static_cast<hipStream_t>(stream), kEncode);
 }
 
 int shmr_ec_reconstruct_batch_dev(shmr_ec_t* rs, uint8_t* d_shards, size_t shard_pitch, size_t block_pitch,
@@ -499,7 +584,7 @@ int shmr_ec_reconstruct_batch_dev(shmr_ec_t* rs, uint8_t* d_shards, size_t shard
                 while (j + 1 < blks.size() && blks[j + 1] - blks[j] == stride) ++j;
                 ++j;
             }
-            rc = run_plan(*plan, device, L, blks[i], stride, j - i, shard_len, s);
+            rc = run_plan(*plan, device, L, blks[i], stride, j - i, shard_len, s, kDecode);
             if (rc) return rc;
             i = j;
         }
@@ -551,7 +636,7 @@ int shmr_ec_encode_blocks_host(shmr_ec_t* rs, uint8_t* const* host_shards, size_
                         return;
                     }
             Layout L{s.dbuf, s.dbuf, pitch * t, pitch, pitch * t, pitch, 0};
-            rc = run_plan(*c.encode_plan(), dev, L, 0, 1, n, shard_len, s.stream);
+            rc = run_plan(*c.encode_plan(), dev, L, 0, 1, n, shard_len, s.stream, kEncode);
             if (rc) {
                 results[di] = rc;
                 return;

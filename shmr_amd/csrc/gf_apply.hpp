@@ -37,11 +37,23 @@ struct ApplyArgs {
     uint32_t tab_off;        // byte offset of the PermTab array in the image
 };
 
+// Compiled-in kernel variant for full tiles (see gf_apply.hip dispatch_full).
+struct Variant {
+    int u = 1;               // 16-byte chunks per lane per shard (1, 2, 4)
+    bool nt_load = false;    // nontemporal loads
+    bool nt_store = false;   // nontemporal stores
+    bool scalar_tabs = false;// coefficient tables via scalar loads instead of LDS
+    bool occ8 = false;       // __launch_bounds__ for 8 waves / SIMD
+    bool diag = false;       // diagnostics: XOR-only (wrong results)
+};
+
 // rows in [1, kMaxRowsPerLaunch].  mode 0: full tiles, every shard base
-// (base + b*bpitch + idx*spitch) 16-byte aligned; mode 1: one partial tail
-// tile per block (aligned); mode 2: any alignment, byte-granular.
-// grid_cap <= 0: occupancy-sized grid.
-hipError_t launch_apply(const ApplyArgs& a, unsigned rows, int u, int mode, bool nt, int grid_cap,
+// (base + b*bpitch + idx*spitch) 16-byte aligned (variant v); mode 1: one
+// partial tail tile per block (aligned, U = 1); mode 2: any alignment,
+// byte-granular (U = 1; the variant only affects mode 0).
+// grid_cap: -1 one workgroup per tile; 0 balanced persistent grid sized by
+// occupancy; > 0 persistent grid capped at grid_cap.
+hipError_t launch_apply(const ApplyArgs& a, unsigned rows, const Variant& v, int mode, int grid_cap,
                         hipStream_t stream);
 
 }  // namespace kern

@@ -19,7 +19,7 @@ import numpy as np
 
 from ._native import _u8p, lib
 
-__all__ = ["Error", "ReedSolomon", "calculate_shard_size", "device_count", "set_tuning"]
+__all__ = ["Error", "ReedSolomon", "calculate_shard_size", "device_count", "set_tuning", "get_tuning"]
 
 
 class Error(Exception):
@@ -45,8 +45,14 @@ def device_count() -> int:
     return int(lib().shmr_ec_device_count())
 
 
-def set_tuning(chunks_per_lane: int = 2, nontemporal: bool = False, grid_cap: int = 0) -> None:
-    _check(lib().shmr_ec_set_tuning(chunks_per_lane, int(bool(nontemporal)), grid_cap))
+def set_tuning(**knobs) -> None:
+    """Kernel knobs, e.g. set_tuning(chunks=1, grid=-1) or set_tuning(**{"decode.nt_load": 1})."""
+    for key, value in knobs.items():
+        _check(lib().shmr_ec_set_tuning(key.encode(), int(value)))
+
+
+def get_tuning(key: str) -> int:
+    return int(lib().shmr_ec_get_tuning(key.encode()))
 
 
 def _writable_u8(buf) -> np.ndarray:

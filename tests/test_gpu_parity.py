@@ -129,9 +129,13 @@ def test_reconstruct_all_patterns_10_4(gpu):
 
 
 # --------------------------------------------------------------- device batch API
-def _dev_encode_check(gpu, k, p, L, B, chunks=2, nt=False, pitch=None):
+KNOBS = ("chunks", "nt_load", "nt_store", "scalar_tabs", "occ8", "grid")
+
+
+def _dev_encode_check(gpu, k, p, L, B, pitch=None, **knobs):
     import torch
-    shmr_amd.set_tuning(chunks, nt, 0)
+    saved = {f"encode.{kk}": shmr_amd.get_tuning(f"encode.{kk}") for kk in KNOBS}
+    shmr_amd.set_tuning(**{f"encode.{kk}": v for kk, v in knobs.items()})
     try:
         pitch = pitch or L
         g = torch.Generator(device=gpu)
@@ -147,7 +151,7 @@ def _dev_encode_check(gpu, k, p, L, B, chunks=2, nt=False, pitch=None):
                 assert np.array_equal(hp[b, r, :L], ref[r]), (b, r)
                 assert (hp[b, r, L:] == 0x5A).all(), "wrote past shard_len"
     finally:
-        shmr_amd.set_tuning(2, False, 0)
+        shmr_amd.set_tuning(**saved)
 
 
 @pytest.mark.parametrize("k,p,L,B", [(8, 3, 524288, 16), (4, 2, 262144, 8), (10, 4, 1677722, 3),
@@ -156,10 +160,63 @@ def test_encode_batch_dev(gpu, k, p, L, B):
     _dev_encode_check(gpu, k, p, L, B, pitch=(L + 255) // 256 * 256)
 
 
-@pytest.mark.parametrize("chunks,nt", [(1, False), (2, True), (4, False), (4, True)])
-def test_encode_batch_dev_tuning_variants(gpu, chunks, nt):
-    _dev_encode_check(gpu, 8, 3, 524288 + 4096 + 48, 4, chunks=chunks, nt=nt,
-                      pitch=524288 + 8192)
+BASE = dict(chunks=1, nt_load=0, nt_store=0, scalar_tabs=0, occ8=0, grid=-1)
+VARIANTS = [dict(BASE, **v) for v in (
+    {}, dict(nt_load=1), dict(nt_store=1), dict(nt_load=1, nt_store=1),
+    dict(scalar_tabs=1, nt_load=1, nt_store=1), dict(occ8=1, nt_load=1, nt_store=1),
+    dict(chunks=2), dict(chunks=2, nt_load=1, nt_store=1), dict(chunks=4, nt_load=1, nt_store=1),
+    dict(grid=0), dict(chunks=2, grid=0), dict(chunks=4, grid=7, nt_load=1, nt_store=1))]
+
+
+@pytest.mark.parametrize("knobs", VARIANTS, ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items() if BASE[k] != v) or "base")
+@pytest.mark.parametrize("k,p", [(8, 3), (5, 1), (10, 4), (7, 6)])
+def test_encode_batch_dev_tuning_variants(gpu, knobs, k, p):
+    _dev_encode_check(gpu, k, p, 524288 + 4096 + 48, 3, pitch=524288 + 8192, **knobs)
+
+
+def test_reconstruct_variants_match(gpu):
+    """Every decode variant produces identical bytes."""
+    import torch
+    k, p, S, B = 8, 3, 65536 * 3 + 4096 + 32, 6
+    pitch = (S + 255) // 256 * 256
+    rng = np.random.default_rng(4)
+    host = rng.integers(0, 256, (B, k + p, pitch), dtype=np.uint8)
+    for b in range(B):
+        par = oracle_parity(k, p, [host[b, i, :S].copy() for i in range(k)])
+        for r in range(p):
+            host[b, k + r, :S] = par[r]
+    present = np.ones((B, k + p), np.uint8)
+    for b in range(B):
+        present[b, [b % k, k + b % p]] = 0
+    rs = shmr_amd.ReedSolomon(k, p)
+    saved = {f"decode.{kk}": shmr_amd.get_tuning(f"decode.{kk}") for kk in KNOBS}
+    try:
+        for knobs in VARIANTS:
+            shmr_amd.set_tuning(**{f"decode.{kk}": v for kk, v in knobs.items()})
+            dev = torch.from_numpy(host.copy()).to(gpu)
+            for b in range(B):
+                for i in range(k + p):
+                    if not present[b, i]:
+                        dev[b, i, :S] = 0
+            rs.reconstruct_batch_dev(dev, present, shard_len=S)
+            torch.cuda.synchronize()
+            assert np.array_equal(dev.cpu().numpy()[:, :, :S], host[:, :, :S]), knobs
+    finally:
+        shmr_amd.set_tuning(**saved)
+
+
+def test_uncompiled_variant_is_reported(gpu):
+    import torch
+    saved = {f"encode.{kk}": shmr_amd.get_tuning(f"encode.{kk}") for kk in KNOBS}
+    try:
+        shmr_amd.set_tuning(**{"encode.chunks": 4, "encode.nt_load": 0, "encode.nt_store": 1, "encode.occ8": 1})
+        data = torch.zeros((1, 2, 65536), dtype=torch.uint8, device=gpu)
+        parity = torch.zeros((1, 1, 65536), dtype=torch.uint8, device=gpu)
+        with pytest.raises(shmr_amd.Error) as ei:
+            shmr_amd.ReedSolomon(2, 1).encode_batch_dev(data, parity)
+        assert ei.value.name == "InvalidArgument"
+    finally:
+        shmr_amd.set_tuning(**saved)
 
 
 def test_encode_batch_dev_unaligned_reference_layout(gpu):

@@ -1,0 +1,144 @@
+#!/usr/bin/env python3
+"""A/B kernel variants of the encode/decode path in ONE process, interleaved
+rounds (cdna_hip_programming.md rule 24).  Prints a table of median/min kernel
+times and the HBM roofline fraction of each variant.
+
+    python tools/tune.py --config encode83 --rounds 5
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+import shmr_amd  # noqa: E402
+
+CFG = {
+    "encode83": (8, 3, 4 << 20, 0, 512),
+    "decode83": (8, 3, 4 << 20, 1, 512),
+    "encode104": (10, 4, 16 << 20, 0, 64),
+    "decode104": (10, 4, 16 << 20, 2, 64),
+    "encode42": (4, 2, 1 << 20, 0, 1024),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="encode83")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--variants", default="chunks=1;nt_load=1;nt_store=1;nt_load=1,nt_store=1;"
+                    "scalar_tabs=1,nt_load=1,nt_store=1;occ8=1,nt_load=1,nt_store=1;chunks=2;"
+                    "chunks=2,nt_load=1,nt_store=1;chunks=4,nt_load=1,nt_store=1;grid=0;nt_load=1,nt_store=1,grid=0",
+                    help="';'-separated knob sets applied on top of the defaults (prefix-free keys)")
+    ap.add_argument("--json", default="")
+    ap.add_argument("--pad", type=int, default=0, help="extra bytes per shard pitch (de-alias 2^n strides)")
+    ap.add_argument("--diag", action="store_true", help="also time the XOR-only ceiling kernel")
+    ap.add_argument("--ref", action="store_true", help="also time torch copy / xor references")
+    a = ap.parse_args()
+    if a.config in CFG:
+        k, p, block, er, B = CFG[a.config]
+    else:  # "k,p,block_MiB,blocks"
+        kk, pp, mb, bb = a.config.split(",")
+        k, p, block, er, B = int(kk), int(pp), int(mb) << 20, 0, int(bb)
+    S = shmr_amd.calculate_shard_size(block, k)
+    dev = torch.device("cuda", 0)
+    rs = shmr_amd.ReedSolomon(k, p)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1)
+    if er == 0:
+        P = (S + 255) // 256 * 256 + a.pad
+        data = torch.randint(0, 256, (B, k, P), dtype=torch.uint8, device=dev, generator=g)
+        parity = torch.empty((B, p, P), dtype=torch.uint8, device=dev)
+        algo = B * (k + p) * S
+
+        def run():
+            rs.encode_batch_dev(data, parity, shard_len=S)
+    else:
+        pitch = (S + 255) // 256 * 256
+        shards = torch.zeros((B, k + p, pitch), dtype=torch.uint8, device=dev)
+        shards[:, :k, :S] = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=dev, generator=g)
+        present = np.ones((B, k + p), np.uint8)
+        b = np.arange(B)
+        if er == 1:
+            present[b, b % k] = 0
+        else:
+            present[b, b % 10] = 0
+            present[b, (b + 3) % 10] = 0
+        algo = B * (k + er) * S
+
+        def run():
+            rs.reconstruct_batch_dev(shards, present, shard_len=S)
+    base = {"chunks": 1, "nt_load": 0, "nt_store": 0, "scalar_tabs": 0, "occ8": 0, "grid": -1, "diag": 0}
+    variants = []
+    for spec in a.variants.split(";"):
+        kn = dict(base)
+        for kv in filter(None, spec.split(",")):
+            kk, vv = kv.split("=")
+            kn[kk] = int(vv)
+        variants.append(tuple(sorted(kn.items())))
+    if a.diag:
+        variants.append(tuple(sorted(dict(base, diag=1).items())))
+        variants.append(tuple(sorted(dict(base, diag=1, nt_load=1, nt_store=1).items())))
+    times = {v: [] for v in variants}
+    st = torch.cuda.current_stream()
+    for rnd in range(a.rounds):
+        for v in variants:
+            shmr_amd.set_tuning(**dict(v))
+            run()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(a.iters):
+                run()
+            e1.record(st)
+            torch.cuda.synchronize()
+            times[v].append(e0.elapsed_time(e1) / a.iters)
+    rows = []
+    if a.ref:
+        n = 2 << 30
+        src = torch.randint(0, 256, (n,), dtype=torch.uint8, device=dev)
+        dst = torch.empty_like(src)
+        x2 = src.view(torch.int64)
+        o2 = dst.view(torch.int64)[: x2.numel() // 2]
+        refs = {"copy_2GiB": (lambda: dst.copy_(src), 2 * n),
+                "xor_2in_1out_1GiB": (lambda: torch.bitwise_xor(x2[: x2.numel() // 2], x2[x2.numel() // 2:], out=o2), 1.5 * n)}
+        for name, (fn, nbytes) in refs.items():
+            fn()
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(a.rounds):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                for _ in range(a.iters):
+                    fn()
+                e1.record(st)
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1) / a.iters)
+            med = float(np.median(ts))
+            print(json.dumps({"ref": name, "median_ms": round(med, 4), "TBps": round(nbytes / med / 1e9, 3),
+                              "frac": round(nbytes / (med / 1e3) / 8e12, 4)}))
+        del src, dst
+    for v in variants:
+        med, mn = float(np.median(times[v])), float(np.min(times[v]))
+        rows.append({"knobs": {kk: vv for kk, vv in v if vv != base.get(kk)}, "median_ms": round(med, 4),
+                     "min_ms": round(mn, 4), "TBps": round(algo / med / 1e9, 3),
+                     "frac": round(algo / (med / 1e3) / 8e12, 4)})
+    rows.sort(key=lambda r: r["median_ms"])
+    print(f"config={a.config} k={k} p={p} S={S} B={B} algo_bytes={algo}")
+    for r in rows:
+        print(json.dumps(r))
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump({"config": a.config, "rows": rows}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
