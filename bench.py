@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--tune", default="", help="kernel knobs, e.g. 'chunks=2,grid=0' (default: library defaults)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the cpu_baseline sample")
+    ap.add_argument("--ramp-seconds", type=float, default=0.5,
+                    help="untimed device clock ramp before the warmup steps (MI355X needs ~0.1 s of "
+                         "sustained load to reach its steady clock)")
     return ap.parse_args()
 
 
@@ -78,8 +81,8 @@ def main():
         key, val = kv.split("=")
         shmr_amd.set_tuning(**{key: int(val)})
     op = "encode" if erasures is None else "decode"
-    tuning = {key: shmr_amd.get_tuning(f"{op}.{key}")
-              for key in ("chunks", "nt_load", "nt_store", "scalar_tabs", "occ8", "grid")}
+    rows = p if erasures is None else erasures
+    tuning = shmr_amd.describe_variant(op == "decode", k, rows)
     rs = shmr_amd.ReedSolomon(k, p)
 
     # Synthetic blocks, generated on the GPU from a per-rank seed (inputs
@@ -118,6 +121,15 @@ def main():
     torch.cuda.synchronize(dev)
 
     stream = torch.cuda.current_stream(dev)
+    # Untimed clock ramp: run the same step until ramp_seconds of wall time
+    # have passed (measured: with only 5 warmup steps, ~2 ms of work, the
+    # first timed steps run 10-15 % slow while the GPU clock ramps up).
+    ramp_steps, t_ramp = 0, time.perf_counter()
+    while time.perf_counter() - t_ramp < args.ramp_seconds:
+        for _ in range(8):
+            step()
+        ramp_steps += 8
+        torch.cuda.synchronize(dev)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -154,6 +166,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "clock_ramp": {"seconds": args.ramp_seconds, "steps": ramp_steps},
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",

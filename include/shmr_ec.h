@@ -151,12 +151,19 @@ int shmr_ec_set_device(shmr_ec_t* rs, int device);
 /* Kernel tuning knobs (process-wide).  key is one of "chunks" (16-B chunks
  * per lane per tile: 1, 2, 4), "nt_load", "nt_store" (nontemporal 0/1),
  * "scalar_tabs" (0/1), "occ8" (0/1), "grid" (-1 one workgroup per tile,
- * 0 balanced persistent grid, >0 capped persistent grid), "diag" (0/1:
+ * 0 balanced persistent grid, >0 capped persistent grid), "threads" (lanes
+ * per workgroup: 128, 256, 512), "diag" (0/1:
  * XOR-only diagnostic kernel, WRONG results, for ceiling measurements).
- * Prefix "encode." or "decode." to set one operation class only.  Defaults
- * are the fastest variants measured on MI355X. */
+ * Prefix "encode." or "decode." to set one operation class only.
+ * "chunks", "nt_load" and "nt_store" default to -2 (auto): a per-shape policy
+ * of the fastest variants measured on MI355X; any other value pins the knob,
+ * and setting -2 returns it to the policy. */
 int shmr_ec_set_tuning(const char* key, int value);
 int shmr_ec_get_tuning(const char* key);
+
+/* Writes the kernel variant that a launch of `rows` output rows over
+ * `data_shards` inputs would use (encode: decode=0, reconstruct: decode=1). */
+int shmr_ec_describe_variant(int decode, uint32_t data_shards, uint32_t rows, char* buf, size_t len);
 
 /* Decode-matrix LRU statistics of the (data, parity) codec (crate cache
  * semantics, capacity 254). */

@@ -50,6 +50,7 @@ SIGNATURES = [
     ("shmr_ec_set_device", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("shmr_ec_set_tuning", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
     ("shmr_ec_get_tuning", ctypes.c_int, [ctypes.c_char_p]),
+    ("shmr_ec_describe_variant", ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p, _sz]),
     ("shmr_ec_cache_stats", ctypes.c_int,
      [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     ("shmr_ec_device_count", ctypes.c_int, []),

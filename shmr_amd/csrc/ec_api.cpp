@@ -11,6 +11,7 @@
 #include <atomic>
 #include <cmath>
 #include <condition_variable>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -33,37 +34,46 @@ struct shmr_ec {
 namespace {
 
 // Kernel tuning per operation class (encode / reconstruct), process-wide.
-// Defaults are the fastest variants measured on MI355X (DESIGN.md "Tuning").
+// kAuto knobs follow variant_policy(), the fastest variants measured on MI355X
+// per launch shape (DESIGN.md "Tuning"); set_tuning() pins a knob explicitly.
+constexpr int kAuto = -2;
 struct Tuning {
-    std::atomic<int> u{1};
-    std::atomic<int> nt_load{0};
-    std::atomic<int> nt_store{0};
+    std::atomic<int> u{kAuto};
+    std::atomic<int> nt_load{kAuto};
+    std::atomic<int> nt_store{kAuto};
     std::atomic<int> scalar_tabs{0};
     std::atomic<int> occ8{0};
     std::atomic<int> grid{-1};     // -1: one workgroup per tile
     std::atomic<int> diag{0};
-    shmr::kern::Variant variant() const {
-        shmr::kern::Variant v;
-        v.u = u.load();
-        v.nt_load = nt_load.load() != 0;
-        v.nt_store = nt_store.load() != 0;
-        v.scalar_tabs = scalar_tabs.load() != 0;
-        v.occ8 = occ8.load() != 0;
-        v.diag = diag.load() != 0;
-        return v;
-    }
+    std::atomic<int> threads{256};
 };
 Tuning g_tune[2];   // [0] encode, [1] reconstruct
 enum OpClass { kEncode = 0, kDecode = 1 };
 
-struct TuningInit {
-    TuningInit() {
-        g_tune[kEncode].nt_load = 1;
-        g_tune[kEncode].nt_store = 1;
-        g_tune[kDecode].nt_load = 1;
-        g_tune[kDecode].nt_store = 1;
-    }
-} g_tuning_init;
+// Measured (tools/tune.py, interleaved A/B in one process, MI355X):
+//  encode RS(8,3): NT loads+stores, U=1 (78 %); RS(4,2): NT stores only (77 %
+//  vs 72 % with NT loads); RS(10,4) (4 rows per launch): U=2 (71 % vs 66 %);
+//  reconstruct: NT loads+stores, U=1.
+shmr::kern::Variant variant_policy(OpClass op, unsigned k, unsigned rows) {
+    shmr::kern::Variant v;
+    v.u = (op == kEncode && rows >= 4) ? 2 : 1;
+    v.nt_store = true;
+    v.nt_load = op == kDecode || k >= 8;
+    return v;
+}
+
+shmr::kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows) {
+    const Tuning& T = g_tune[op];
+    shmr::kern::Variant v = variant_policy(op, k, rows);
+    if (T.u.load() != kAuto) v.u = T.u.load();
+    if (T.nt_load.load() != kAuto) v.nt_load = T.nt_load.load() != 0;
+    if (T.nt_store.load() != kAuto) v.nt_store = T.nt_store.load() != 0;
+    v.scalar_tabs = T.scalar_tabs.load() != 0;
+    v.occ8 = T.occ8.load() != 0;
+    v.diag = T.diag.load() != 0;
+    v.threads = T.threads.load();
+    return v;
+}
 
 #define HIP_TRY(expr)                                     \
     do {                                                  \
@@ -134,24 +144,45 @@ bool aligned16(uint64_t v) { return (v & 15u) == 0; }
 
 // Enqueues the plan over blocks {first + j * stride, j < nblk} on the current
 // device.  Rows are processed in groups of <= 4 per launch.
-int run_plan(Plan& plan, int dev, const Layout& L, uint64_t first, uint64_t stride, uint64_t nblk,
-             uint64_t len, hipStream_t stream, OpClass op) {
+// Blocks covered by one launch set: {first + j * stride} or, with d_list, the
+// device list d_list[j]; multi-plan sets also carry a per-block plan index into
+// the device table d_plans (all plans share k and m).
+struct BlockSet {
+    uint64_t first = 0, stride = 1, n = 0;
+    const uint32_t* d_list = nullptr;
+    const uint16_t* d_plan_idx = nullptr;
+    const uint8_t* const* d_plans = nullptr;
+};
+
+uint32_t plan_tab_off(unsigned k, unsigned m) {
+    return uint32_t((8 + 2 * size_t(k) + 2 * size_t(m) + 31) & ~size_t(31));
+}
+
+// Enqueues out = rows (x) in for a block set on the current device.  `shape`
+// supplies k and m (and the device image for single-plan sets); rows are
+// processed in groups of <= 4 per launch.
+int launch_set(Plan& shape, int dev, const Layout& L, const BlockSet& bs, uint64_t len, hipStream_t stream,
+               OpClass op) {
+    const uint64_t nblk = bs.n;
+    Plan& plan = shape;
     if (nblk == 0 || plan.m == 0) return SHMR_EC_OK;
     const uint8_t* dplan = nullptr;
-    uint32_t tab_off = 0;
-    int rc = plan_on_device(plan, dev, &dplan, &tab_off);
-    if (rc) return rc;
+    const uint32_t tab_off = plan_tab_off(plan.k, plan.m);
+    if (!bs.d_plans) {
+        uint32_t off = 0;
+        int rc = plan_on_device(plan, dev, &dplan, &off);
+        if (rc) return rc;
+    }
     const Tuning& T = g_tune[op];
-    const shmr::kern::Variant var = T.variant();
     shmr::kern::Variant tail;   // tail / unaligned launches: U = 1, plain loads
-    const int u = var.u;
     const int cap = T.grid.load();
     const bool aligned = aligned16(uintptr_t(L.in_base)) && aligned16(uintptr_t(L.out_base)) &&
                          aligned16(L.in_bpitch) && aligned16(L.in_spitch) && aligned16(L.out_bpitch) &&
                          aligned16(L.out_spitch);
-    const uint64_t tb = shmr::kern::tile_bytes(u);
     for (uint32_t row0 = 0; row0 < plan.m; row0 += shmr::kern::kMaxRowsPerLaunch) {
         const uint32_t rows = std::min<uint32_t>(shmr::kern::kMaxRowsPerLaunch, plan.m - row0);
+        const shmr::kern::Variant var = resolve_variant(op, plan.k, rows);
+        const uint64_t tb = shmr::kern::tile_bytes(var.u, var.threads);
         shmr::kern::ApplyArgs a{};
         a.in_base = L.in_base;
         a.out_base = L.out_base;
@@ -160,10 +191,12 @@ int run_plan(Plan& plan, int dev, const Layout& L, uint64_t first, uint64_t stri
         a.out_bpitch = L.out_bpitch;
         a.out_spitch = L.out_spitch;
         a.out_bias = L.out_bias;
-        a.blk_list = nullptr;
-        a.blk_first = first;
-        a.blk_stride = stride;
+        a.blk_list = bs.d_list;
+        a.blk_first = bs.first;
+        a.blk_stride = bs.stride;
         a.nblk = nblk;
+        a.plan_table = bs.d_plans;
+        a.blk_plan = bs.d_plan_idx;
         a.len = len;
         a.k = plan.k;
         a.m = plan.m;
@@ -198,6 +231,106 @@ int run_plan(Plan& plan, int dev, const Layout& L, uint64_t first, uint64_t stri
     }
     return SHMR_EC_OK;
 }
+
+int run_plan(Plan& plan, int dev, const Layout& L, uint64_t first, uint64_t stride, uint64_t nblk,
+             uint64_t len, hipStream_t stream, OpClass op) {
+    BlockSet bs;
+    bs.first = first;
+    bs.stride = stride;
+    bs.n = nblk;
+    return launch_set(plan, dev, L, bs, len, stream, op);
+}
+
+// ---------------------------------------------------------------------------
+// Per-device ring of pinned upload slots for small per-call tables (block
+// lists, per-block plan indices, plan pointer tables).  A slot is reused only
+// after the event recorded behind the kernels that read it has completed.
+// ---------------------------------------------------------------------------
+class UploadRing {
+public:
+    static constexpr int kSlots = 32;
+    static constexpr size_t kSlotBytes = 256 * 1024;
+
+    static UploadRing* for_device(int dev, int* rc) {
+        static std::mutex mu;
+        static auto* rings = new std::map<int, UploadRing*>;   // leaked: outlives static teardown
+        std::lock_guard<std::mutex> lock(mu);
+        auto& r = (*rings)[dev];
+        if (!r) {
+            auto* ring = new UploadRing;
+            if (hipHostMalloc(reinterpret_cast<void**>(&ring->host_), kSlots * kSlotBytes, hipHostMallocDefault) !=
+                    hipSuccess ||
+                hipMalloc(reinterpret_cast<void**>(&ring->dev_), kSlots * kSlotBytes) != hipSuccess) {
+                *rc = SHMR_EC_OUT_OF_MEMORY;
+                return nullptr;
+            }
+            for (int i = 0; i < kSlots; ++i) {
+                if (hipEventCreateWithFlags(&ring->ev_[i], hipEventDisableTiming) != hipSuccess) {
+                    *rc = SHMR_EC_DEVICE_ERROR;
+                    return nullptr;
+                }
+            }
+            r = ring;
+        }
+        *rc = SHMR_EC_OK;
+        return r;
+    }
+
+    // Claims a slot; *host/*dev point at its kSlotBytes of pinned / device memory.
+    int acquire(uint8_t** host, uint8_t** dev, int* slot) {
+        std::unique_lock<std::mutex> lock(mu_);
+        for (;;) {
+            for (int n = 0; n < kSlots; ++n) {
+                const int i = (next_ + n) % kSlots;
+                if (inuse_[i]) continue;
+                inuse_[i] = true;
+                next_ = (i + 1) % kSlots;
+                const bool armed = armed_[i];
+                lock.unlock();
+                if (armed && hipEventSynchronize(ev_[i]) != hipSuccess) {
+                    release_now(i);
+                    return SHMR_EC_DEVICE_ERROR;
+                }
+                *host = host_ + size_t(i) * kSlotBytes;
+                *dev = dev_ + size_t(i) * kSlotBytes;
+                *slot = i;
+                return SHMR_EC_OK;
+            }
+            cv_.wait(lock);
+        }
+    }
+    // Copies the first `bytes` of the slot to the device on `stream`.
+    int upload(int slot, size_t bytes, hipStream_t stream) {
+        const size_t off = size_t(slot) * kSlotBytes;
+        return hipMemcpyAsync(dev_ + off, host_ + off, bytes, hipMemcpyHostToDevice, stream) == hipSuccess
+                   ? SHMR_EC_OK
+                   : SHMR_EC_DEVICE_ERROR;
+    }
+    // Releases the slot once all work enqueued on `stream` so far has finished.
+    int release_after(int slot, hipStream_t stream) {
+        const bool ok = hipEventRecord(ev_[slot], stream) == hipSuccess;
+        std::lock_guard<std::mutex> lock(mu_);
+        armed_[slot] = ok;
+        inuse_[slot] = false;
+        cv_.notify_one();
+        return ok ? SHMR_EC_OK : SHMR_EC_DEVICE_ERROR;
+    }
+
+private:
+    void release_now(int slot) {
+        std::lock_guard<std::mutex> lock(mu_);
+        inuse_[slot] = false;
+        cv_.notify_one();
+    }
+    uint8_t* host_ = nullptr;
+    uint8_t* dev_ = nullptr;
+    hipEvent_t ev_[kSlots] = {};
+    bool armed_[kSlots] = {};
+    bool inuse_[kSlots] = {};
+    int next_ = 0;
+    std::mutex mu_;
+    std::condition_variable cv_;
+};
 
 // ---------------------------------------------------------------------------
 // Device staging for the host-buffer entry points.
@@ -383,12 +516,12 @@ int shmr_ec_set_tuning(const char* key, int value) {
     for (int i = first; i <= last; ++i) {
         Tuning& T = g_tune[i];
         if (k == "chunks") {
-            if (value != 1 && value != 2 && value != 4) return SHMR_EC_INVALID_ARGUMENT;
+            if (value != 1 && value != 2 && value != 4 && value != kAuto) return SHMR_EC_INVALID_ARGUMENT;
             T.u = value;
         } else if (k == "nt_load") {
-            T.nt_load = value != 0;
+            T.nt_load = value == kAuto ? kAuto : (value != 0);
         } else if (k == "nt_store") {
-            T.nt_store = value != 0;
+            T.nt_store = value == kAuto ? kAuto : (value != 0);
         } else if (k == "scalar_tabs") {
             T.scalar_tabs = value != 0;
         } else if (k == "occ8") {
@@ -398,6 +531,9 @@ int shmr_ec_set_tuning(const char* key, int value) {
             T.grid = value;
         } else if (k == "diag") {
             T.diag = value != 0;
+        } else if (k == "threads") {
+            if (value != 128 && value != 256 && value != 512) return SHMR_EC_INVALID_ARGUMENT;
+            T.threads = value;
         } else {
             return SHMR_EC_INVALID_ARGUMENT;
         }
@@ -423,7 +559,18 @@ int shmr_ec_get_tuning(const char* key) {
     if (k == "occ8") return T.occ8;
     if (k == "grid") return T.grid;
     if (k == "diag") return T.diag;
+    if (k == "threads") return T.threads;
     return SHMR_EC_INVALID_ARGUMENT;
+}
+
+int shmr_ec_describe_variant(int decode, uint32_t data_shards, uint32_t rows, char* buf, size_t len) {
+    if (!buf || len == 0 || rows == 0) return SHMR_EC_INVALID_ARGUMENT;
+    const OpClass op = decode ? kDecode : kEncode;
+    const shmr::kern::Variant v = resolve_variant(op, data_shards, std::min<uint32_t>(rows, shmr::kern::kMaxRowsPerLaunch));
+    std::snprintf(buf, len, "chunks=%d nt_load=%d nt_store=%d scalar_tabs=%d occ8=%d threads=%d grid=%d diag=%d", v.u,
+                  int(v.nt_load), int(v.nt_store), int(v.scalar_tabs), int(v.occ8), v.threads,
+                  g_tune[op].grid.load(), int(v.diag));
+    return SHMR_EC_OK;
 }
 
 int shmr_ec_cache_stats(const shmr_ec_t* rs, uint64_t* hits, uint64_t* misses) {
@@ -571,22 +718,72 @@ int shmr_ec_reconstruct_batch_dev(shmr_ec_t* rs, uint8_t* d_shards, size_t shard
     if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
     Layout L{d_shards, d_shards, block_pitch, shard_pitch, block_pitch, shard_pitch, 0};
     hipStream_t s = static_cast<hipStream_t>(stream);
+    // Plans with the same number of rebuilt shards share one multi-plan launch
+    // set: the kernel picks each block's plan from a device table, so a batch
+    // with many erasure patterns is still one launch (plus a tail launch).
+    struct Group {
+        std::vector<std::shared_ptr<Plan>> plans;
+        std::vector<uint32_t> blocks;
+        std::vector<uint16_t> plan_idx;
+    };
+    std::map<unsigned, Group> by_m;
     for (auto& g : groups) {
         auto plan = c.reconstruct_plan(g.first, data_only != 0);
-        const auto& blks = g.second;
-        // split the group into arithmetic runs -> one launch set per run
-        size_t i = 0;
-        while (i < blks.size()) {
-            size_t j = i + 1;
-            uint64_t stride = 1;
-            if (j < blks.size()) {
-                stride = blks[j] - blks[i];
-                while (j + 1 < blks.size() && blks[j + 1] - blks[j] == stride) ++j;
-                ++j;
-            }
-            rc = run_plan(*plan, device, L, blks[i], stride, j - i, shard_len, s, kDecode);
+        if (plan->m == 0) continue;
+        Group& grp = by_m[plan->m];
+        const uint16_t pi = uint16_t(grp.plans.size());
+        grp.plans.push_back(plan);
+        for (uint64_t b : g.second) {
+            grp.blocks.push_back(uint32_t(b));
+            grp.plan_idx.push_back(pi);
+        }
+    }
+    for (auto& kv : by_m) {
+        Group& grp = kv.second;
+        // A single pattern over an arithmetic block sequence needs no upload.
+        bool arith = grp.plans.size() == 1;
+        const uint64_t stride = grp.blocks.size() > 1 ? uint64_t(grp.blocks[1]) - grp.blocks[0] : 1;
+        for (size_t i = 1; arith && i < grp.blocks.size(); ++i)
+            arith = uint64_t(grp.blocks[i]) - grp.blocks[i - 1] == stride;
+        if (arith) {
+            rc = run_plan(*grp.plans[0], device, L, grp.blocks[0], stride, grp.blocks.size(), shard_len, s, kDecode);
             if (rc) return rc;
-            i = j;
+            continue;
+        }
+        if (grp.plans.size() > 65535) return SHMR_EC_INVALID_ARGUMENT;
+        std::vector<const uint8_t*> dplans(grp.plans.size());
+        for (size_t i = 0; i < grp.plans.size(); ++i) {
+            uint32_t off = 0;
+            rc = plan_on_device(*grp.plans[i], device, &dplans[i], &off);
+            if (rc) return rc;
+        }
+        UploadRing* ring = UploadRing::for_device(device, &rc);
+        if (!ring) return rc;
+        const size_t table_bytes = (dplans.size() * sizeof(void*) + 15) & ~size_t(15);
+        if (table_bytes + 64 > UploadRing::kSlotBytes) return SHMR_EC_INVALID_ARGUMENT;
+        const size_t per_chunk = (UploadRing::kSlotBytes - table_bytes - 32) / (sizeof(uint32_t) + sizeof(uint16_t));
+        for (size_t c0 = 0; c0 < grp.blocks.size(); c0 += per_chunk) {
+            const size_t n = std::min(per_chunk, grp.blocks.size() - c0);
+            uint8_t *hslot = nullptr, *dslot = nullptr;
+            int slot = -1;
+            rc = ring->acquire(&hslot, &dslot, &slot);
+            if (rc) return rc;
+            const size_t list_off = table_bytes;
+            const size_t pidx_off = (list_off + n * sizeof(uint32_t) + 15) & ~size_t(15);
+            const size_t total = pidx_off + n * sizeof(uint16_t);
+            std::memcpy(hslot, dplans.data(), dplans.size() * sizeof(void*));
+            std::memcpy(hslot + list_off, grp.blocks.data() + c0, n * sizeof(uint32_t));
+            std::memcpy(hslot + pidx_off, grp.plan_idx.data() + c0, n * sizeof(uint16_t));
+            rc = ring->upload(slot, total, s);
+            BlockSet bs;
+            bs.n = n;
+            bs.d_plans = reinterpret_cast<const uint8_t* const*>(dslot);
+            bs.d_list = reinterpret_cast<const uint32_t*>(dslot + list_off);
+            bs.d_plan_idx = reinterpret_cast<const uint16_t*>(dslot + pidx_off);
+            if (rc == SHMR_EC_OK) rc = launch_set(*grp.plans[0], device, L, bs, shard_len, s, kDecode);
+            const int rc2 = ring->release_after(slot, s);
+            if (rc) return rc;
+            if (rc2) return rc2;
         }
     }
     return SHMR_EC_OK;

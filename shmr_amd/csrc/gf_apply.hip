@@ -41,6 +41,13 @@ constexpr int kNtStore = 2;      // nontemporal stores
 constexpr int kScalarTabs = 4;   // tables/offsets via scalar loads, no LDS staging
 constexpr int kOcc8 = 8;         // ask for 8 waves / SIMD (<= 64 VGPRs)
 constexpr int kDiagXor = 16;     // diagnostics: XOR without GF multiply (wrong results)
+constexpr int kTh128 = 32;       // 128-lane workgroups (default 256)
+constexpr int kTh512 = 64;       // 512-lane workgroups
+
+template <int F>
+constexpr int threads_of() {
+    return (F & kTh128) ? 128 : (F & kTh512) ? 512 : kThreads;
+}
 
 struct Tab {
     uint32_t t0lo, t0hi, t1lo, t1hi, t2;
@@ -184,6 +191,7 @@ __device__ __forceinline__ uint64_t out_off(const ApplyArgs& a, const Ctx& c, ui
 template <int R, int U, int MODE, int F>
 __device__ __forceinline__ void do_tile(const ApplyArgs& a, const Ctx& c, const uint8_t* ib, uint8_t* ob,
                                         uint64_t col0) {
+    constexpr int TH = threads_of<F>();
     const uint32_t k = a.k;
     const uint64_t len = a.len;
     const uint32_t tid = threadIdx.x;
@@ -199,7 +207,7 @@ __device__ __forceinline__ void do_tile(const ApplyArgs& a, const Ctx& c, const 
         const uint32_t tt = t < k ? t : k - 1;
         const uint8_t* base = ib + in_off<F>(a, c, tt);
 #pragma unroll
-        for (int u = 0; u < U; ++u) buf[u] = ld<MODE, F>(base, col0 + (uint64_t(u) * kThreads + tid) * 16, len);
+        for (int u = 0; u < U; ++u) buf[u] = ld<MODE, F>(base, col0 + (uint64_t(u) * TH + tid) * 16, len);
     };
     auto consume = [&](const u32x4 (&buf)[U], uint32_t t) {
         Tab tb[R];
@@ -234,47 +242,74 @@ __device__ __forceinline__ void do_tile(const ApplyArgs& a, const Ctx& c, const 
         uint8_t* o = ob + out_off<F>(a, c, r);
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            st<MODE, F>(o, col0 + (uint64_t(u) * kThreads + tid) * 16, len,
+            st<MODE, F>(o, col0 + (uint64_t(u) * TH + tid) * 16, len,
                         u32x4{acc[u][r][0], acc[u][r][1], acc[u][r][2], acc[u][r][3]});
     }
 }
 
-template <int R, int U, int MODE, int F>
-__global__ __launch_bounds__(kThreads, (F & kOcc8) ? 8 : 1) void gf_apply_kernel(const ApplyArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+// Stages rows [row0, row0 + R) of a plan image into LDS:
+// [tables k*R*32 B][in_off k*8 B][out_off R*8 B].
+template <int R, int TH>
+__device__ __forceinline__ void stage_plan(const ApplyArgs& a, const uint8_t* plan, uint8_t* smem, Ctx& c) {
     const uint32_t k = a.k;
-    Ctx c{};
-    c.g_in_idx = reinterpret_cast<const uint16_t*>(a.plan + 8);
+    c.g_in_idx = reinterpret_cast<const uint16_t*>(plan + 8);
     c.g_out_idx = c.g_in_idx + k;
-    c.g_tab = reinterpret_cast<const uint32_t*>(a.plan + a.tab_off);
-    if constexpr ((F & kScalarTabs) == 0) {
-        // LDS carve: [tables k*R*32 B][in_off k*8 B][out_off R*8 B].  Stage this
-        // launch's rows [row0, row0 + R) of the plan image.
-        u32x4* s_tab = reinterpret_cast<u32x4*>(smem);
-        uint64_t* s_in_off = reinterpret_cast<uint64_t*>(smem + size_t(k) * R * 32);
-        uint64_t* s_out_off = s_in_off + k;
-        const u32x4* ptab = reinterpret_cast<const u32x4*>(a.plan + a.tab_off);
-        const uint32_t n16 = k * R * 2;   // u32x4 count
-        for (uint32_t i = threadIdx.x; i < n16; i += kThreads) {
-            const uint32_t e = i >> 1, half = i & 1;
-            const uint32_t t = e / R, r = e - t * R;
-            s_tab[i] = ptab[(size_t(t) * a.m + a.row0 + r) * 2 + half];
-        }
-        for (uint32_t t = threadIdx.x; t < k; t += kThreads) s_in_off[t] = uint64_t(c.g_in_idx[t]) * a.in_spitch;
-        for (uint32_t r = threadIdx.x; r < uint32_t(R); r += kThreads)
-            s_out_off[r] = uint64_t(c.g_out_idx[a.row0 + r] - a.out_bias) * a.out_spitch;
-        c.s_tab = s_tab;
-        c.s_in_off = s_in_off;
-        c.s_out_off = s_out_off;
-        __syncthreads();
+    c.g_tab = reinterpret_cast<const uint32_t*>(plan + a.tab_off);
+    u32x4* s_tab = reinterpret_cast<u32x4*>(smem);
+    uint64_t* s_in_off = reinterpret_cast<uint64_t*>(smem + size_t(k) * R * 32);
+    uint64_t* s_out_off = s_in_off + k;
+    const u32x4* ptab = reinterpret_cast<const u32x4*>(plan + a.tab_off);
+    const uint32_t n16 = k * R * 2;   // u32x4 count
+    for (uint32_t i = threadIdx.x; i < n16; i += TH) {
+        const uint32_t e = i >> 1, half = i & 1;
+        const uint32_t t = e / R, r = e - t * R;
+        s_tab[i] = ptab[(size_t(t) * a.m + a.row0 + r) * 2 + half];
     }
+    for (uint32_t t = threadIdx.x; t < k; t += TH) s_in_off[t] = uint64_t(c.g_in_idx[t]) * a.in_spitch;
+    for (uint32_t r = threadIdx.x; r < uint32_t(R); r += TH)
+        s_out_off[r] = uint64_t(c.g_out_idx[a.row0 + r] - a.out_bias) * a.out_spitch;
+    c.s_tab = s_tab;
+    c.s_in_off = s_in_off;
+    c.s_out_off = s_out_off;
+}
 
+template <int R, int U, int MODE, int F>
+__global__ __launch_bounds__(threads_of<F>(), (F & kOcc8) ? 8 : 1) void gf_apply_kernel(const ApplyArgs a) {
+    constexpr int TH = threads_of<F>();
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr bool kLds = (F & kScalarTabs) == 0;
+    // Multi-plan launches (reconstruct batches with several erasure patterns)
+    // pick the plan per block; single-plan launches stage it once.
+    const bool multi = a.plan_table != nullptr;
+    Ctx c{};
+    if (!multi) {
+        if constexpr (kLds) {
+            stage_plan<R, TH>(a, a.plan, smem, c);
+            __syncthreads();
+        } else {
+            c.g_in_idx = reinterpret_cast<const uint16_t*>(a.plan + 8);
+            c.g_out_idx = c.g_in_idx + a.k;
+            c.g_tab = reinterpret_cast<const uint32_t*>(a.plan + a.tab_off);
+        }
+    }
     const uint32_t tpb = a.tiles_per_block;
-    const uint64_t tb = uint64_t(kThreads) * 16 * U;
+    const uint64_t tb = uint64_t(TH) * 16 * U;
     for (uint64_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
         const uint64_t j = tile / tpb;
         const uint64_t cc = tile - j * tpb;
         const uint64_t blk = a.blk_list ? uint64_t(a.blk_list[j]) : a.blk_first + j * a.blk_stride;
+        if (multi) {
+            const uint8_t* plan = a.plan_table[a.blk_plan[j]];
+            if constexpr (kLds) {
+                __syncthreads();   // previous tile's LDS reads are done
+                stage_plan<R, TH>(a, plan, smem, c);
+                __syncthreads();
+            } else {
+                c.g_in_idx = reinterpret_cast<const uint16_t*>(plan + 8);
+                c.g_out_idx = c.g_in_idx + a.k;
+                c.g_tab = reinterpret_cast<const uint32_t*>(plan + a.tab_off);
+            }
+        }
         const uint8_t* ib = a.in_base + blk * a.in_bpitch;
         uint8_t* ob = a.out_base + blk * a.out_bpitch;
         do_tile<R, U, MODE, F>(a, c, ib, ob, a.col_base + cc * tb);
@@ -301,7 +336,7 @@ hipError_t launch_one(const ApplyArgs& a, int grid_cap, hipStream_t stream) {
         int cus = 0, per_cu = 0;
         e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (e != hipSuccess) return e;
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, lds);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads_of<F>(), lds);
         if (e != hipSuccess) return e;
         if (per_cu < 1) per_cu = 1;
         uint64_t maxg = uint64_t(cus) * uint64_t(per_cu);
@@ -313,7 +348,7 @@ hipError_t launch_one(const ApplyArgs& a, int grid_cap, hipStream_t stream) {
     }
     if (grid > a.ntiles) grid = a.ntiles;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL(kern, dim3(uint32_t(grid)), dim3(kThreads), lds, stream, a);
+    hipLaunchKernelGGL(kern, dim3(uint32_t(grid)), dim3(threads_of<F>()), lds, stream, a);
     return hipGetLastError();
 }
 
@@ -321,7 +356,8 @@ hipError_t launch_one(const ApplyArgs& a, int grid_cap, hipStream_t stream) {
 template <int R>
 hipError_t dispatch_full(const ApplyArgs& a, const Variant& v, int grid_cap, hipStream_t s) {
     const int f = (v.nt_load ? kNtLoad : 0) | (v.nt_store ? kNtStore : 0) | (v.scalar_tabs ? kScalarTabs : 0) |
-                  (v.occ8 ? kOcc8 : 0) | (v.diag ? kDiagXor : 0);
+                  (v.occ8 ? kOcc8 : 0) | (v.diag ? kDiagXor : 0) | (v.threads == 128 ? kTh128 : 0) |
+                  (v.threads == 512 ? kTh512 : 0);
 // Not every flag combination is compiled: unsupported combinations return
 // hipErrorInvalidValue (the C ABI reports SHMR_EC_INVALID_ARGUMENT).
 #define SHMR_F(UU, FL) \
@@ -337,6 +373,10 @@ hipError_t dispatch_full(const ApplyArgs& a, const Variant& v, int grid_cap, hip
     SHMR_F(2, 0)
     SHMR_F(2, kNtLoad | kNtStore)
     SHMR_F(4, kNtLoad | kNtStore)
+    SHMR_F(1, kNtLoad | kNtStore | kTh128)
+    SHMR_F(1, kNtLoad | kNtStore | kTh512)
+    SHMR_F(1, kNtStore | kTh512)
+    SHMR_F(2, kNtLoad | kNtStore | kTh128)
 #undef SHMR_F
     return hipErrorInvalidValue;
 }

@@ -11,7 +11,7 @@ namespace kern {
 constexpr int kThreads = 256;                          // lanes per workgroup (4 waves)
 // A tile = kThreads * 16 * U bytes of columns of one block; U (16-byte chunks
 // per lane per shard) is a launch parameter in {1, 2, 4}.
-inline uint64_t tile_bytes(int u) { return uint64_t(kThreads) * 16 * uint64_t(u); }
+inline uint64_t tile_bytes(int u, int threads = kThreads) { return uint64_t(threads) * 16 * uint64_t(u); }
 constexpr unsigned kMaxRowsPerLaunch = 4;
 
 // Shard t of block b lives at in_base + b * in_bpitch + in_idx[t] * in_spitch,
@@ -33,7 +33,11 @@ struct ApplyArgs {
     uint32_t m;              // rows in the plan image
     uint32_t row0;           // first plan row handled by this launch
     uint32_t out_bias;       // output r at (out_idx[row0 + r] - out_bias) * out_spitch
-    const uint8_t* plan;     // device plan image (gf256.hpp Plan::image)
+    const uint8_t* plan;     // device plan image (gf256.hpp Plan::image), single-plan launches
+    // Multi-plan launches (plan_table != nullptr): block j uses plan
+    // plan_table[blk_plan[j]]; every plan of a launch has the same k and m.
+    const uint8_t* const* plan_table;
+    const uint16_t* blk_plan;
     uint32_t tab_off;        // byte offset of the PermTab array in the image
 };
 
@@ -45,6 +49,7 @@ struct Variant {
     bool scalar_tabs = false;// coefficient tables via scalar loads instead of LDS
     bool occ8 = false;       // __launch_bounds__ for 8 waves / SIMD
     bool diag = false;       // diagnostics: XOR-only (wrong results)
+    int threads = kThreads;  // lanes per workgroup (128, 256, 512)
 };
 
 // rows in [1, kMaxRowsPerLaunch].  mode 0: full tiles, every shard base

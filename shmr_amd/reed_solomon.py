@@ -19,7 +19,7 @@ import numpy as np
 
 from ._native import _u8p, lib
 
-__all__ = ["Error", "ReedSolomon", "calculate_shard_size", "device_count", "set_tuning", "get_tuning"]
+__all__ = ["Error", "ReedSolomon", "calculate_shard_size", "device_count", "set_tuning", "get_tuning", "describe_variant"]
 
 
 class Error(Exception):
@@ -53,6 +53,13 @@ def set_tuning(**knobs) -> None:
 
 def get_tuning(key: str) -> int:
     return int(lib().shmr_ec_get_tuning(key.encode()))
+
+
+def describe_variant(decode: bool, data_shards: int, rows: int) -> str:
+    """The kernel variant a launch of this shape uses (after the auto policy)."""
+    buf = ctypes.create_string_buffer(256)
+    _check(lib().shmr_ec_describe_variant(int(decode), data_shards, rows, buf, 256))
+    return buf.value.decode()
 
 
 def _writable_u8(buf) -> np.ndarray:

@@ -1,20 +1,22 @@
 #!/bin/bash
-# rocprofv3 passes for the bench command: kernel trace + stats, then one PMC
-# pass per counter (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950).
-# Usage: tools/profile.sh <tag> [bench args...]
+# rocprofv3 passes for one bench config: kernel trace + stats, then one PMC
+# pass per counter (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950),
+# then tools/pmc_traffic.py merges the summary into gpurun_out/pmc_traffic.json.
+# Usage: tools/profile.sh <tag> <config> <blocks> <algo_bytes_per_launch>
 set -u
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
-TAG=${1:-r01}; shift || true
-ARGS="$*"
-OUT="$ROOT/gpurun_out/prof_$TAG"
+TAG=$1; CFG=$2; BLOCKS=$3; ALGO=$4
+OUT="$ROOT/gpurun_out/prof_${TAG}_${CFG}"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o kt -- \
-  python3 "$ROOT/bench.py" --no-cpu $ARGS > "$OUT/kt.log" 2>&1
-rc=$?; echo "kernel-trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  python3 "$ROOT/bench.py" --no-cpu --config "$CFG" --blocks "$BLOCKS" > "$OUT/kt.log" 2>&1
+rc=$?; echo "kernel-trace $CFG rc=$rc"; [ $rc -eq 0 ] || exit $rc
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d "$OUT/$C" -o pmc -- \
-    python3 "$ROOT/bench.py" --no-cpu --steps 5 --warmup 1 $ARGS > "$OUT/$C.log" 2>&1
+    python3 "$ROOT/bench.py" --no-cpu --config "$CFG" --blocks "$BLOCKS" --steps 5 --warmup 1 --ramp-seconds 0.2 \
+    > "$OUT/$C.log" 2>&1
   rc=$?; echo "pmc $C rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
-find "$OUT" -name "*.csv" | head -20
+python3 "$ROOT/tools/pmc_traffic.py" "$OUT" --config "$CFG" --blocks "$BLOCKS" --algo-bytes "$ALGO" \
+  --merge "$ROOT/gpurun_out/pmc_traffic.json"
