@@ -32,6 +32,7 @@ import torch  # noqa: E402  (before shmr_amd: share one HIP runtime)
 import torch.distributed as dist  # noqa: E402
 
 import shmr_amd  # noqa: E402
+from shmr_amd import placement  # noqa: E402
 
 METRIC = "GiB/s erasure-encoded (device-resident), RS(8,3) 4 MiB StorageBlocks, 1/2/4/8 GPUs"
 HBM_PEAK = 8.0e12          # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -107,7 +108,7 @@ def main():
         rs.encode_batch_dev(shards[:, :k], shards[:, k:], shard_len=S,
                             data_shard_pitch=pitch, parity_shard_pitch=pitch)
         present = np.ones((B, k + p), dtype=np.uint8)
-        gb = np.arange(B) * world + rank
+        gb = np.array(placement.weak_batch(B, rank, world))         # global block ids of this rank
         if erasures == 1:
             present[np.arange(B), gb % k] = 0
         else:
@@ -150,10 +151,7 @@ def main():
     step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
     gpu_s = sum(step_ms) / 1e3
     elapsed = max(wall, gpu_s)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = placement.max_over_ranks(elapsed, device=dev)
 
     total_payload = payload_bytes_per_block * B * world * args.steps
     value = total_payload / elapsed / 2 ** 30

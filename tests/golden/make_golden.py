@@ -1,0 +1,141 @@
+#!/usr/bin/env python3
+"""Generates the committed golden fixtures under tests/golden/.
+
+Two kinds of data, kept apart on purpose:
+
+* kat.json "published" -- known-answer values of the crate the reference calls
+  (reed-solomon-erasure 6.0.0, itself a port of Backblaze JavaReedSolomon):
+  galois multiply/exp KATs and the RS(5,5) encode vector.  These pin the
+  oracle to the upstream algorithm; they are data, not code.
+* everything else -- produced by this repo's CPU oracle (oracle/rs_oracle.py)
+  from seeded inputs: parity rows of the BASELINE configs, small blocks in full
+  bytes, benchmark-sized blocks as SHA-256 per shard, shmr glue cases
+  (calculate_shard_size f32 edges, sync_data partial buffers, load_block
+  quirks).  These are the build's own pins (regression vectors).
+
+Run:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle import rs_oracle as O  # noqa: E402
+
+SEED = O.BENCH_SEED
+
+
+def sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def published_kats():
+    return {
+        "source": "reed-solomon-erasure 6.0.0 galois_8 tests / Backblaze JavaReedSolomon (published KATs)",
+        "gal_mul": [[3, 4, 12], [7, 7, 21], [23, 45, 41]],
+        "gal_exp": [[2, 2, 4], [5, 20, 235], [13, 7, 43]],
+        "encode": [{"data_shards": 5, "parity_shards": 5,
+                    "data": [[0, 1], [4, 5], [2, 3], [6, 7], [8, 9]],
+                    "parity": [[12, 13], [10, 11], [14, 15], [90, 91], [94, 95]]}],
+    }
+
+
+def build_pins():
+    pins = {"parity_rows": {}, "shard_size": [], "tables": {}}
+    for k, p in [(4, 2), (8, 3), (10, 4), (5, 5), (1, 1), (2, 1), (17, 3), (200, 56)]:
+        pins["parity_rows"][f"{k},{p}"] = O.ReedSolomon(k, p).parity_rows().tolist()
+    for length, k in [(1 << 20, 4), (4 << 20, 8), (16 << 20, 10), (7000, 4), (16777217, 8), (16777221, 10),
+                      (16777216, 3), (1, 7), (0, 3), (33554433, 16), (100, 3)]:
+        pins["shard_size"].append([length, k, O.calculate_shard_size(length, k)])
+    pins["tables"] = {"log_sha256": sha(O.LOG_TABLE), "exp_sha256": sha(O.EXP_TABLE),
+                      "mul_sha256": sha(O.MUL_TABLE)}
+    return pins
+
+
+def small_vectors():
+    """Full-byte vectors, small enough to commit as .npz."""
+    out = {}
+    cases = [(4, 2, 1024), (8, 3, 777), (10, 4, 1000), (3, 3, 17), (1, 1, 5), (6, 2, 4096 + 3)]
+    for ci, (k, p, L) in enumerate(cases):
+        rng = np.random.default_rng([SEED, 1000 + ci])
+        data = rng.integers(0, 256, (k, L), dtype=np.uint8)
+        sh = [d.copy() for d in data] + [np.zeros(L, np.uint8) for _ in range(p)]
+        O.ReedSolomon(k, p).encode(sh)
+        out[f"enc_{k}_{p}_{L}_data"] = data
+        out[f"enc_{k}_{p}_{L}_parity"] = np.stack(sh[k:])
+    # reconstruct vectors: inconsistent (random) shards exercise the crate's
+    # "first k present + re-encode parity" rule
+    k, p, L = 4, 3, 64
+    rng = np.random.default_rng([SEED, 2000])
+    shards = rng.integers(0, 256, (k + p, L), dtype=np.uint8)
+    out["rec_4_3_shards"] = shards
+    pats = [[0], [6], [0, 4], [1, 2, 3], [3, 5, 6], [0, 1, 2]]
+    results = []
+    for miss in pats:
+        got = [None if i in miss else shards[i].copy() for i in range(k + p)]
+        O.ReedSolomon(k, p).reconstruct(got)
+        results.append(np.stack(got))
+    out["rec_4_3_missing"] = np.array([m + [-1] * (3 - len(m)) for m in pats], dtype=np.int16)
+    out["rec_4_3_result"] = np.stack(results)
+    return out
+
+
+def large_vectors():
+    """Benchmark-sized blocks as SHA-256 per shard (inputs regenerated from seed)."""
+    out = []
+    for k, p, size, idx in [(4, 2, 1 << 20, 0), (8, 3, 4 << 20, 0), (8, 3, 4 << 20, 1), (10, 4, 16 << 20, 0)]:
+        S = O.calculate_shard_size(size, k)
+        buf = O.seeded_block(SEED, idx, size)
+        shards = O.sync_data_erasure(buf.tobytes(), size, k, p)
+        out.append({"k": k, "p": p, "block_bytes": size, "seed": [SEED, idx], "shard_bytes": S,
+                    "generator": "numpy.random.default_rng([seed, idx]).integers(0, 256, block_bytes, uint8)",
+                    "shard_sha256": [sha(s) for s in shards]})
+    # edge blocks: all-0x00, all-0xFF, partial buffer 700,001 B
+    for name, buf in [("zeros", np.zeros(1 << 20, np.uint8)), ("ones", np.full(1 << 20, 0xFF, np.uint8)),
+                      ("partial_700001", O.seeded_block(SEED, 7, 700001))]:
+        shards = O.sync_data_erasure(buf.tobytes(), 1 << 20, 4, 2)
+        out.append({"k": 4, "p": 2, "block_bytes": 1 << 20, "case": name, "buffer_len": int(buf.size),
+                    "seed": [SEED, 7] if name.startswith("partial") else None,
+                    "shard_sha256": [sha(s) for s in shards]})
+    return out
+
+
+def glue_cases():
+    """load_block quirks (src/vfs/block.rs:529-579)."""
+    k, p, size = 4, 2, 4096
+    buf = O.seeded_block(SEED, 42, size)
+    shards = O.sync_data_erasure(buf.tobytes(), size, k, p)
+    cases = {}
+    # a read error on data shard 1 -> None -> reconstructed
+    s1 = [bytes(x) for x in shards]
+    s1[1] = None
+    cases["read_error_data1"] = sha(O.load_block_erasure(s1, size, k, p))
+    # a truncated shard is zero-padded and stays "present" -> reconstruct is a
+    # no-op when every shard is Some, so the zero padding survives
+    s2 = [bytes(x) for x in shards]
+    s2[2] = s2[2][:100]
+    cases["truncated_data2"] = sha(O.load_block_erasure(s2, size, k, p))
+    cases["intact"] = sha(O.load_block_erasure([bytes(x) for x in shards], size, k, p))
+    cases["original"] = sha(buf)
+    return cases
+
+
+def main():
+    kat = {"published": published_kats(), "build_pins": build_pins(), "large": large_vectors(),
+           "load_block": glue_cases()}
+    with open(os.path.join(HERE, "kat.json"), "w") as f:
+        json.dump(kat, f, indent=1)
+    np.savez_compressed(os.path.join(HERE, "small_vectors.npz"), **small_vectors())
+    print("wrote", os.path.join(HERE, "kat.json"), "and small_vectors.npz")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,212 @@
+"""CPU tests of the C ABI (include/shmr_ec.h): the library loads, exports every
+declared symbol, and its host-side logic (no GPU compute) matches the oracle
+and the crate's error behaviour.  No kernel is launched here.
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import shmr_amd
+from shmr_amd import _native
+from oracle import rs_oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "shmr_ec.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(shmr_ec_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_header_declares_the_boundary():
+    fns = declared_functions()
+    for required in ("shmr_ec_new", "shmr_ec_free", "shmr_ec_encode", "shmr_ec_reconstruct",
+                     "shmr_ec_shard_size", "shmr_ec_encode_batch_dev", "shmr_ec_reconstruct_batch_dev"):
+        assert required in fns
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _native.lib()
+    for fn in declared_functions():
+        assert hasattr(lib, fn), fn
+    out = subprocess.run(["nm", "-D", "--defined-only", _native.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (shmr_ec_\w+)", out))
+    assert set(declared_functions()) <= exported
+
+
+def test_python_signatures_cover_header():
+    assert {name for name, _, _ in _native.SIGNATURES} == set(declared_functions())
+
+
+def test_library_is_gfx950_code_object():
+    """The fat binary carries a gfx950 (MI355X) device code object and no other target."""
+    data = open(_native.LIB_PATH, "rb").read()
+    assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in data
+    targets = set(re.findall(rb"hipv4-amdgcn-amd-amdhsa--(gfx[0-9a-f]+)", data))
+    assert targets == {b"gfx950"}
+
+
+def test_header_compiles_as_c():
+    src = '#include "shmr_ec.h"\nint main(void){shmr_ec_t* r=0; return shmr_ec_new(8,3,&r) == 0 ? 0 : 1;}\n'
+    path = "/tmp/shmr_abi_check.c"
+    with open(path, "w") as f:
+        f.write(src)
+    r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-c", "-I", os.path.join(ROOT, "include"), path,
+                        "-o", "/tmp/shmr_abi_check.o"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_status_names_match_crate_variants():
+    lib = _native.lib()
+    names = {c: lib.shmr_ec_status_name(c).decode() for c in range(-13, 1)}
+    assert names[-1] == "TooFewShards" and names[-2] == "TooManyShards"
+    assert names[-3] == "TooFewDataShards" and names[-5] == "TooFewParityShards"
+    assert names[-9] == "IncorrectShardSize" and names[-10] == "TooFewShardsPresent"
+    assert names[-11] == "EmptyShard" and names[0] == "Ok"
+
+
+@pytest.mark.parametrize("length,k", [(1 << 20, 4), (4 << 20, 8), (16 << 20, 10), (7000, 4), (16777217, 8),
+                                      (16777221, 10), (1, 7), (0, 3), (2 ** 40 + 3, 13), (123456789, 5)])
+def test_shard_size_matches_oracle(length, k):
+    assert shmr_amd.calculate_shard_size(length, k) == O.calculate_shard_size(length, k)
+
+
+def test_shard_size_random_sweep():
+    rng = np.random.default_rng(0)
+    for length, k in zip(rng.integers(1, 1 << 34, 2000), rng.integers(1, 256, 2000)):
+        assert shmr_amd.calculate_shard_size(int(length), int(k)) == O.calculate_shard_size(int(length), int(k))
+
+
+def test_new_errors_match_crate():
+    for (k, p), name in [((0, 1), "TooFewDataShards"), ((1, 0), "TooFewParityShards"),
+                         ((200, 57), "TooManyShards"), ((255, 2), "TooManyShards")]:
+        with pytest.raises(shmr_amd.Error) as e:
+            shmr_amd.ReedSolomon(k, p)
+        assert e.value.name == name
+    r = shmr_amd.ReedSolomon(255, 1)
+    assert (r.data_shard_count(), r.parity_shard_count(), r.total_shard_count()) == (255, 1, 256)
+
+
+@pytest.mark.parametrize("k,p", [(4, 2), (8, 3), (10, 4), (5, 5), (1, 1), (17, 3), (128, 128)])
+def test_matrix_matches_oracle(k, p):
+    assert (shmr_amd.ReedSolomon(k, p).matrix() == O.build_matrix(k, k + p)).all()
+
+
+@pytest.mark.parametrize("k,p", [(8, 3), (10, 4), (4, 3)])
+def test_reconstruct_plan_rows_match_oracle(k, p):
+    """The GPU runs one fused matrix per erasure pattern: rows of the inverted
+    sub-matrix for absent data, and M[parity] * Dec for absent parity -- the
+    same bytes the crate gets by rebuilding data then re-encoding parity."""
+    import itertools
+    rs = shmr_amd.ReedSolomon(k, p)
+    m = O.build_matrix(k, k + p)
+    for n in range(1, p + 1):
+        for miss in list(itertools.combinations(range(k + p), n))[:40]:
+            present = [i not in miss for i in range(k + p)]
+            for data_only in (False, True):
+                in_idx, out_idx, rows = rs.reconstruct_plan(present, data_only)
+                valid = [i for i in range(k + p) if present[i]][:k]
+                assert in_idx == valid
+                dec = O.mat_invert(m[valid])
+                want_idx = [i for i in miss if i < k] + ([] if data_only else [i for i in miss if i >= k])
+                assert out_idx == want_idx
+                for r, j in enumerate(out_idx):
+                    want = dec[j] if j < k else O.mat_mul(m[j:j + 1], dec)[0]
+                    assert (rows[r] == want).all(), (miss, j)
+
+
+def test_reconstruct_plan_checks():
+    rs = shmr_amd.ReedSolomon(4, 2)
+    assert rs.reconstruct_plan([1] * 6)[1] == []                  # all present: nothing to do
+    with pytest.raises(shmr_amd.Error) as e:
+        rs.reconstruct_plan([1, 1, 1, 0, 0, 0])
+    assert e.value.name == "TooFewShardsPresent"
+    with pytest.raises(shmr_amd.Error) as e:
+        rs.reconstruct_plan([1] * 5)
+    assert e.value.name == "TooFewShards"
+
+
+def test_encode_validation_precedes_device_use():
+    """The crate's checks (count, then empty, then equal lengths) run before any
+    device is touched, in the crate's order."""
+    rs = shmr_amd.ReedSolomon(3, 2)
+    with pytest.raises(shmr_amd.Error) as e:
+        rs.encode([np.zeros(4, np.uint8)] * 4)
+    assert e.value.name == "TooFewShards"
+    with pytest.raises(shmr_amd.Error) as e:
+        rs.encode([np.zeros(4, np.uint8)] * 6)
+    assert e.value.name == "TooManyShards"
+    with pytest.raises(shmr_amd.Error) as e:
+        rs.encode([np.zeros(0, np.uint8) for _ in range(5)])
+    assert e.value.name == "EmptyShard"
+    with pytest.raises(shmr_amd.Error) as e:
+        rs.encode([np.zeros(4, np.uint8) for _ in range(4)] + [np.zeros(5, np.uint8)])
+    assert e.value.name == "IncorrectShardSize"
+
+
+def test_reconstruct_validation_precedes_device_use():
+    rs = shmr_amd.ReedSolomon(3, 2)
+    full = [np.arange(4, dtype=np.uint8) for _ in range(5)]
+    same = [x.copy() for x in full]
+    rs.reconstruct(same)                                          # all present: no-op, no device
+    with pytest.raises(shmr_amd.Error) as e:
+        rs.reconstruct([full[0], None, None, None, full[4]])
+    assert e.value.name == "TooFewShardsPresent"
+    with pytest.raises(shmr_amd.Error) as e:
+        rs.reconstruct([full[0], np.zeros(3, np.uint8), None, full[3], full[4]])
+    assert e.value.name == "IncorrectShardSize"
+    with pytest.raises(shmr_amd.Error) as e:
+        rs.reconstruct([np.zeros(0, np.uint8), None, full[2], full[3], full[4]])
+    assert e.value.name == "EmptyShard"
+
+
+def test_compute_without_gpu_fails_loudly():
+    """No CPU fallback: on a machine without a GPU the compute entry points
+    report NoDevice instead of computing anything."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    rs = shmr_amd.ReedSolomon(3, 2)
+    with pytest.raises(shmr_amd.Error) as e:
+        rs.encode([np.zeros(4, np.uint8) for _ in range(5)])
+    assert e.value.name == "NoDevice"
+    assert shmr_amd.device_count() == 0
+
+
+def test_tuning_api():
+    saved = shmr_amd.get_tuning("encode.chunks")
+    try:
+        shmr_amd.set_tuning(**{"encode.chunks": 2})
+        assert shmr_amd.get_tuning("encode.chunks") == 2
+        assert "chunks=2" in shmr_amd.describe_variant(False, 8, 3)
+        with pytest.raises(shmr_amd.Error):
+            shmr_amd.set_tuning(chunks=3)
+        with pytest.raises(shmr_amd.Error):
+            shmr_amd.set_tuning(no_such_knob=1)
+    finally:
+        shmr_amd.set_tuning(**{"encode.chunks": saved})
+    # the measured policy: 4 output rows -> 2 chunks/lane; k < 8 -> no NT loads
+    assert "chunks=2" in shmr_amd.describe_variant(False, 10, 4)
+    assert "nt_load=0" in shmr_amd.describe_variant(False, 4, 2)
+    assert "nt_load=1" in shmr_amd.describe_variant(True, 8, 1)
+
+
+def test_native_library_is_required():
+    """The package refuses to run without the in-tree .so (no fallback)."""
+    assert os.path.exists(_native.LIB_PATH)
+    assert _native.LIB_PATH.startswith(os.path.join(ROOT, "shmr_amd"))
+    saved = _native.LIB_PATH
+    try:
+        _native._lib, keep = None, _native._lib
+        _native.LIB_PATH = "/nonexistent/libshmr_ec.so"
+        with pytest.raises(_native.NativeLibraryMissing):
+            _native.lib()
+    finally:
+        _native.LIB_PATH = saved
+        _native._lib = keep
