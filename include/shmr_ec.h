@@ -135,13 +135,28 @@ int shmr_ec_reconstruct_batch_dev(shmr_ec_t* rs, uint8_t* d_shards, size_t shard
                                   size_t block_pitch, const uint8_t* present, size_t nblocks,
                                   size_t shard_len, int data_only, int device, void* stream);
 
-/* ---- multi-GPU host batch ------------------------------------------------ *
- * Encode nblocks blocks held in HOST memory, whole blocks round-robin across
- * `devices` (block b -> devices[b % ndev]), H2D/kernel/D2H pipelined per
- * device.  host_shards[b * total + i] points at shard i of block b (data
- * read, parity written), each shard_len bytes.  Synchronous. */
+/* ---- host-buffer batches over one or more GPUs ---------------------------- *
+ * Blocks held in HOST memory (the Block Cache / shard file buffers), whole
+ * blocks round-robin across `devices` (block b -> devices[b % ndev]); per
+ * device the H2D copy, the kernel and the D2H copy of successive chunks
+ * overlap on separate streams.  host_shards[b * total + i] points at shard i
+ * of block b, each shard_len bytes.  Pinned buffers (shmr_ec_host_alloc) are
+ * DMA'd directly; pageable ones are staged through pinned memory by a crew of
+ * copy threads.  Synchronous; every block is validated before device work. */
 int shmr_ec_encode_blocks_host(shmr_ec_t* rs, uint8_t* const* host_shards, size_t nblocks,
                                size_t shard_len, const int* devices, int ndev);
+
+/* Reconstruct host-resident blocks: present = nblocks x total flags; absent
+ * shards are written (absent parity only when data_only == 0) and need a
+ * buffer; semantics per block as shmr_ec_reconstruct. */
+int shmr_ec_reconstruct_blocks_host(shmr_ec_t* rs, uint8_t* const* host_shards, const uint8_t* present,
+                                    size_t nblocks, size_t shard_len, int data_only,
+                                    const int* devices, int ndev);
+
+/* Pinned (page-locked) host memory for Block Cache buffers: the host-buffer
+ * entry points DMA it directly without a staging copy. */
+int shmr_ec_host_alloc(size_t bytes, void** out);
+void shmr_ec_host_free(void* p);
 
 /* ---- configuration -------------------------------------------------------- */
 

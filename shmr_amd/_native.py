@@ -47,6 +47,10 @@ SIGNATURES = [
       ctypes.c_void_p]),
     ("shmr_ec_encode_blocks_host", ctypes.c_int,
      [ctypes.c_void_p, _u8pp, _sz, _sz, ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    ("shmr_ec_reconstruct_blocks_host", ctypes.c_int,
+     [ctypes.c_void_p, _u8pp, _u8p, _sz, _sz, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    ("shmr_ec_host_alloc", ctypes.c_int, [_sz, ctypes.POINTER(ctypes.c_void_p)]),
+    ("shmr_ec_host_free", None, [ctypes.c_void_p]),
     ("shmr_ec_set_device", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("shmr_ec_set_tuning", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
     ("shmr_ec_get_tuning", ctypes.c_int, [ctypes.c_char_p]),

@@ -1,0 +1,464 @@
+// Device-side core of the erasure path (see ec_core.hpp).
+#include "ec_core.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+
+namespace shmr {
+namespace core {
+
+// ===========================================================================
+// Tuning.  kAuto knobs follow variant_policy(): the fastest variants measured
+// on MI355X per launch shape (tools/tune.py, interleaved A/B in one process;
+// DESIGN.md "Tuning").  set_tuning() pins a knob explicitly.
+// ===========================================================================
+namespace {
+
+struct Tuning {
+    std::atomic<int> u{kAuto};
+    std::atomic<int> nt_load{kAuto};
+    std::atomic<int> nt_store{kAuto};
+    std::atomic<int> scalar_tabs{0};
+    std::atomic<int> occ8{0};
+    std::atomic<int> grid{-1};     // -1: one workgroup per tile
+    std::atomic<int> diag{0};
+    std::atomic<int> threads{256};
+};
+Tuning g_tune[2];   // [kEncode], [kDecode]
+
+// Measured: encode RS(8,3): NT loads+stores, U=1 (78 % of HBM peak); RS(4,2):
+// NT stores only (77 % vs 72 % with NT loads); RS(10,4) (4 rows per launch):
+// U=2 (71 % vs 66 %); reconstruct: NT loads+stores, U=1.
+kern::Variant variant_policy(OpClass op, unsigned k, unsigned rows) {
+    kern::Variant v;
+    v.u = (op == kEncode && rows >= 4) ? 2 : 1;
+    v.nt_store = true;
+    v.nt_load = op == kDecode || k >= 8;
+    return v;
+}
+
+bool split_key(const char* key, std::string* k, int* first, int* last) {
+    if (!key) return false;
+    *k = key;
+    *first = kEncode;
+    *last = kDecode;
+    if (k->rfind("encode.", 0) == 0) {
+        *first = *last = kEncode;
+        *k = k->substr(7);
+    } else if (k->rfind("decode.", 0) == 0) {
+        *first = *last = kDecode;
+        *k = k->substr(7);
+    }
+    return true;
+}
+
+bool aligned16(uint64_t v) { return (v & 15u) == 0; }
+
+}  // namespace
+
+int set_tuning(const char* key, int value) {
+    std::string k;
+    int first = 0, last = 1;
+    if (!split_key(key, &k, &first, &last)) return SHMR_EC_INVALID_ARGUMENT;
+    for (int i = first; i <= last; ++i) {
+        Tuning& T = g_tune[i];
+        if (k == "chunks") {
+            if (value != 1 && value != 2 && value != 4 && value != kAuto) return SHMR_EC_INVALID_ARGUMENT;
+            T.u = value;
+        } else if (k == "nt_load") {
+            T.nt_load = value == kAuto ? kAuto : (value != 0);
+        } else if (k == "nt_store") {
+            T.nt_store = value == kAuto ? kAuto : (value != 0);
+        } else if (k == "scalar_tabs") {
+            T.scalar_tabs = value != 0;
+        } else if (k == "occ8") {
+            T.occ8 = value != 0;
+        } else if (k == "grid") {
+            if (value < -1) return SHMR_EC_INVALID_ARGUMENT;
+            T.grid = value;
+        } else if (k == "diag") {
+            T.diag = value != 0;
+        } else if (k == "threads") {
+            if (value != 128 && value != 256 && value != 512) return SHMR_EC_INVALID_ARGUMENT;
+            T.threads = value;
+        } else {
+            return SHMR_EC_INVALID_ARGUMENT;
+        }
+    }
+    return SHMR_EC_OK;
+}
+
+int get_tuning(const char* key) {
+    std::string k;
+    int first = 0, last = 1;
+    if (!split_key(key, &k, &first, &last)) return SHMR_EC_INVALID_ARGUMENT;
+    const Tuning& T = g_tune[first];
+    if (k == "chunks") return T.u;
+    if (k == "nt_load") return T.nt_load;
+    if (k == "nt_store") return T.nt_store;
+    if (k == "scalar_tabs") return T.scalar_tabs;
+    if (k == "occ8") return T.occ8;
+    if (k == "grid") return T.grid;
+    if (k == "diag") return T.diag;
+    if (k == "threads") return T.threads;
+    return SHMR_EC_INVALID_ARGUMENT;
+}
+
+kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows) {
+    const Tuning& T = g_tune[op];
+    kern::Variant v = variant_policy(op, k, rows);
+    if (T.u.load() != kAuto) v.u = T.u.load();
+    if (T.nt_load.load() != kAuto) v.nt_load = T.nt_load.load() != 0;
+    if (T.nt_store.load() != kAuto) v.nt_store = T.nt_store.load() != 0;
+    v.scalar_tabs = T.scalar_tabs.load() != 0;
+    v.occ8 = T.occ8.load() != 0;
+    v.diag = T.diag.load() != 0;
+    v.threads = T.threads.load();
+    return v;
+}
+
+int grid_mode(OpClass op) { return g_tune[op].grid.load(); }
+
+// ===========================================================================
+// Devices and plans
+// ===========================================================================
+int device_count() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int check_device(int dev) {
+    const int n = device_count();
+    if (n <= 0) return SHMR_EC_NO_DEVICE;
+    if (dev < 0 || dev >= n) return SHMR_EC_INVALID_ARGUMENT;
+    return SHMR_EC_OK;
+}
+
+uint32_t plan_tab_off(unsigned k, unsigned m) {
+    return uint32_t((8 + 2 * size_t(k) + 2 * size_t(m) + 31) & ~size_t(31));
+}
+
+int plan_on_device(Plan& plan, int dev, const uint8_t** out) {
+    std::lock_guard<std::mutex> lock(plan.dev_mu);
+    auto it = plan.dev_image.find(dev);
+    if (it != plan.dev_image.end()) {
+        *out = static_cast<const uint8_t*>(it->second);
+        return SHMR_EC_OK;
+    }
+    std::vector<uint8_t> img = plan.image();
+    void* d = nullptr;
+    if (hipMalloc(&d, img.size()) != hipSuccess) return SHMR_EC_OUT_OF_MEMORY;
+    if (hipMemcpy(d, img.data(), img.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        return SHMR_EC_DEVICE_ERROR;
+    }
+    plan.dev_image[dev] = d;
+    *out = static_cast<const uint8_t*>(d);
+    return SHMR_EC_OK;
+}
+
+// ===========================================================================
+// Launch sets.  Rows go in groups of <= 4 per launch; each group is one
+// full-tile launch (the tuned variant) plus, when len is not a multiple of the
+// tile, one launch over the remaining U=1 tiles (the last partial, byte-exact
+// bounds).  Unaligned layouts take the byte-granular kernel.
+// ===========================================================================
+int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_t len, hipStream_t stream,
+               OpClass op) {
+    const uint64_t nblk = bs.n;
+    if (nblk == 0 || plan.m == 0) return SHMR_EC_OK;
+    const uint8_t* dplan = nullptr;
+    const uint32_t tab_off = plan_tab_off(plan.k, plan.m);
+    if (!bs.d_plans) {
+        int rc = plan_on_device(plan, dev, &dplan);
+        if (rc) return rc;
+    }
+    kern::Variant tail;   // tail / unaligned launches: U = 1, plain loads
+    const int cap = grid_mode(op);
+    const bool aligned = aligned16(uintptr_t(L.in_base)) && aligned16(uintptr_t(L.out_base)) &&
+                         aligned16(L.in_bpitch) && aligned16(L.in_spitch) && aligned16(L.out_bpitch) &&
+                         aligned16(L.out_spitch);
+    for (uint32_t row0 = 0; row0 < plan.m; row0 += kern::kMaxRowsPerLaunch) {
+        const uint32_t rows = std::min<uint32_t>(kern::kMaxRowsPerLaunch, plan.m - row0);
+        const kern::Variant var = resolve_variant(op, plan.k, rows);
+        const uint64_t tb = kern::tile_bytes(var.u, var.threads);
+        kern::ApplyArgs a{};
+        a.in_base = L.in_base;
+        a.out_base = L.out_base;
+        a.in_bpitch = L.in_bpitch;
+        a.in_spitch = L.in_spitch;
+        a.out_bpitch = L.out_bpitch;
+        a.out_spitch = L.out_spitch;
+        a.out_bias = L.out_bias;
+        a.blk_list = bs.d_list;
+        a.blk_first = bs.first;
+        a.blk_stride = bs.stride;
+        a.nblk = nblk;
+        a.plan_table = bs.d_plans;
+        a.blk_plan = bs.d_plan_idx;
+        a.len = len;
+        a.k = plan.k;
+        a.m = plan.m;
+        a.row0 = row0;
+        a.plan = dplan;
+        a.tab_off = tab_off;
+        if (!aligned) {
+            const uint64_t tb1 = kern::tile_bytes(1);
+            a.col_base = 0;
+            a.tiles_per_block = uint32_t((len + tb1 - 1) / tb1);
+            a.ntiles = nblk * a.tiles_per_block;
+            SHMR_HIP_TRY(kern::launch_apply(a, rows, tail, 2, cap, stream));
+            continue;
+        }
+        const uint64_t full = len / tb;
+        if (full) {
+            a.col_base = 0;
+            a.tiles_per_block = uint32_t(full);
+            a.ntiles = nblk * full;
+            const hipError_t e = kern::launch_apply(a, rows, var, 0, cap, stream);
+            if (e == hipErrorInvalidValue) return SHMR_EC_INVALID_ARGUMENT;   // variant not compiled
+            if (e != hipSuccess) return SHMR_EC_DEVICE_ERROR;
+        }
+        if (len % tb) {
+            const uint64_t tb1 = kern::tile_bytes(1);
+            a.col_base = full * tb;
+            a.tiles_per_block = uint32_t((len - full * tb + tb1 - 1) / tb1);
+            a.ntiles = nblk * a.tiles_per_block;
+            SHMR_HIP_TRY(kern::launch_apply(a, rows, tail, 1, cap, stream));
+        }
+    }
+    return SHMR_EC_OK;
+}
+
+int encode_on_device(Codec& c, int dev, const Layout& L, uint64_t nblocks, uint64_t len, hipStream_t stream) {
+    BlockSet bs;
+    bs.n = nblocks;
+    return launch_set(*c.encode_plan(), dev, L, bs, len, stream, kEncode);
+}
+
+int validate_presence(const Codec& c, const uint8_t* present, uint64_t nblocks) {
+    const unsigned k = c.k(), t = k + c.p();
+    for (uint64_t b = 0; b < nblocks; ++b) {
+        unsigned np = 0;
+        for (unsigned i = 0; i < t; ++i) np += present[b * t + i] ? 1 : 0;
+        if (np != t && np < k) return SHMR_EC_TOO_FEW_SHARDS_PRESENT;
+    }
+    return SHMR_EC_OK;
+}
+
+int reconstruct_on_device(Codec& c, int dev, uint8_t* d_shards, uint64_t shard_pitch, uint64_t block_pitch,
+                          const uint8_t* present, uint64_t nblocks, uint64_t len, bool data_only,
+                          hipStream_t stream) {
+    const unsigned k = c.k(), t = k + c.p();
+    std::map<std::vector<uint8_t>, std::vector<uint64_t>> groups;   // pattern -> blocks
+    for (uint64_t b = 0; b < nblocks; ++b) {
+        const uint8_t* pr = present + b * t;
+        unsigned np = 0;
+        for (unsigned i = 0; i < t; ++i) np += pr[i] ? 1 : 0;
+        if (np == t) continue;                          // crate: all present -> Ok(())
+        if (np < k) return SHMR_EC_TOO_FEW_SHARDS_PRESENT;
+        std::vector<uint8_t> key(t);
+        for (unsigned i = 0; i < t; ++i) key[i] = pr[i] ? 1 : 0;
+        groups[key].push_back(b);
+    }
+    if (groups.empty()) return SHMR_EC_OK;
+    const Layout L{d_shards, d_shards, block_pitch, shard_pitch, block_pitch, shard_pitch, 0};
+    // Patterns with the same number of rebuilt shards share one multi-plan
+    // launch set: the kernel picks each block's plan from a device table, so a
+    // batch with many erasure patterns is still one launch (plus a tail).
+    struct Group {
+        std::vector<std::shared_ptr<Plan>> plans;
+        std::vector<uint32_t> blocks;
+        std::vector<uint16_t> plan_idx;
+    };
+    std::map<unsigned, Group> by_m;
+    for (auto& g : groups) {
+        auto plan = c.reconstruct_plan(g.first, data_only);
+        if (plan->m == 0) continue;
+        Group& grp = by_m[plan->m];
+        const uint16_t pi = uint16_t(grp.plans.size());
+        grp.plans.push_back(plan);
+        for (uint64_t b : g.second) {
+            grp.blocks.push_back(uint32_t(b));
+            grp.plan_idx.push_back(pi);
+        }
+    }
+    int rc = SHMR_EC_OK;
+    for (auto& kv : by_m) {
+        Group& grp = kv.second;
+        // A single pattern over an arithmetic block sequence needs no upload.
+        bool arith = grp.plans.size() == 1;
+        const uint64_t stride = grp.blocks.size() > 1 ? uint64_t(grp.blocks[1]) - grp.blocks[0] : 1;
+        for (size_t i = 1; arith && i < grp.blocks.size(); ++i)
+            arith = uint64_t(grp.blocks[i]) - grp.blocks[i - 1] == stride;
+        if (arith) {
+            BlockSet bs;
+            bs.first = grp.blocks[0];
+            bs.stride = stride;
+            bs.n = grp.blocks.size();
+            rc = launch_set(*grp.plans[0], dev, L, bs, len, stream, kDecode);
+            if (rc) return rc;
+            continue;
+        }
+        if (grp.plans.size() > 65535) return SHMR_EC_INVALID_ARGUMENT;
+        std::vector<const uint8_t*> dplans(grp.plans.size());
+        for (size_t i = 0; i < grp.plans.size(); ++i) {
+            rc = plan_on_device(*grp.plans[i], dev, &dplans[i]);
+            if (rc) return rc;
+        }
+        UploadRing* ring = UploadRing::for_device(dev, &rc);
+        if (!ring) return rc;
+        const size_t table_bytes = (dplans.size() * sizeof(void*) + 15) & ~size_t(15);
+        if (table_bytes + 64 > UploadRing::kSlotBytes) return SHMR_EC_INVALID_ARGUMENT;
+        const size_t per_chunk = (UploadRing::kSlotBytes - table_bytes - 32) / (sizeof(uint32_t) + sizeof(uint16_t));
+        for (size_t c0 = 0; c0 < grp.blocks.size(); c0 += per_chunk) {
+            const size_t n = std::min(per_chunk, grp.blocks.size() - c0);
+            uint8_t *hslot = nullptr, *dslot = nullptr;
+            int slot = -1;
+            rc = ring->acquire(&hslot, &dslot, &slot);
+            if (rc) return rc;
+            const size_t list_off = table_bytes;
+            const size_t pidx_off = (list_off + n * sizeof(uint32_t) + 15) & ~size_t(15);
+            const size_t total = pidx_off + n * sizeof(uint16_t);
+            std::memcpy(hslot, dplans.data(), dplans.size() * sizeof(void*));
+            std::memcpy(hslot + list_off, grp.blocks.data() + c0, n * sizeof(uint32_t));
+            std::memcpy(hslot + pidx_off, grp.plan_idx.data() + c0, n * sizeof(uint16_t));
+            rc = ring->upload(slot, total, stream);
+            BlockSet bs;
+            bs.n = n;
+            bs.d_plans = reinterpret_cast<const uint8_t* const*>(dslot);
+            bs.d_list = reinterpret_cast<const uint32_t*>(dslot + list_off);
+            bs.d_plan_idx = reinterpret_cast<const uint16_t*>(dslot + pidx_off);
+            if (rc == SHMR_EC_OK) rc = launch_set(*grp.plans[0], dev, L, bs, len, stream, kDecode);
+            const int rc2 = ring->release_after(slot, stream);
+            if (rc) return rc;
+            if (rc2) return rc2;
+        }
+    }
+    return SHMR_EC_OK;
+}
+
+// ===========================================================================
+// Upload ring
+// ===========================================================================
+UploadRing* UploadRing::for_device(int dev, int* rc) {
+    static std::mutex mu;
+    static auto* rings = new std::map<int, UploadRing*>;   // leaked: outlives static teardown
+    std::lock_guard<std::mutex> lock(mu);
+    auto& r = (*rings)[dev];
+    if (!r) {
+        auto* ring = new UploadRing;
+        if (hipHostMalloc(reinterpret_cast<void**>(&ring->host_), kSlots * kSlotBytes, hipHostMallocDefault) !=
+                hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&ring->dev_), kSlots * kSlotBytes) != hipSuccess) {
+            *rc = SHMR_EC_OUT_OF_MEMORY;
+            return nullptr;
+        }
+        for (int i = 0; i < kSlots; ++i) {
+            if (hipEventCreateWithFlags(&ring->ev_[i], hipEventDisableTiming) != hipSuccess) {
+                *rc = SHMR_EC_DEVICE_ERROR;
+                return nullptr;
+            }
+        }
+        r = ring;
+    }
+    *rc = SHMR_EC_OK;
+    return r;
+}
+
+int UploadRing::acquire(uint8_t** host, uint8_t** dev, int* slot) {
+    std::unique_lock<std::mutex> lock(mu_);
+    for (;;) {
+        for (int n = 0; n < kSlots; ++n) {
+            const int i = (next_ + n) % kSlots;
+            if (inuse_[i]) continue;
+            inuse_[i] = true;
+            next_ = (i + 1) % kSlots;
+            const bool armed = armed_[i];
+            lock.unlock();
+            if (armed && hipEventSynchronize(ev_[i]) != hipSuccess) {
+                release_now(i);
+                return SHMR_EC_DEVICE_ERROR;
+            }
+            *host = host_ + size_t(i) * kSlotBytes;
+            *dev = dev_ + size_t(i) * kSlotBytes;
+            *slot = i;
+            return SHMR_EC_OK;
+        }
+        cv_.wait(lock);
+    }
+}
+
+int UploadRing::upload(int slot, size_t bytes, hipStream_t stream) {
+    const size_t off = size_t(slot) * kSlotBytes;
+    return hipMemcpyAsync(dev_ + off, host_ + off, bytes, hipMemcpyHostToDevice, stream) == hipSuccess
+               ? SHMR_EC_OK
+               : SHMR_EC_DEVICE_ERROR;
+}
+
+int UploadRing::release_after(int slot, hipStream_t stream) {
+    const bool ok = hipEventRecord(ev_[slot], stream) == hipSuccess;
+    std::lock_guard<std::mutex> lock(mu_);
+    armed_[slot] = ok;
+    inuse_[slot] = false;
+    cv_.notify_one();
+    return ok ? SHMR_EC_OK : SHMR_EC_DEVICE_ERROR;
+}
+
+void UploadRing::release_now(int slot) {
+    std::lock_guard<std::mutex> lock(mu_);
+    inuse_[slot] = false;
+    cv_.notify_one();
+}
+
+// ===========================================================================
+// Staging pool
+// ===========================================================================
+StagingPool& StagingPool::get() {
+    static StagingPool* p = new StagingPool;   // leaked: outlives static teardown
+    return *p;
+}
+
+Staging* StagingPool::acquire(int dev, size_t bytes, int* rc) {
+    Staging* s = nullptr;
+    {
+        std::lock_guard<std::mutex> lock(mu_);
+        auto& lst = free_[dev];
+        if (!lst.empty()) {
+            s = lst.back();
+            lst.pop_back();
+        }
+    }
+    if (!s) {
+        s = new Staging;
+        s->dev = dev;
+        if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+            delete s;
+            *rc = SHMR_EC_DEVICE_ERROR;
+            return nullptr;
+        }
+    }
+    if (s->cap < bytes) {
+        if (s->dbuf) (void)hipFree(s->dbuf);
+        s->dbuf = nullptr;
+        s->cap = 0;
+        if (hipMalloc(reinterpret_cast<void**>(&s->dbuf), bytes) != hipSuccess) {
+            release(s);
+            *rc = SHMR_EC_OUT_OF_MEMORY;
+            return nullptr;
+        }
+        s->cap = bytes;
+    }
+    *rc = SHMR_EC_OK;
+    return s;
+}
+
+void StagingPool::release(Staging* s) {
+    std::lock_guard<std::mutex> lock(mu_);
+    free_[s->dev].push_back(s);
+}
+
+}  // namespace core
+}  // namespace shmr

@@ -1,0 +1,161 @@
+// Internal device-side core of the erasure path: tuning policy, plan images on
+// the device, launch sets over block batches, the per-device upload ring and
+// staging pool.  Used by the C ABI (ec_api.cpp) and the host-buffer pipeline
+// (host_engine.cpp).  Not part of the public interface.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "gf256.hpp"
+#include "gf_apply.hpp"
+#include "shmr_ec.h"
+
+namespace shmr {
+namespace core {
+
+using gf::Codec;
+using gf::Plan;
+
+#define SHMR_HIP_TRY(expr)                                 \
+    do {                                                   \
+        hipError_t _e = (expr);                            \
+        if (_e != hipSuccess) return SHMR_EC_DEVICE_ERROR; \
+    } while (0)
+
+// ---- tuning ---------------------------------------------------------------
+enum OpClass { kEncode = 0, kDecode = 1 };
+constexpr int kAuto = -2;
+
+int set_tuning(const char* key, int value);
+int get_tuning(const char* key);
+kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows);
+int grid_mode(OpClass op);
+
+// ---- devices --------------------------------------------------------------
+int device_count();
+int check_device(int dev);   // SHMR_EC_OK / NO_DEVICE / INVALID_ARGUMENT
+
+// Sets the calling thread's device for the scope, restoring the previous one.
+class DeviceScope {
+public:
+    explicit DeviceScope(int dev) {
+        ok_ = hipGetDevice(&prev_) == hipSuccess && hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceScope() {
+        if (ok_) (void)hipSetDevice(prev_);
+    }
+    bool ok() const { return ok_; }
+
+private:
+    int prev_ = 0;
+    bool ok_ = false;
+};
+
+// Device image of a plan, uploaded once per device (synchronously, on first
+// use) and kept for the codec's lifetime.
+int plan_on_device(Plan& plan, int dev, const uint8_t** out);
+uint32_t plan_tab_off(unsigned k, unsigned m);
+
+// ---- launches -----------------------------------------------------------------
+struct Layout {
+    const uint8_t* in_base;
+    uint8_t* out_base;
+    uint64_t in_bpitch, in_spitch, out_bpitch, out_spitch;
+    uint32_t out_bias;   // subtracted from plan out_idx (encode into a parity-only buffer)
+};
+
+// Blocks covered by one launch set: {first + j * stride} or, with d_list, the
+// device list d_list[j]; multi-plan sets also carry a per-block plan index into
+// the device table d_plans (all plans share k and m).
+struct BlockSet {
+    uint64_t first = 0, stride = 1, n = 0;
+    const uint32_t* d_list = nullptr;
+    const uint16_t* d_plan_idx = nullptr;
+    const uint8_t* const* d_plans = nullptr;
+};
+
+// Enqueues out = rows (x) in over a block set on the current device (= dev).
+int launch_set(Plan& shape, int dev, const Layout& L, const BlockSet& bs, uint64_t len, hipStream_t stream,
+               OpClass op);
+
+// Encode nblocks blocks laid out per `L` (plan = the codec's parity rows).
+int encode_on_device(Codec& c, int dev, const Layout& L, uint64_t nblocks, uint64_t len, hipStream_t stream);
+
+// Reconstruct in place: all shards of block b at base + b*block_pitch +
+// i*shard_pitch; present = host flags [nblocks][total].  Validates every block
+// before enqueueing anything.  Caller has set the device.
+int reconstruct_on_device(Codec& c, int dev, uint8_t* d_shards, uint64_t shard_pitch, uint64_t block_pitch,
+                          const uint8_t* present, uint64_t nblocks, uint64_t len, bool data_only,
+                          hipStream_t stream);
+
+// Validation shared by every reconstruct entry point.
+int validate_presence(const Codec& c, const uint8_t* present, uint64_t nblocks);
+
+// ---- per-device ring of pinned upload slots ------------------------------
+// Small per-call tables (block lists, per-block plan indices, plan pointer
+// tables).  A slot is reused only after the event recorded behind the
+// kernels that read it has completed.
+class UploadRing {
+public:
+    static constexpr int kSlots = 32;
+    static constexpr size_t kSlotBytes = 256 * 1024;
+    static UploadRing* for_device(int dev, int* rc);
+    int acquire(uint8_t** host, uint8_t** dev, int* slot);
+    int upload(int slot, size_t bytes, hipStream_t stream);
+    int release_after(int slot, hipStream_t stream);
+
+private:
+    void release_now(int slot);
+    uint8_t* host_ = nullptr;
+    uint8_t* dev_ = nullptr;
+    hipEvent_t ev_[kSlots] = {};
+    bool armed_[kSlots] = {};
+    bool inuse_[kSlots] = {};
+    int next_ = 0;
+    std::mutex mu_;
+    std::condition_variable cv_;
+};
+
+// ---- device staging for the single-call host-buffer entry points ---------
+struct Staging {
+    int dev = -1;
+    hipStream_t stream = nullptr;
+    uint8_t* dbuf = nullptr;
+    size_t cap = 0;
+};
+
+class StagingPool {
+public:
+    static StagingPool& get();
+    Staging* acquire(int dev, size_t bytes, int* rc);
+    void release(Staging* s);
+
+private:
+    std::mutex mu_;
+    std::map<int, std::vector<Staging*>> free_;
+};
+
+struct StagingLease {
+    Staging* s = nullptr;
+    ~StagingLease() {
+        if (s) StagingPool::get().release(s);
+    }
+};
+
+inline uint64_t round_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+
+}  // namespace core
+}  // namespace shmr
+
+struct shmr_ec {
+    std::shared_ptr<shmr::gf::Codec> codec;
+    std::atomic<int> device{0};
+};

@@ -1,0 +1,304 @@
+// Host-buffer batch engine: StorageBlocks that start and end in host memory
+// (the reference's Block Cache buffers / shard files), encoded or rebuilt on
+// one or more MI355X.  Whole blocks go round-robin to devices (block b ->
+// devices[b % ndev]); on each device a worker pipelines chunks of blocks
+// through NS staging sets so the H2D copy of chunk c+1, the kernel of chunk c
+// and the D2H copy of chunk c-1 overlap on separate streams.
+//
+// Host buffers in pinned memory (shmr_ec_host_alloc, the MI355X-native Block
+// Cache) are DMA'd directly; pageable buffers (plain Vec<u8>/malloc) are first
+// gathered into a pinned mirror by a crew of copy threads.
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "ec_core.hpp"
+#include "host_engine.hpp"
+
+namespace shmr {
+namespace core {
+
+namespace {
+
+// A crew of threads that runs batches of memcpy tasks in parallel (the caller
+// thread participates).  Lives for the duration of one device worker.
+class CopyCrew {
+public:
+    explicit CopyCrew(int n) {
+        for (int i = 1; i < n; ++i) th_.emplace_back([this] { loop(); });
+    }
+    ~CopyCrew() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    struct Task {
+        void* dst;
+        const void* src;
+        size_t n;
+    };
+    void run(std::vector<Task>& tasks) {
+        // split large copies into 1 MiB pieces for balance
+        pieces_.clear();
+        constexpr size_t kPiece = 1 << 20;
+        for (auto& t : tasks)
+            for (size_t off = 0; off < t.n; off += kPiece)
+                pieces_.push_back(Task{static_cast<uint8_t*>(t.dst) + off, static_cast<const uint8_t*>(t.src) + off,
+                                       std::min(kPiece, t.n - off)});
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            next_ = 0;
+            active_ = int(th_.size());
+            ++gen_;
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [this] { return active_ == 0; });
+    }
+
+private:
+    void work() {
+        for (;;) {
+            const size_t i = next_.fetch_add(1);
+            if (i >= pieces_.size()) break;
+            std::memcpy(pieces_[i].dst, pieces_[i].src, pieces_[i].n);
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+            }
+            work();
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--active_ == 0) done_cv_.notify_all();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::vector<Task> pieces_;
+    std::atomic<size_t> next_{0};
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    uint64_t gen_ = 0;
+    int active_ = 0;
+    bool stop_ = false;
+};
+
+bool is_pinned(const void* p) {
+    hipPointerAttribute_t attr{};
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();   // pageable memory reports an error: clear it
+        return false;
+    }
+    return attr.type == hipMemoryTypeHost;
+}
+
+struct StageSet {
+    uint8_t* dbuf = nullptr;   // [C][t][pitch] device
+    uint8_t* hbuf = nullptr;   // pinned mirror (pageable mode)
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    std::vector<size_t> blocks;   // global block ids of the chunk in flight
+    bool pending = false;
+};
+
+}  // namespace
+
+int copy_threads_default() {
+    const unsigned hw = std::thread::hardware_concurrency();
+    return int(std::max(1u, std::min(8u, hw ? hw : 1u)));
+}
+
+int run_host_job(const HostJob& job, const int* devices, int ndev) {
+    Codec& c = job.codec;
+    const unsigned k = c.k(), t = k + c.p();
+    const uint64_t len = job.len;
+    const uint64_t pitch = round_up(len, 256);
+    // Every block is validated before any device work starts.
+    if (job.op == kDecode) {
+        int rc = validate_presence(c, job.present, job.nblocks);
+        if (rc) return rc;
+    }
+    const bool pinned = is_pinned(job.host_shards[0]);
+    std::vector<int> results(size_t(ndev), SHMR_EC_OK);
+
+    auto worker = [&](int di) {
+        int& result = results[size_t(di)];
+        const int dev = devices[di];
+        DeviceScope scope(dev);
+        if (!scope.ok()) {
+            result = SHMR_EC_DEVICE_ERROR;
+            return;
+        }
+        std::vector<size_t> mine;
+        for (size_t b = size_t(di); b < job.nblocks; b += size_t(ndev)) mine.push_back(b);
+        if (mine.empty()) return;
+        const uint64_t block_bytes = uint64_t(t) * pitch;
+        const size_t C = std::max<size_t>(1, std::min<size_t>(mine.size(), size_t((job.chunk_bytes + block_bytes - 1) /
+                                                                                     block_bytes)));
+        constexpr int NS = 3;
+        StageSet sets[NS];
+        auto cleanup = [&] {
+            for (auto& s : sets) {
+                if (s.stream) (void)hipStreamSynchronize(s.stream);
+                if (s.done) (void)hipEventDestroy(s.done);
+                if (s.stream) (void)hipStreamDestroy(s.stream);
+                if (s.dbuf) (void)hipFree(s.dbuf);
+                if (s.hbuf) (void)hipHostFree(s.hbuf);
+            }
+        };
+        for (auto& s : sets) {
+            if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess ||
+                hipMalloc(reinterpret_cast<void**>(&s.dbuf), C * block_bytes) != hipSuccess ||
+                (!pinned && hipHostMalloc(reinterpret_cast<void**>(&s.hbuf), C * block_bytes, hipHostMallocDefault) !=
+                                hipSuccess)) {
+                result = SHMR_EC_OUT_OF_MEMORY;
+                cleanup();
+                return;
+            }
+        }
+        CopyCrew crew(pinned ? 1 : job.copy_threads);
+        std::vector<CopyCrew::Task> tasks;
+        std::vector<uint8_t> present;
+
+        // input / output shard indices of one block
+        auto io = [&](size_t b, std::vector<unsigned>& in, std::vector<unsigned>& out) {
+            in.clear();
+            out.clear();
+            if (job.op == kEncode) {
+                for (unsigned i = 0; i < k; ++i) in.push_back(i);
+                for (unsigned i = k; i < t; ++i) out.push_back(i);
+                return;
+            }
+            const uint8_t* pr = job.present + b * t;
+            unsigned np = 0;
+            for (unsigned i = 0; i < t; ++i) np += pr[i] ? 1 : 0;
+            if (np == t) return;   // nothing to rebuild
+            for (unsigned i = 0; i < t; ++i) {
+                if (pr[i]) {
+                    if (in.size() < k) in.push_back(i);
+                } else if (i < k || !job.data_only) {
+                    out.push_back(i);
+                }
+            }
+        };
+        std::vector<unsigned> in, out;
+        // staged mode: pinned mirror -> user output buffers of a finished chunk
+        auto drain = [&](StageSet& s) -> int {
+            if (!s.pending) return SHMR_EC_OK;
+            if (hipEventSynchronize(s.done) != hipSuccess) return SHMR_EC_DEVICE_ERROR;
+            s.pending = false;
+            if (pinned) return SHMR_EC_OK;
+            tasks.clear();
+            for (size_t j = 0; j < s.blocks.size(); ++j) {
+                io(s.blocks[j], in, out);
+                for (unsigned i : out)
+                    tasks.push_back({job.host_shards[s.blocks[j] * t + i], s.hbuf + (j * t + i) * pitch, len});
+            }
+            crew.run(tasks);
+            return SHMR_EC_OK;
+        };
+
+        size_t chunk = 0;
+        for (size_t c0 = 0; c0 < mine.size(); c0 += C, ++chunk) {
+            StageSet& s = sets[chunk % NS];
+            int rc = drain(s);
+            if (rc) {
+                result = rc;
+                break;
+            }
+            const size_t n = std::min(C, mine.size() - c0);
+            s.blocks.assign(mine.begin() + long(c0), mine.begin() + long(c0 + n));
+            // gather inputs (pageable: into the pinned mirror first)
+            if (!pinned) {
+                tasks.clear();
+                for (size_t j = 0; j < n; ++j) {
+                    io(s.blocks[j], in, out);
+                    for (unsigned i : in)
+                        tasks.push_back({s.hbuf + (j * t + i) * pitch, job.host_shards[s.blocks[j] * t + i], len});
+                }
+                crew.run(tasks);
+            }
+            for (size_t j = 0; j < n && rc == SHMR_EC_OK; ++j) {
+                io(s.blocks[j], in, out);
+                if (job.op == kEncode && !pinned) {   // k data shards are contiguous in the mirror
+                    if (hipMemcpyAsync(s.dbuf + j * block_bytes, s.hbuf + j * block_bytes, (k - 1) * pitch + len,
+                                       hipMemcpyHostToDevice, s.stream) != hipSuccess)
+                        rc = SHMR_EC_DEVICE_ERROR;
+                    continue;
+                }
+                for (unsigned i : in) {
+                    const uint8_t* src = pinned ? job.host_shards[s.blocks[j] * t + i] : s.hbuf + (j * t + i) * pitch;
+                    if (hipMemcpyAsync(s.dbuf + (j * t + i) * pitch, src, len, hipMemcpyHostToDevice, s.stream) !=
+                        hipSuccess)
+                        rc = SHMR_EC_DEVICE_ERROR;
+                }
+            }
+            // compute
+            if (rc == SHMR_EC_OK) {
+                if (job.op == kEncode) {
+                    const Layout L{s.dbuf, s.dbuf, block_bytes, pitch, block_bytes, pitch, 0};
+                    rc = encode_on_device(c, dev, L, n, len, s.stream);
+                } else {
+                    present.assign(n * t, 1);
+                    for (size_t j = 0; j < n; ++j)
+                        std::memcpy(present.data() + j * t, job.present + s.blocks[j] * t, t);
+                    rc = reconstruct_on_device(c, dev, s.dbuf, pitch, block_bytes, present.data(), n, len,
+                                               job.data_only, s.stream);
+                }
+            }
+            // outputs
+            for (size_t j = 0; j < n && rc == SHMR_EC_OK; ++j) {
+                io(s.blocks[j], in, out);
+                if (job.op == kEncode && !pinned) {   // p parity shards are contiguous too
+                    if (hipMemcpyAsync(s.hbuf + (j * t + k) * pitch, s.dbuf + (j * t + k) * pitch,
+                                       (t - k - 1) * pitch + len, hipMemcpyDeviceToHost, s.stream) != hipSuccess)
+                        rc = SHMR_EC_DEVICE_ERROR;
+                    continue;
+                }
+                for (unsigned i : out) {
+                    uint8_t* dst = pinned ? job.host_shards[s.blocks[j] * t + i] : s.hbuf + (j * t + i) * pitch;
+                    if (hipMemcpyAsync(dst, s.dbuf + (j * t + i) * pitch, len, hipMemcpyDeviceToHost, s.stream) !=
+                        hipSuccess)
+                        rc = SHMR_EC_DEVICE_ERROR;
+                }
+            }
+            if (rc == SHMR_EC_OK && hipEventRecord(s.done, s.stream) != hipSuccess) rc = SHMR_EC_DEVICE_ERROR;
+            s.pending = rc == SHMR_EC_OK;
+            if (rc) {
+                result = rc;
+                break;
+            }
+        }
+        for (auto& s : sets) {
+            const int rc = drain(s);
+            if (rc && result == SHMR_EC_OK) result = rc;
+        }
+        cleanup();
+    };
+
+    std::vector<std::thread> th;
+    for (int d = 1; d < ndev; ++d) th.emplace_back(worker, d);
+    worker(0);
+    for (auto& x : th) x.join();
+    for (int r : results)
+        if (r) return r;
+    return SHMR_EC_OK;
+}
+
+}  // namespace core
+}  // namespace shmr

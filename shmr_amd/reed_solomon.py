@@ -19,7 +19,8 @@ import numpy as np
 
 from ._native import _u8p, lib
 
-__all__ = ["Error", "ReedSolomon", "calculate_shard_size", "device_count", "set_tuning", "get_tuning", "describe_variant"]
+__all__ = ["Error", "ReedSolomon", "calculate_shard_size", "device_count", "set_tuning", "get_tuning", "describe_variant",
+           "PinnedBuffer"]
 
 
 class Error(Exception):
@@ -209,15 +210,49 @@ class ReedSolomon:
         _check(lib().shmr_ec_reconstruct_batch_dev(self._h, ctypes.c_void_p(shards.data_ptr()), shards.stride(1),
                                                    shards.stride(0), _ptr(pr), B, L, int(data_only), dev, stream))
 
-    def encode_blocks_host(self, blocks: Sequence[Sequence[np.ndarray]], devices: Sequence[int] = (0,)) -> None:
-        """Encode many host-resident blocks, whole blocks round-robin over devices."""
+    def _host_ptrs(self, blocks):
         t = self.total_shard_count()
-        arrs = [[_writable_u8(s) for s in blk] for blk in blocks]
+        arrs = [[(None if s is None else _writable_u8(s)) for s in blk] for blk in blocks]
         for blk in arrs:
             if len(blk) != t:
                 raise Error(-1 if len(blk) < t else -2)
-        L = arrs[0][0].size if arrs else 0
+        L = next((a.size for blk in arrs for a in blk if a is not None), 0)
         flat = [a for blk in arrs for a in blk]
-        ptrs = (_u8p * max(len(flat), 1))(*[_ptr(a) for a in flat])
+        ptrs = (_u8p * max(len(flat), 1))(*[(_ptr(a) if a is not None else _u8p()) for a in flat])
+        return arrs, L, ptrs
+
+    def encode_blocks_host(self, blocks: Sequence[Sequence[np.ndarray]], devices: Sequence[int] = (0,)) -> None:
+        """Encode many host-resident blocks (each a list of total shards; parity
+        overwritten), whole blocks round-robin over devices, pipelined."""
+        arrs, L, ptrs = self._host_ptrs(blocks)
         devs = (ctypes.c_int * len(devices))(*devices)
         _check(lib().shmr_ec_encode_blocks_host(self._h, ptrs, len(arrs), L, devs, len(devices)))
+
+    def reconstruct_blocks_host(self, blocks: Sequence[Sequence[np.ndarray]], present, data_only: bool = False,
+                                devices: Sequence[int] = (0,)) -> None:
+        """Rebuild absent shards of many host-resident blocks in place.
+        present: [nblocks][total] flags; absent shards need (writable) buffers."""
+        arrs, L, ptrs = self._host_ptrs(blocks)
+        pr = np.ascontiguousarray(present, dtype=np.uint8).reshape(len(arrs), self.total_shard_count())
+        devs = (ctypes.c_int * len(devices))(*devices)
+        _check(lib().shmr_ec_reconstruct_blocks_host(self._h, ptrs, _ptr(pr), len(arrs), L, int(data_only), devs,
+                                                     len(devices)))
+
+
+class PinnedBuffer:
+    """Page-locked host memory from shmr_ec_host_alloc (Block Cache buffers):
+    host-buffer entry points DMA it without a staging copy."""
+
+    def __init__(self, nbytes: int):
+        p = ctypes.c_void_p()
+        _check(lib().shmr_ec_host_alloc(nbytes, ctypes.byref(p)))
+        self._p = p
+        self.nbytes = nbytes
+        self.array = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint8)), shape=(nbytes,))
+
+    def __del__(self):
+        p = getattr(self, "_p", None)
+        if p:
+            self.array = None
+            lib().shmr_ec_host_free(p)
+            self._p = None
