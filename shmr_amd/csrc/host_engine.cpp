@@ -13,6 +13,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -109,11 +110,78 @@ bool is_pinned(const void* p) {
 struct StageSet {
     uint8_t* dbuf = nullptr;   // [C][t][pitch] device
     uint8_t* hbuf = nullptr;   // pinned mirror (pageable mode)
+    size_t dcap = 0, hcap = 0;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
     std::vector<size_t> blocks;   // global block ids of the chunk in flight
     bool pending = false;
 };
+
+constexpr int kStageSets = 3;
+
+// Staging sets of one device, kept across jobs (allocating hundreds of MB of
+// device and pinned memory per call would cost as much as the copies).  One
+// job per device at a time holds `mu`.
+struct DevicePipe {
+    std::mutex mu;
+    StageSet sets[kStageSets];
+    int ensure(size_t dbytes, size_t hbytes) {
+        for (auto& s : sets) {
+            if (!s.stream && (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
+                              hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess))
+                return SHMR_EC_DEVICE_ERROR;
+            if (s.dcap < dbytes) {
+                if (s.dbuf) (void)hipFree(s.dbuf);
+                s.dbuf = nullptr;
+                s.dcap = 0;
+                if (hipMalloc(reinterpret_cast<void**>(&s.dbuf), dbytes) != hipSuccess) return SHMR_EC_OUT_OF_MEMORY;
+                s.dcap = dbytes;
+            }
+            if (s.hcap < hbytes) {
+                if (s.hbuf) (void)hipHostFree(s.hbuf);
+                s.hbuf = nullptr;
+                s.hcap = 0;
+                if (hipHostMalloc(reinterpret_cast<void**>(&s.hbuf), hbytes, hipHostMallocDefault) != hipSuccess)
+                    return SHMR_EC_OUT_OF_MEMORY;
+                s.hcap = hbytes;
+            }
+            s.pending = false;
+            s.blocks.clear();
+        }
+        return SHMR_EC_OK;
+    }
+};
+
+DevicePipe& pipe_for(int dev) {
+    static std::mutex mu;
+    static auto* pipes = new std::map<int, DevicePipe*>;   // leaked: outlives static teardown
+    std::lock_guard<std::mutex> lock(mu);
+    auto& p = (*pipes)[dev];
+    if (!p) p = new DevicePipe;
+    return *p;
+}
+
+// Enqueues copies of shards idx[...] (ascending) of one block between host
+// pointers and the device block image (pitch apart).  Runs of shards that are
+// adjacent both in host memory and in the device image (pitch == len) become a
+// single hipMemcpyAsync.
+int copy_runs(uint8_t* const* host, const std::vector<unsigned>& idx, uint8_t* dev_block, uint64_t pitch,
+              uint64_t len, bool h2d, hipStream_t stream) {
+    size_t i = 0;
+    while (i < idx.size()) {
+        size_t j = i + 1;
+        while (j < idx.size() && idx[j] == idx[j - 1] + 1 && pitch == len &&
+               host[idx[j]] == host[idx[j - 1]] + len)
+            ++j;
+        const uint64_t bytes = uint64_t(j - i) * len;
+        uint8_t* d = dev_block + uint64_t(idx[i]) * pitch;
+        const hipError_t e = h2d ? hipMemcpyAsync(d, host[idx[i]], bytes, hipMemcpyHostToDevice, stream)
+                                 : hipMemcpyAsync(host[idx[i]], d, bytes, hipMemcpyDeviceToHost, stream);
+        if (e != hipSuccess) return SHMR_EC_DEVICE_ERROR;
+        i = j;
+    }
+    return SHMR_EC_OK;
+}
 
 }  // namespace
 
@@ -149,25 +217,18 @@ int run_host_job(const HostJob& job, const int* devices, int ndev) {
         const uint64_t block_bytes = uint64_t(t) * pitch;
         const size_t C = std::max<size_t>(1, std::min<size_t>(mine.size(), size_t((job.chunk_bytes + block_bytes - 1) /
                                                                                      block_bytes)));
-        constexpr int NS = 3;
-        StageSet sets[NS];
+        constexpr int NS = kStageSets;
+        DevicePipe& dp = pipe_for(dev);
+        std::lock_guard<std::mutex> pipe_lock(dp.mu);
+        StageSet* sets = dp.sets;
         auto cleanup = [&] {
-            for (auto& s : sets) {
-                if (s.stream) (void)hipStreamSynchronize(s.stream);
-                if (s.done) (void)hipEventDestroy(s.done);
-                if (s.stream) (void)hipStreamDestroy(s.stream);
-                if (s.dbuf) (void)hipFree(s.dbuf);
-                if (s.hbuf) (void)hipHostFree(s.hbuf);
-            }
+            for (int i = 0; i < NS; ++i)
+                if (sets[i].stream) (void)hipStreamSynchronize(sets[i].stream);
         };
-        for (auto& s : sets) {
-            if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
-                hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess ||
-                hipMalloc(reinterpret_cast<void**>(&s.dbuf), C * block_bytes) != hipSuccess ||
-                (!pinned && hipHostMalloc(reinterpret_cast<void**>(&s.hbuf), C * block_bytes, hipHostMallocDefault) !=
-                                hipSuccess)) {
-                result = SHMR_EC_OUT_OF_MEMORY;
-                cleanup();
+        {
+            const int rc = dp.ensure(C * block_bytes, pinned ? 0 : C * block_bytes);
+            if (rc) {
+                result = rc;
                 return;
             }
         }
@@ -241,10 +302,14 @@ int run_host_job(const HostJob& job, const int* devices, int ndev) {
                         rc = SHMR_EC_DEVICE_ERROR;
                     continue;
                 }
+                if (pinned) {
+                    rc = copy_runs(job.host_shards + s.blocks[j] * t, in, s.dbuf + j * block_bytes, pitch, len, true,
+                                   s.stream);
+                    continue;
+                }
                 for (unsigned i : in) {
-                    const uint8_t* src = pinned ? job.host_shards[s.blocks[j] * t + i] : s.hbuf + (j * t + i) * pitch;
-                    if (hipMemcpyAsync(s.dbuf + (j * t + i) * pitch, src, len, hipMemcpyHostToDevice, s.stream) !=
-                        hipSuccess)
+                    if (hipMemcpyAsync(s.dbuf + (j * t + i) * pitch, s.hbuf + (j * t + i) * pitch, len,
+                                       hipMemcpyHostToDevice, s.stream) != hipSuccess)
                         rc = SHMR_EC_DEVICE_ERROR;
                 }
             }
@@ -270,10 +335,14 @@ int run_host_job(const HostJob& job, const int* devices, int ndev) {
                         rc = SHMR_EC_DEVICE_ERROR;
                     continue;
                 }
+                if (pinned) {
+                    rc = copy_runs(job.host_shards + s.blocks[j] * t, out, s.dbuf + j * block_bytes, pitch, len,
+                                   false, s.stream);
+                    continue;
+                }
                 for (unsigned i : out) {
-                    uint8_t* dst = pinned ? job.host_shards[s.blocks[j] * t + i] : s.hbuf + (j * t + i) * pitch;
-                    if (hipMemcpyAsync(dst, s.dbuf + (j * t + i) * pitch, len, hipMemcpyDeviceToHost, s.stream) !=
-                        hipSuccess)
+                    if (hipMemcpyAsync(s.hbuf + (j * t + i) * pitch, s.dbuf + (j * t + i) * pitch, len,
+                                       hipMemcpyDeviceToHost, s.stream) != hipSuccess)
                         rc = SHMR_EC_DEVICE_ERROR;
                 }
             }
@@ -284,8 +353,8 @@ int run_host_job(const HostJob& job, const int* devices, int ndev) {
                 break;
             }
         }
-        for (auto& s : sets) {
-            const int rc = drain(s);
+        for (int i = 0; i < NS; ++i) {
+            const int rc = drain(sets[i]);
             if (rc && result == SHMR_EC_OK) result = rc;
         }
         cleanup();
