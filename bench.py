@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--tune", default="", help="kernel knobs, e.g. 'chunks=2,grid=0' (default: library defaults)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the cpu_baseline sample")
+    ap.add_argument("--backend", default="gloo", choices=["gloo", "nccl"],
+                    help="process group for the timing barrier / max-over-ranks only (the data path "
+                         "exchanges nothing between GPUs)")
     ap.add_argument("--ramp-seconds", type=float, default=0.5,
                     help="untimed device clock ramp before the warmup steps (MI355X needs ~0.1 s of "
                          "sustained load to reach its steady clock)")
@@ -66,12 +69,24 @@ def parse():
 
 def main():
     args = parse()
+    if args.gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} needs a torch.distributed.run launch with that many ranks")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    if local >= ndev:
+        # Rehearsal on a box with fewer GPUs than ranks (several ranks share a
+        # GPU) is opt-in only; a real N-GPU run maps rank -> its own GPU.
+        if os.environ.get("SHMR_BENCH_SHARE_GPU") != "1":
+            raise SystemExit(f"LOCAL_RANK {local} but only {ndev} GPU(s) visible")
+        local = local % ndev
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -151,7 +166,7 @@ def main():
     step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
     gpu_s = sum(step_ms) / 1e3
     elapsed = max(wall, gpu_s)
-    elapsed = placement.max_over_ranks(elapsed, device=dev)
+    elapsed = placement.max_over_ranks(elapsed, device=dev if args.backend == "nccl" else None)
 
     total_payload = payload_bytes_per_block * B * world * args.steps
     value = total_payload / elapsed / 2 ** 30
@@ -179,7 +194,8 @@ def main():
                          "encode42": "RS(4,2) encode, 1 MiB StorageBlocks, device-resident"}[args.config],
             "data_shards": k, "parity_shards": p, "shard_bytes": S, "blocks_per_gpu": B,
             "global_batch_blocks": B * world,
-            "parallelism": f"blocks round-robin over {world} GPU(s), no collectives",
+            "parallelism": f"blocks round-robin over {world} GPU(s), no data-path collectives "
+                           f"({args.backend} only for the timing barrier / max-over-ranks)",
             "tuning": tuning,
         },
         "roofline": {
