@@ -1,0 +1,176 @@
+// C++ host mirror of the reference's StorageBlock layer (src/vfs/{block,mod,path}.rs,
+// src/config.rs) around the MI355X codec.  Same types, method names and error
+// behaviour as the reference; the Erasure arms call shmr::ReedSolomon (GPU) and
+// VirtualFile::sync_data batches every Erasure block of a flush into one
+// pipelined GPU call (shmr_ec_encode_blocks_host) instead of one encode per
+// block.  Deviations from the reference are opt-in (VfsOptions).
+#pragma once
+
+#include <cstdint>
+#include <filesystem>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <optional>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "reed_solomon.hpp"
+
+namespace shmr {
+
+namespace fs = std::filesystem;
+
+constexpr uint64_t VIRTUAL_BLOCK_DEFAULT_SIZE = 1024 * 1024;   // src/vfs/path.rs:12
+constexpr uint64_t VFS_DEFAULT_BLOCK_SIZE = 4096;              // src/lib.rs:22 (the chunk size)
+constexpr const char* VP_DEFAULT_FILE_EXT = "bin";             // src/vfs/path.rs:14
+
+// ShmrError (src/config.rs:151-164).  FsError carries errno, EcError the crate code.
+struct ShmrError {
+    enum Kind {
+        InvalidPoolId,
+        InvalidBucketId,
+        OutOfSpace,
+        EndOfFile,
+        FsError,
+        EcError,
+        ShardOpened,
+        ShardMissing,
+        InvalidInodeType,
+        InodeNotExist,
+        BlockIndexOutOfBounds,
+    } kind;
+    int code = 0;   // errno for FsError, shmr_ec status for EcError
+    std::string what() const;
+};
+using Status = std::optional<ShmrError>;   // std::nullopt == Ok(())
+
+// BlockTopology (src/vfs/block.rs:22-98)
+struct BlockTopology {
+    enum Kind { Single, Mirror, Erasure } kind = Single;
+    uint8_t n = 0;                              // Mirror(n)
+    uint8_t version = 0, data = 0, parity = 0;  // Erasure(version, data, parity)
+    static BlockTopology single() { return {}; }
+    static BlockTopology mirror(uint8_t n) { return {Mirror, n, 0, 0, 0}; }
+    static BlockTopology erasure(uint8_t v, uint8_t d, uint8_t p) { return {Erasure, 0, v, d, p}; }
+    // BlockTopology::try_from(String); error text as the reference's.
+    static std::optional<BlockTopology> try_from(const std::string& value, std::string* err = nullptr);
+    std::string to_string() const;   // Display
+};
+
+// Bucket / ShmrFsConfig (src/config.rs:17-39, 100-139)
+enum class BucketPriority { Evacuate = 0, Ignore = 1, Deprioritize = 2, Normal = 3, Prioritize = 4 };
+struct Bucket {
+    fs::path path;
+    uint64_t capacity = 0;
+    uint64_t available = 0;
+    BucketPriority priority = BucketPriority::Normal;
+};
+struct ShmrFsConfig {
+    std::map<std::string, std::map<std::string, Bucket>> pools;   // pool -> bucket name -> bucket
+    std::string write_pool;
+    uint64_t block_size = VIRTUAL_BLOCK_DEFAULT_SIZE;
+    // select_buckets (src/config.rs:46-85): buckets above Ignore, sorted by
+    // (priority, available) ascending, repeated until `count`, first `count`.
+    // (The reference iterates a HashMap, so ties are unordered there; here
+    // ties keep bucket-name order.)
+    Status select_buckets(const std::string& pool, size_t count, std::vector<std::string>* out) const;
+};
+
+// VirtualPath (src/vfs/path.rs:20-83)
+struct VirtualPath {
+    std::string pool, bucket, filename;
+    // (file path, directory) -- the directory is the unused <bucket>/fn[0..2]/fn[2..4]
+    Status resolve(const ShmrFsConfig& cfg, fs::path* file, fs::path* dir) const;
+    Status create(const ShmrFsConfig& cfg) const;   // mkdir -p dir; create+truncate file
+    std::string to_string() const;
+};
+
+// Opt-in deviations from the reference (all off = reference behaviour).
+struct VfsOptions {
+    // load_block: a shard file that cannot be opened is an erasure (the
+    // reference fails in open_handles, block.rs:481-487).
+    bool missing_shard_is_erasure = false;
+    // load_block: read shards with pread at offset 0 (the reference reads from
+    // the handle's current cursor, so a second load after drop_buffer without
+    // drop_handles reads 0 bytes, block.rs:544).
+    bool pread_from_start = false;
+    // load_block: a shard whose length is not S is an erasure (the reference
+    // zero-pads it and keeps it present, block.rs:548-551).
+    bool short_shard_is_erasure = false;
+};
+
+// VirtualBlock (src/vfs/block.rs:119-634).  Copies share state, like the
+// reference's Arc<Mutex<..>> fields.
+class VirtualBlock {
+public:
+    uint64_t ino = 0;
+    uint64_t idx = 0;
+    uint64_t size = 0;
+    BlockTopology topology;
+    std::vector<VirtualPath> shards;
+
+    VirtualBlock();
+    static Status create(uint64_t ino, uint64_t idx, std::shared_ptr<const ShmrFsConfig> cfg, uint64_t size,
+                         BlockTopology topology, VirtualBlock* out);
+    static Status create_with_pool(uint64_t ino, uint64_t idx, const std::string& pool,
+                                   std::shared_ptr<const ShmrFsConfig> cfg, uint64_t size, BlockTopology topology,
+                                   VirtualBlock* out);
+    void populate(std::shared_ptr<const ShmrFsConfig> cfg) { cfg_ = std::move(cfg); }
+    void set_options(const VfsOptions& o) { opt_ = o; }
+
+    Status read(uint64_t pos, uint8_t* buf, size_t len, size_t* nread) const;
+    Status write(uint64_t pos, const uint8_t* buf, size_t len, size_t* nwritten) const;
+    Status sync_data(bool force) const;
+    Status drop_buffer() const;
+    Status drop_handles() const;
+
+    // Test hooks (the reference's tests read these fields directly).
+    std::vector<uint8_t> buffer_snapshot() const;
+    bool buffer_loaded() const;
+
+    // --- used by VirtualFile's batched flush ---
+    // For an Erasure block that needs syncing: the k+p shards exactly as the
+    // Erasure arm builds them before encode (block.rs:406-423).  false if the
+    // block has nothing to flush or is not Erasure.
+    bool erasure_shards_for_sync(bool force, std::vector<std::vector<uint8_t>>* shards, Status* st) const;
+    // Writes already-encoded shards to the shard files (block.rs:436-439).
+    Status write_shards(const std::vector<std::vector<uint8_t>>& shards) const;
+
+private:
+    struct State;
+    Status open_handles() const;
+    Status load_block() const;
+    std::shared_ptr<State> st_;
+    std::shared_ptr<const ShmrFsConfig> cfg_;
+    VfsOptions opt_;
+};
+
+// VirtualFile (src/vfs/mod.rs:35-272)
+class VirtualFile {
+public:
+    uint64_t ino = 0;
+    uint64_t size = 0;
+    uint64_t chunk_size = VFS_DEFAULT_BLOCK_SIZE;
+    std::vector<VirtualBlock> blocks;
+    uint64_t block_size = VIRTUAL_BLOCK_DEFAULT_SIZE;
+
+    static VirtualFile new_with(uint64_t ino, uint64_t size);
+    void populate(std::shared_ptr<const ShmrFsConfig> cfg);
+
+    Status read(uint64_t pos, uint8_t* buf, size_t len, size_t* nread) const;
+    Status write(uint64_t pos, const uint8_t* buf, size_t len, size_t* nwritten);
+    // sync_data (mod.rs:91-103): every block is flushed, errors reported after
+    // all were attempted.  Erasure blocks of the same (k, p) are encoded in
+    // one batched GPU call over `devices`.
+    Status sync_data(bool force, const std::vector<int>& devices = {0}) const;
+    Status drop_buffers() const;
+    Status replace_block(size_t block_idx, VirtualBlock new_block);
+
+private:
+    Status allocate_block();
+    std::shared_ptr<const ShmrFsConfig> cfg_;
+};
+
+}  // namespace shmr

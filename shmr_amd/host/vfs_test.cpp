@@ -1,0 +1,432 @@
+// Test driver for the C++ StorageBlock mirror (vfs.hpp).  Each case mirrors a
+// test of the reference (src/vfs/block.rs:647-812, src/vfs/mod.rs:322-370) or
+// exercises the MI355X Erasure arms.  Run by tests/test_host_cpp.py:
+//
+//   shmr_vfs_test <case> <bucket_dir> [input_file]
+//
+// Prints "PASS" and exits 0, or prints "FAIL: ..." and exits 1.  Erasure cases
+// also print one "SHARDS <block> <path>..." line per block so the Python side
+// can compare the shard files with the CPU oracle.
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <functional>
+#include <random>
+
+#include "vfs.hpp"
+
+using namespace shmr;
+
+namespace {
+
+struct Failure {
+    std::string msg;
+};
+
+#define CHECK(cond)                                                                     \
+    do {                                                                                \
+        if (!(cond)) throw Failure{std::string(#cond) + " (line " + std::to_string(__LINE__) + ")"}; \
+    } while (0)
+#define CHECK_OK(st)                                                                    \
+    do {                                                                                \
+        Status _s = (st);                                                               \
+        if (_s) throw Failure{std::string(#st) + " -> " + _s->what() + " (line " + std::to_string(__LINE__) + ")"}; \
+    } while (0)
+
+std::string g_bucket;
+std::string g_input;
+std::mt19937_64 g_rng(0x53484D52);
+
+// get_shmr_config (src/lib.rs tests): one bucket "bucket1" in pool "test_pool".
+std::shared_ptr<const ShmrFsConfig> test_config() {
+    auto cfg = std::make_shared<ShmrFsConfig>();
+    Bucket b;
+    b.path = g_bucket;
+    b.capacity = 999;
+    b.available = 999;
+    cfg->pools["test_pool"]["bucket1"] = b;
+    cfg->write_pool = "test_pool";
+    return cfg;
+}
+
+std::vector<uint8_t> random_data(size_t n) {   // config.rs random_data
+    std::vector<uint8_t> v(n);
+    for (auto& x : v) x = uint8_t(g_rng());
+    return v;
+}
+
+std::vector<uint8_t> read_input() {
+    std::ifstream f(g_input, std::ios::binary);
+    return std::vector<uint8_t>((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+}
+
+fs::path shard_file(const ShmrFsConfig& cfg, const VirtualBlock& b, size_t i) {
+    fs::path p;
+    CHECK_OK(b.shards[i].resolve(cfg, &p, nullptr));
+    return p;
+}
+
+uint64_t fsize(const fs::path& p) { return fs::file_size(p); }
+
+std::vector<uint8_t> read_file(const fs::path& p, size_t n) {
+    std::vector<uint8_t> v(n);
+    FILE* f = std::fopen(p.c_str(), "rb");
+    CHECK(f != nullptr);
+    const size_t got = std::fread(v.data(), 1, n, f);
+    std::fclose(f);
+    CHECK(got == n);   // read_exact
+    return v;
+}
+
+void print_shards(const ShmrFsConfig& cfg, size_t idx, const VirtualBlock& b) {
+    std::printf("SHARDS %zu", idx);
+    for (size_t i = 0; i < b.shards.size(); ++i) std::printf(" %s", shard_file(cfg, b, i).c_str());
+    std::printf("\n");
+}
+
+// ---- reference tests -------------------------------------------------------
+
+void test_block_topology_try_from() {   // block.rs:647-659
+    auto t = BlockTopology::try_from("Erasure(1, 3, 2)");
+    CHECK(t && t->kind == BlockTopology::Erasure && t->version == 1 && t->data == 3 && t->parity == 2);
+    auto m = BlockTopology::try_from("Mirror(3)");
+    CHECK(m && m->kind == BlockTopology::Mirror && m->n == 3);
+    auto s = BlockTopology::try_from("Single()");
+    CHECK(s && s->kind == BlockTopology::Single);
+    std::string err;
+    CHECK(!BlockTopology::try_from("Single", &err) && err == "'Single' does not have '('");
+    CHECK(!BlockTopology::try_from("Erasure(1, x, 2)", &err) && err == "Unable to parse data shards");
+    CHECK(!BlockTopology::try_from("Raid(5)", &err));
+    CHECK(BlockTopology::erasure(1, 8, 3).to_string() == "Erasure(1, 8, 3)");
+    auto rt = BlockTopology::try_from(BlockTopology::erasure(1, 8, 3).to_string());
+    CHECK(rt && rt->data == 8 && rt->parity == 3);
+}
+
+void test_virtual_block_new_block() {   // block.rs:661-675
+    auto cfg = test_config();
+    VirtualBlock b;
+    CHECK_OK(VirtualBlock::create(1, 0, cfg, 1024, BlockTopology::single(), &b));
+    for (size_t i = 0; i < b.shards.size(); ++i) CHECK(fs::exists(shard_file(*cfg, b, i)));
+    CHECK(b.shards[0].filename == "1:0_single_0.bin");
+    fs::path dir;
+    CHECK_OK(b.shards[0].resolve(*cfg, nullptr, &dir));
+    CHECK(fs::is_directory(dir));   // <bucket>/1:/0_ is created (unused by the file)
+}
+
+void unbuffered_common(bool read_back) {   // block.rs:677-744
+    auto cfg = test_config();
+    VirtualBlock b;
+    CHECK_OK(VirtualBlock::create(3, 0, cfg, 1024, BlockTopology::single(), &b));
+    const fs::path sp = shard_file(*cfg, b, 0);
+    auto data = random_data(500);
+    size_t n = 0;
+    CHECK_OK(b.write(0, data.data(), data.size(), &n));
+    CHECK(n == 500);
+    CHECK_OK(b.sync_data(true));
+    CHECK(fsize(sp) == data.size());
+    CHECK_OK(b.drop_buffer());
+    CHECK(!b.buffer_loaded());
+    CHECK(b.buffer_snapshot().empty());
+    if (!read_back) {
+        CHECK(read_file(sp, 500) == data);
+        return;
+    }
+    std::vector<uint8_t> rb(500);
+    CHECK_OK(b.read(0, rb.data(), rb.size(), &n));
+    CHECK(n == 500);
+    CHECK(rb == data);
+}
+
+void test_virtual_block_unbuffered_backing() { unbuffered_common(false); }
+void test_virtual_block_unbuffered() { unbuffered_common(true); }
+
+void test_virtual_block_buffered() {   // block.rs:746-797
+    auto cfg = test_config();
+    VirtualBlock b;
+    CHECK_OK(VirtualBlock::create(5, 0, cfg, 1024, BlockTopology::single(), &b));
+    const fs::path sp = shard_file(*cfg, b, 0);
+    auto data = random_data(420);
+    size_t n = 0;
+    CHECK_OK(b.write(0, data.data(), data.size(), &n));
+    CHECK(fsize(sp) == 0);
+    {
+        auto buf = b.buffer_snapshot();
+        CHECK(buf.size() == data.size());
+        CHECK(std::equal(data.begin(), data.end(), buf.begin()));
+    }
+    std::vector<uint8_t> rb(data.size());
+    CHECK_OK(b.read(0, rb.data(), rb.size(), &n));
+    CHECK(n == data.size());
+    auto data2 = random_data(420);
+    CHECK_OK(b.write(0, data2.data(), data2.size(), &n));
+    CHECK_OK(b.read(0, rb.data(), rb.size(), &n));
+    CHECK(rb == data2);
+    CHECK(fsize(sp) == 0);
+    CHECK_OK(b.sync_data(true));
+    CHECK(read_file(sp, 420) == data2);
+    CHECK(fsize(sp) == 1024);   // load_block grew the buffer to `size` before the flush
+}
+
+void test_virtual_block_erasure_buffered() {   // block.rs:799-811 (a Single block there too)
+    auto cfg = test_config();
+    VirtualBlock b;
+    CHECK_OK(VirtualBlock::create(7, 0, cfg, 1024, BlockTopology::single(), &b));
+    auto data = random_data(500);
+    size_t n = 0;
+    CHECK_OK(b.write(0, data.data(), data.size(), &n));
+    std::vector<uint8_t> rb(250);
+    CHECK_OK(b.read(0, rb.data(), rb.size(), &n));
+    CHECK(std::equal(rb.begin(), rb.end(), data.begin()));
+}
+
+void test_block_errors() {
+    auto cfg = test_config();
+    VirtualBlock b;
+    CHECK_OK(VirtualBlock::create(9, 0, cfg, 1024, BlockTopology::single(), &b));
+    std::vector<uint8_t> buf(2048);
+    size_t n = 0;
+    Status st = b.write(1000, buf.data(), 100, &n);   // pos + len > size
+    CHECK(st && st->kind == ShmrError::OutOfSpace);
+    CHECK_OK(b.read(0, buf.data(), 0, &n));            // zero-length read: Ok(0), nothing loaded
+    CHECK(n == 0 && !b.buffer_loaded());
+    Status sp = VirtualBlock::create(9, 1, cfg, 1024, BlockTopology::single(), &b);
+    CHECK(!sp);
+    VirtualBlock bad;
+    st = VirtualBlock::create_with_pool(9, 2, "nope", cfg, 1024, BlockTopology::single(), &bad);
+    CHECK(st && st->kind == ShmrError::InvalidPoolId);
+    // select_buckets repeats the single bucket for every shard
+    VirtualBlock ec;
+    CHECK_OK(VirtualBlock::create(9, 3, cfg, 1024, BlockTopology::erasure(1, 4, 2), &ec));
+    CHECK(ec.shards.size() == 6 && ec.shards[5].filename == "9:3_ec42_5.bin");
+    // no GPU work: an Erasure block with an empty buffer flushes nothing
+    CHECK_OK(ec.sync_data(true));
+    CHECK(fsize(shard_file(*cfg, ec, 0)) == 0);
+}
+
+void test_virtual_file_1() {   // mod.rs:322-349
+    auto cfg = test_config();
+    VirtualFile vf = VirtualFile::new_with(g_rng() >> 16, 0);
+    vf.populate(cfg);
+    auto data = random_data(7000);
+    size_t n = 0;
+    CHECK_OK(vf.write(0, data.data(), data.size(), &n));
+    CHECK(n == 7000);
+    CHECK(vf.size == 7000);
+    CHECK(vf.blocks.size() == 1);
+    for (size_t i = 0; i < vf.blocks.size(); ++i) {
+        std::vector<uint8_t> buf(vf.chunk_size);
+        CHECK_OK(vf.blocks[i].read(0, buf.data(), buf.size(), &n));
+        CHECK(n == vf.chunk_size);
+        const size_t s = i * vf.chunk_size, e = std::min<size_t>(s + vf.chunk_size, data.size());
+        CHECK(std::equal(buf.begin(), buf.end(), data.begin() + s) && e - s == buf.size());
+    }
+    std::vector<uint8_t> buf(7000);
+    CHECK_OK(vf.read(0, buf.data(), buf.size(), &n));
+    CHECK(n == 7000);
+    CHECK(buf == data);
+}
+
+void test_virtual_file_2_4_mb() {   // mod.rs:351-370
+    auto cfg = test_config();
+    VirtualFile vf = VirtualFile::new_with(g_rng() >> 16, 0);
+    vf.populate(cfg);
+    auto data = random_data(2 * 1024 * 1024);
+    size_t n = 0;
+    CHECK_OK(vf.write(0, data.data(), data.size(), &n));
+    CHECK(vf.size == 2 * 1024 * 1024);
+    CHECK(vf.blocks.size() == 3);   // the trailing empty chunk allocates a third block
+    CHECK_OK(vf.sync_data(true));
+    auto f = read_file(shard_file(*cfg, vf.blocks[0], 0), 1024 * 1024);
+    CHECK(std::equal(f.begin(), f.end(), data.begin()));
+}
+
+void test_virtual_file_errors() {
+    auto cfg = test_config();
+    VirtualFile vf = VirtualFile::new_with(77, 0);
+    size_t n = 0;
+    std::vector<uint8_t> buf(16);
+    Status st = vf.write(0, buf.data(), buf.size(), &n);
+    CHECK(st && st->kind == ShmrError::FsError);   // config not populated (a panic in the reference)
+    vf.populate(cfg);
+    CHECK_OK(vf.read(0, buf.data(), buf.size(), &n));   // size 0: Ok(0)
+    CHECK(n == 0);
+    CHECK_OK(vf.write(0, buf.data(), buf.size(), &n));
+    st = vf.read(100, buf.data(), buf.size(), &n);
+    CHECK(st && st->kind == ShmrError::EndOfFile);
+    st = vf.replace_block(5, VirtualBlock());
+    CHECK(st && st->kind == ShmrError::BlockIndexOutOfBounds);
+}
+
+// ---- MI355X Erasure arms (GPU) ---------------------------------------------
+
+// Erasure(1, k, p) block: write the input, sync (GPU encode), print the shard
+// files; then drop and load it back, with erasures per the reference's rules
+// (a shard truncated to 0 bytes is zero-padded and kept present).
+void test_erasure_block_sync_load() {
+    auto cfg = test_config();
+    auto in = read_input();
+    VirtualBlock b;
+    const uint64_t size = 1024 * 1024;
+    CHECK_OK(VirtualBlock::create(11, 0, cfg, size, BlockTopology::erasure(1, 8, 3), &b));
+    size_t n = 0;
+    CHECK(in.size() <= size);
+    CHECK_OK(b.write(0, in.data(), in.size(), &n));
+    CHECK_OK(b.sync_data(true));
+    print_shards(*cfg, 0, b);
+    CHECK_OK(b.drop_buffer());
+    CHECK_OK(b.drop_handles());
+    // intact load
+    std::vector<uint8_t> rb(size);
+    CHECK_OK(b.read(0, rb.data(), rb.size(), &n));
+    CHECK(n == size);
+    CHECK(std::equal(in.begin(), in.end(), rb.begin()));
+    for (size_t i = in.size(); i < size; ++i) CHECK(rb[i] == 0);
+    // reference rule: truncate data shard 1 -> zero-padded, present
+    CHECK_OK(b.drop_buffer());
+    CHECK_OK(b.drop_handles());
+    fs::resize_file(shard_file(*cfg, b, 1), 0);
+    CHECK_OK(b.read(0, rb.data(), rb.size(), &n));
+    auto snap = b.buffer_snapshot();
+    std::printf("LOADED_TRUNCATED %zu\n", snap.size());
+    FILE* f = std::fopen((g_bucket + "/loaded_truncated.bin").c_str(), "wb");
+    std::fwrite(snap.data(), 1, snap.size(), f);
+    std::fclose(f);
+}
+
+// Opt-in rule: missing shard files are erasures; 3 of 11 removed -> exact data.
+void test_erasure_block_missing_shards() {
+    auto cfg = test_config();
+    auto in = read_input();
+    const uint64_t size = 1024 * 1024;
+    VirtualBlock b;
+    CHECK_OK(VirtualBlock::create(12, 0, cfg, size, BlockTopology::erasure(1, 8, 3), &b));
+    VfsOptions o;
+    o.missing_shard_is_erasure = true;
+    o.short_shard_is_erasure = true;
+    o.pread_from_start = true;
+    b.set_options(o);
+    size_t n = 0;
+    CHECK_OK(b.write(0, in.data(), in.size(), &n));
+    CHECK_OK(b.sync_data(true));
+    const fs::path keep0 = shard_file(*cfg, b, 0);
+    CHECK_OK(b.drop_buffer());
+    CHECK_OK(b.drop_handles());
+    fs::remove(shard_file(*cfg, b, 0));
+    fs::remove(shard_file(*cfg, b, 5));
+    fs::resize_file(shard_file(*cfg, b, 9), 17);   // short -> erasure
+    std::vector<uint8_t> rb(size);
+    CHECK_OK(b.read(0, rb.data(), rb.size(), &n));
+    CHECK(std::equal(in.begin(), in.end(), rb.begin()));
+    // the flush rewrote (repaired) every shard; now lose one more than parity
+    CHECK_OK(b.drop_buffer());
+    CHECK_OK(b.drop_handles());
+    CHECK(fs::exists(keep0) && fsize(keep0) == calculate_shard_size(size, 8));
+    for (size_t i : {1, 2, 3, 4}) fs::remove(shard_file(*cfg, b, i));
+    // without the option a missing file fails in open_handles (block.rs:481-487)
+    VirtualBlock strict;
+    strict.ino = b.ino;
+    strict.idx = b.idx;
+    strict.size = b.size;
+    strict.topology = b.topology;
+    strict.shards = b.shards;
+    strict.populate(cfg);
+    Status st = strict.read(0, rb.data(), rb.size(), &n);
+    CHECK(st && st->kind == ShmrError::FsError && st->code == ENOENT);
+    // with it, 4 erasures > 3 parity: the crate's TooFewShardsPresent
+    st = b.read(0, rb.data(), rb.size(), &n);
+    CHECK(st && st->kind == ShmrError::EcError && st->code == SHMR_EC_TOO_FEW_SHARDS_PRESENT);
+}
+
+// VirtualFile with Erasure blocks: one batched GPU encode per flush.
+void test_virtual_file_erasure_batch() {
+    auto cfg = test_config();
+    auto in = read_input();
+    const uint64_t bs = 1024 * 1024;
+    const size_t nblk = in.size() / bs;
+    CHECK(nblk * bs == in.size() && nblk > 0);
+    VirtualFile vf = VirtualFile::new_with(13, 0);
+    vf.populate(cfg);
+    for (size_t i = 0; i < nblk; ++i) {
+        VirtualBlock b;
+        CHECK_OK(VirtualBlock::create(13, i + 1, cfg, bs, BlockTopology::erasure(1, 8, 3), &b));
+        vf.blocks.push_back(b);
+    }
+    size_t n = 0;
+    CHECK_OK(vf.write(0, in.data(), in.size(), &n));
+    CHECK(n == in.size());
+    CHECK(vf.blocks.size() == nblk + 1);   // trailing empty chunk -> one Single block
+    CHECK_OK(vf.sync_data(true));
+    for (size_t i = 0; i < nblk; ++i) print_shards(*cfg, i, vf.blocks[i]);
+    CHECK_OK(vf.drop_buffers());
+    for (auto& b : vf.blocks) CHECK_OK(b.drop_handles());
+    std::vector<uint8_t> rb(in.size());
+    CHECK_OK(vf.read(0, rb.data(), rb.size(), &n));
+    CHECK(rb == in);
+}
+
+// replace_block: Single -> Erasure(1, 4, 2) migration (mod.rs:244-271)
+void test_replace_block_erasure() {
+    auto cfg = test_config();
+    VirtualFile vf = VirtualFile::new_with(14, 0);
+    vf.populate(cfg);
+    auto data = read_input();
+    size_t n = 0;
+    CHECK(data.size() < vf.block_size);
+    CHECK_OK(vf.write(0, data.data(), data.size(), &n));
+    VirtualBlock ec;
+    CHECK_OK(VirtualBlock::create(14, 99, cfg, vf.block_size, BlockTopology::erasure(1, 4, 2), &ec));
+    CHECK_OK(vf.replace_block(0, ec));
+    print_shards(*cfg, 0, vf.blocks[0]);
+    CHECK_OK(vf.blocks[0].drop_buffer());
+    CHECK_OK(vf.blocks[0].drop_handles());
+    std::vector<uint8_t> rb(data.size());
+    CHECK_OK(vf.read(0, rb.data(), rb.size(), &n));
+    CHECK(rb == data);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc < 3) {
+        std::fprintf(stderr, "usage: %s <case> <bucket_dir> [input]\n", argv[0]);
+        return 2;
+    }
+    const std::string name = argv[1];
+    g_bucket = argv[2];
+    if (argc > 3) g_input = argv[3];
+    static const std::map<std::string, std::function<void()>> cases = {
+        {"block_topology_try_from", test_block_topology_try_from},
+        {"virtual_block_new_block", test_virtual_block_new_block},
+        {"virtual_block_unbuffered_backing", test_virtual_block_unbuffered_backing},
+        {"virtual_block_unbuffered", test_virtual_block_unbuffered},
+        {"virtual_block_buffered", test_virtual_block_buffered},
+        {"virtual_block_erasure_buffered", test_virtual_block_erasure_buffered},
+        {"block_errors", test_block_errors},
+        {"virtual_file_1", test_virtual_file_1},
+        {"virtual_file_2_4_mb", test_virtual_file_2_4_mb},
+        {"virtual_file_errors", test_virtual_file_errors},
+        {"erasure_block_sync_load", test_erasure_block_sync_load},
+        {"erasure_block_missing_shards", test_erasure_block_missing_shards},
+        {"virtual_file_erasure_batch", test_virtual_file_erasure_batch},
+        {"replace_block_erasure", test_replace_block_erasure},
+    };
+    auto it = cases.find(name);
+    if (it == cases.end()) {
+        std::printf("FAIL: unknown case %s\n", name.c_str());
+        return 1;
+    }
+    try {
+        it->second();
+    } catch (const Failure& f) {
+        std::printf("FAIL: %s\n", f.msg.c_str());
+        return 1;
+    } catch (const std::exception& e) {
+        std::printf("FAIL: exception %s\n", e.what());
+        return 1;
+    }
+    std::printf("PASS\n");
+    return 0;
+}
