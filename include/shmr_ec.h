@@ -167,10 +167,13 @@ int shmr_ec_set_device(shmr_ec_t* rs, int device);
  * per lane per tile: 1, 2, 4), "nt_load", "nt_store" (nontemporal 0/1),
  * "scalar_tabs" (0/1), "occ8" (0/1), "grid" (-1 one workgroup per tile,
  * 0 balanced persistent grid, >0 capped persistent grid), "threads" (lanes
- * per workgroup: 128, 256, 512), "diag" (0/1:
+ * per workgroup: 128, 256, 512), "depth" (register ring depth = shards of
+ * loads in flight + 1: 1, 2, 3, 5, 9), "wgs_per_cu" (0 = no cap, else the
+ * most workgroups resident per CU, enforced by LDS padding), "occ" (0, 6, 7:
+ * register budget for that many waves per SIMD), "diag" (0/1:
  * XOR-only diagnostic kernel, WRONG results, for ceiling measurements).
  * Prefix "encode." or "decode." to set one operation class only.
- * "chunks", "nt_load" and "nt_store" default to -2 (auto): a per-shape policy
+ * "chunks", "nt_load", "nt_store", "depth" and "occ" default to -2 (auto): a per-shape policy
  * of the fastest variants measured on MI355X; any other value pins the knob,
  * and setting -2 returns it to the policy. */
 int shmr_ec_set_tuning(const char* key, int value);

@@ -24,17 +24,26 @@ struct Tuning {
     std::atomic<int> grid{-1};     // -1: one workgroup per tile
     std::atomic<int> diag{0};
     std::atomic<int> threads{256};
+    std::atomic<int> depth{kAuto};
+    std::atomic<int> wgs_per_cu{0};
+    std::atomic<int> occ{kAuto};
 };
 Tuning g_tune[2];   // [kEncode], [kDecode]
 
-// Measured: encode RS(8,3): NT loads+stores, U=1 (78 % of HBM peak); RS(4,2):
-// NT stores only (77 % vs 72 % with NT loads); RS(10,4) (4 rows per launch):
-// U=2 (71 % vs 66 %); reconstruct: NT loads+stores, U=1.
+// Measured (tools/tune.py, interleaved A/B in one process): a register ring
+// of depth 2 (one shard of loads in flight per wave) beats depth 3 on every
+// shape -- RS(8,3) encode 80 % vs 78 % of HBM peak (it also frees the VGPRs
+// that lift RS(8,3) from 5 to 6 waves/SIMD), RS(4,2) 78 % vs 77 %, RS(10,4)
+// 71 % vs 70 %, reconstruct RS(8,3) 72 % vs 71 %; deeper rings (5, 9) and
+// occupancy caps lose.  With depth 2, NT loads + NT stores win everywhere;
+// encodes with 4 rows per launch (RS(10,4)) use U = 2.
 kern::Variant variant_policy(OpClass op, unsigned k, unsigned rows) {
+    (void)k;
     kern::Variant v;
     v.u = (op == kEncode && rows >= 4) ? 2 : 1;
     v.nt_store = true;
-    v.nt_load = op == kDecode || k >= 8;
+    v.nt_load = true;
+    v.depth = 2;
     return v;
 }
 
@@ -82,6 +91,15 @@ int set_tuning(const char* key, int value) {
         } else if (k == "threads") {
             if (value != 128 && value != 256 && value != 512) return SHMR_EC_INVALID_ARGUMENT;
             T.threads = value;
+        } else if (k == "depth") {
+            if (value != 1 && value != 2 && value != 3 && value != 5 && value != 9 && value != kAuto) return SHMR_EC_INVALID_ARGUMENT;
+            T.depth = value;
+        } else if (k == "wgs_per_cu") {
+            if (value < 0 || value > 32) return SHMR_EC_INVALID_ARGUMENT;
+            T.wgs_per_cu = value;
+        } else if (k == "occ") {
+            if (value != 0 && value != 6 && value != 7 && value != kAuto) return SHMR_EC_INVALID_ARGUMENT;
+            T.occ = value;
         } else {
             return SHMR_EC_INVALID_ARGUMENT;
         }
@@ -102,6 +120,9 @@ int get_tuning(const char* key) {
     if (k == "grid") return T.grid;
     if (k == "diag") return T.diag;
     if (k == "threads") return T.threads;
+    if (k == "depth") return T.depth;
+    if (k == "wgs_per_cu") return T.wgs_per_cu;
+    if (k == "occ") return T.occ;
     return SHMR_EC_INVALID_ARGUMENT;
 }
 
@@ -115,6 +136,9 @@ kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows) {
     v.occ8 = T.occ8.load() != 0;
     v.diag = T.diag.load() != 0;
     v.threads = T.threads.load();
+    if (T.depth.load() != kAuto) v.depth = T.depth.load();
+    v.wgs_per_cu = T.wgs_per_cu.load();
+    if (T.occ.load() != kAuto) v.occ = T.occ.load();
     return v;
 }
 

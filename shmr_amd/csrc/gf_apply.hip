@@ -43,6 +43,23 @@ constexpr int kOcc8 = 8;         // ask for 8 waves / SIMD (<= 64 VGPRs)
 constexpr int kDiagXor = 16;     // diagnostics: XOR without GF multiply (wrong results)
 constexpr int kTh128 = 32;       // 128-lane workgroups (default 256)
 constexpr int kTh512 = 64;       // 512-lane workgroups
+constexpr int kDepth5 = 128;     // 4 shards of loads in flight (default 2)
+constexpr int kDepth9 = 256;     // 8 shards of loads in flight
+constexpr int kDepth2 = 512;     // 1 shard of loads in flight
+constexpr int kDepth1 = 1024;    // no look-ahead (load, wait, multiply)
+// Bits 12-15: occupancy target in waves per SIMD (0 = compiler's choice);
+// the register allocator must then fit 512 / target VGPRs.
+constexpr int kOccShift = 12;
+
+template <int F>
+constexpr int occ_of() {
+    return (F & kOcc8) ? 8 : ((F >> kOccShift) & 15);
+}
+
+template <int F>
+constexpr int depth_of() {
+    return (F & kDepth9) ? 9 : (F & kDepth5) ? 5 : (F & kDepth2) ? 2 : (F & kDepth1) ? 1 : 3;
+}
 
 template <int F>
 constexpr int threads_of() {
@@ -52,6 +69,22 @@ constexpr int threads_of() {
 struct Tab {
     uint32_t t0lo, t0hi, t1lo, t1hi, t2;
 };
+
+// Constant address space: wave-uniform loads through these are scalar
+// (s_load, lgkmcnt) even though the kernel stores through other pointers --
+// generic loads would be vector loads on the vmcnt queue of the data stream.
+typedef __attribute__((address_space(4))) const uint32_t cu32;
+template <class T>
+__device__ __forceinline__ const T* as_const(const void* p) {
+    return (const T*)(uintptr_t)p;
+}
+
+// Element i of the plan's u16 index array (4-byte aligned base) via a scalar
+// dword load (gfx9 has no 16-bit scalar loads).
+__device__ __forceinline__ uint32_t plan_u16(const uint16_t* base, uint32_t i) {
+    const uint32_t w = as_const<cu32>(base)[i >> 1];
+    return (i & 1) ? (w >> 16) : (w & 0xffffu);
+}
 
 // acc ^= c (x) w for the four bytes of w, given w's three selector words.
 // v_perm_b32(src0=hi, src1=lo, sel): selector byte n picks byte n of {hi:lo};
@@ -158,7 +191,7 @@ __device__ __forceinline__ void read_tabs(const ApplyArgs& a, const Ctx& c, uint
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if constexpr ((F & kScalarTabs) != 0) {
-            const uint32_t* e = c.g_tab + (size_t(t) * a.m + a.row0 + r) * 8;
+            const cu32* e = as_const<cu32>(c.g_tab) + (size_t(t) * a.m + a.row0 + r) * 8;
             tb[r] = Tab{e[0], e[1], e[2], e[3], e[4]};
         } else {
             const u32x4 v = c.s_tab[(size_t(t) * R + r) * 2];
@@ -170,13 +203,14 @@ __device__ __forceinline__ void read_tabs(const ApplyArgs& a, const Ctx& c, uint
 
 template <int F>
 __device__ __forceinline__ uint64_t in_off(const ApplyArgs& a, const Ctx& c, uint32_t t) {
-    if constexpr ((F & kScalarTabs) != 0) return uint64_t(c.g_in_idx[t]) * a.in_spitch;
+    if constexpr ((F & kScalarTabs) != 0) return uint64_t(plan_u16(c.g_in_idx, t)) * a.in_spitch;
     else return c.s_in_off[t];
 }
 
 template <int F>
 __device__ __forceinline__ uint64_t out_off(const ApplyArgs& a, const Ctx& c, uint32_t r) {
-    if constexpr ((F & kScalarTabs) != 0) return uint64_t(c.g_out_idx[a.row0 + r] - a.out_bias) * a.out_spitch;
+    if constexpr ((F & kScalarTabs) != 0)
+        return uint64_t(plan_u16(c.g_in_idx, a.k + a.row0 + r) - a.out_bias) * a.out_spitch;
     else return c.s_out_off[r];
 }
 
@@ -219,23 +253,25 @@ __device__ __forceinline__ void do_tile(const ApplyArgs& a, const Ctx& c, const 
     // sched_barrier(0) pins program order: without it the scheduler sinks the
     // look-ahead loads next to their consumers and the wave drains vmcnt(0)
     // every shard (no overlap of HBM latency with the GF math).
-    u32x4 A[U], B[U], C[U];
-    load(A, 0);
-    load(B, 1);
+    //
+    // Ring of NB register buffers, unrolled by NB so buffer indices are
+    // compile-time: while shard t is multiplied the loads of shards
+    // t+1 .. t+NB-1 are in flight.  Every load is unconditional (a branch
+    // around a load makes the compiler's waitcnt merge fall back to
+    // vmcnt(0)): past the last shard it re-reads shard k-1, an L2 hit.
+    constexpr int NB = depth_of<F>();
+    u32x4 ring[NB][U];
+#pragma unroll
+    for (int i = 0; i < NB - 1; ++i) load(ring[i], i);
     __builtin_amdgcn_sched_barrier(0);
-    for (uint32_t t = 0; t < k; t += 3) {
-        load(C, t + 2);
-        __builtin_amdgcn_sched_barrier(0);
-        consume(A, t);
-        __builtin_amdgcn_sched_barrier(0);
-        load(A, t + 3);
-        __builtin_amdgcn_sched_barrier(0);
-        if (t + 1 < k) consume(B, t + 1);
-        __builtin_amdgcn_sched_barrier(0);
-        load(B, t + 4);
-        __builtin_amdgcn_sched_barrier(0);
-        if (t + 2 < k) consume(C, t + 2);
-        __builtin_amdgcn_sched_barrier(0);
+    for (uint32_t t = 0; t < k; t += NB) {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            load(ring[(i + NB - 1) % NB], t + i + NB - 1);
+            __builtin_amdgcn_sched_barrier(0);
+            if (t + i < k) consume(ring[i], t + i);
+            __builtin_amdgcn_sched_barrier(0);
+        }
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -273,8 +309,9 @@ __device__ __forceinline__ void stage_plan(const ApplyArgs& a, const uint8_t* pl
     c.s_out_off = s_out_off;
 }
 
+// The second __launch_bounds__ argument is amdgpu_waves_per_eu (minimum).
 template <int R, int U, int MODE, int F>
-__global__ __launch_bounds__(threads_of<F>(), (F & kOcc8) ? 8 : 1) void gf_apply_kernel(const ApplyArgs a) {
+__global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) void gf_apply_kernel(const ApplyArgs a) {
     constexpr int TH = threads_of<F>();
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr bool kLds = (F & kScalarTabs) == 0;
@@ -317,9 +354,15 @@ __global__ __launch_bounds__(threads_of<F>(), (F & kOcc8) ? 8 : 1) void gf_apply
 }
 
 template <int R, int U, int MODE, int F>
-hipError_t launch_one(const ApplyArgs& a, int grid_cap, hipStream_t stream) {
+hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStream_t stream) {
     auto kern = gf_apply_kernel<R, U, MODE, F>;
-    const size_t lds = (F & kScalarTabs) ? 0 : size_t(a.k) * R * 32 + size_t(a.k) * 8 + size_t(R) * 8;
+    size_t lds = (F & kScalarTabs) ? 0 : size_t(a.k) * R * 32 + size_t(a.k) * 8 + size_t(R) * 8;
+    // Optional occupancy cap: pad the LDS allocation so at most wgs_per_cu
+    // workgroups fit in a CU's 160 KiB.
+    if (v.wgs_per_cu > 0) {
+        const size_t cap = (160u * 1024u) / unsigned(v.wgs_per_cu) / 128u * 128u;
+        if (cap > lds) lds = cap;
+    }
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
@@ -353,30 +396,56 @@ hipError_t launch_one(const ApplyArgs& a, int grid_cap, hipStream_t stream) {
 }
 
 // Full-tile variants compiled in: each entry is one (U, F) instantiation.
+// Not every flag combination is compiled: an unsupported combination returns
+// hipErrorInvalidValue (the C ABI reports SHMR_EC_INVALID_ARGUMENT).
+#define SHMR_VARIANTS(X) \
+    X(1, 0) \
+    X(1, kNtLoad) \
+    X(1, kNtStore) \
+    X(1, kNtLoad | kNtStore) \
+    X(1, kScalarTabs | kNtLoad | kNtStore) \
+    X(1, kOcc8 | kNtLoad | kNtStore) \
+    X(1, kDiagXor) \
+    X(1, kDiagXor | kNtLoad | kNtStore) \
+    X(2, 0) \
+    X(2, kNtLoad | kNtStore) \
+    X(4, kNtLoad | kNtStore) \
+    X(1, kNtLoad | kNtStore | kTh128) \
+    X(1, kNtLoad | kNtStore | kTh512) \
+    X(1, kNtStore | kTh512) \
+    X(2, kNtLoad | kNtStore | kTh128) \
+    X(1, kNtLoad | kNtStore | kDepth5) \
+    X(1, kNtLoad | kNtStore | kDepth9) \
+    X(1, kNtLoad | kDepth5) \
+    X(1, kNtLoad | kDepth9) \
+    X(1, kNtLoad | kNtStore | kDepth2) \
+    X(1, kNtLoad | kNtStore | kDepth1) \
+    X(1, kNtLoad | kDepth2) \
+    X(1, kNtStore | kDepth2) \
+    X(2, kNtLoad | kNtStore | kDepth2) \
+    X(2, kNtStore | kDepth2) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kTh512) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kTh128) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kOcc8) \
+    X(1, kNtLoad | kNtStore | kDepth2 | (6 << kOccShift)) \
+    X(1, kNtLoad | kNtStore | kDepth2 | (7 << kOccShift)) \
+    X(1, kNtLoad | kNtStore | (6 << kOccShift)) \
+    X(1, kNtLoad | kNtStore | (7 << kOccShift)) \
+    X(2, kNtLoad | kNtStore | kDepth2 | (6 << kOccShift))
+
+int variant_flags(const Variant& v) {
+    return (v.nt_load ? kNtLoad : 0) | (v.nt_store ? kNtStore : 0) | (v.scalar_tabs ? kScalarTabs : 0) |
+           (v.occ8 ? kOcc8 : 0) | (v.diag ? kDiagXor : 0) | (v.threads == 128 ? kTh128 : 0) |
+           (v.threads == 512 ? kTh512 : 0) | (v.depth == 5 ? kDepth5 : 0) | (v.depth == 9 ? kDepth9 : 0) |
+           (v.depth == 2 ? kDepth2 : 0) | (v.depth == 1 ? kDepth1 : 0) | ((v.occ & 15) << kOccShift);
+}
+
 template <int R>
 hipError_t dispatch_full(const ApplyArgs& a, const Variant& v, int grid_cap, hipStream_t s) {
-    const int f = (v.nt_load ? kNtLoad : 0) | (v.nt_store ? kNtStore : 0) | (v.scalar_tabs ? kScalarTabs : 0) |
-                  (v.occ8 ? kOcc8 : 0) | (v.diag ? kDiagXor : 0) | (v.threads == 128 ? kTh128 : 0) |
-                  (v.threads == 512 ? kTh512 : 0);
-// Not every flag combination is compiled: unsupported combinations return
-// hipErrorInvalidValue (the C ABI reports SHMR_EC_INVALID_ARGUMENT).
+    const int f = variant_flags(v);
 #define SHMR_F(UU, FL) \
-    if (v.u == UU && f == (FL)) return launch_one<R, UU, 0, FL>(a, grid_cap, s);
-    SHMR_F(1, 0)
-    SHMR_F(1, kNtLoad)
-    SHMR_F(1, kNtStore)
-    SHMR_F(1, kNtLoad | kNtStore)
-    SHMR_F(1, kScalarTabs | kNtLoad | kNtStore)
-    SHMR_F(1, kOcc8 | kNtLoad | kNtStore)
-    SHMR_F(1, kDiagXor)
-    SHMR_F(1, kDiagXor | kNtLoad | kNtStore)
-    SHMR_F(2, 0)
-    SHMR_F(2, kNtLoad | kNtStore)
-    SHMR_F(4, kNtLoad | kNtStore)
-    SHMR_F(1, kNtLoad | kNtStore | kTh128)
-    SHMR_F(1, kNtLoad | kNtStore | kTh512)
-    SHMR_F(1, kNtStore | kTh512)
-    SHMR_F(2, kNtLoad | kNtStore | kTh128)
+    if (v.u == UU && f == (FL)) return launch_one<R, UU, 0, FL>(a, v, grid_cap, s);
+    SHMR_VARIANTS(SHMR_F)
 #undef SHMR_F
     return hipErrorInvalidValue;
 }
@@ -385,12 +454,21 @@ template <int R>
 hipError_t dispatch(const ApplyArgs& a, const Variant& v, int mode, int grid_cap, hipStream_t s) {
     switch (mode) {
         case 0: return dispatch_full<R>(a, v, grid_cap, s);
-        case 1: return launch_one<R, 1, 1, 0>(a, grid_cap, s);
-        default: return launch_one<R, 1, 2, 0>(a, grid_cap, s);
+        case 1: return launch_one<R, 1, 1, 0>(a, v, grid_cap, s);
+        default: return launch_one<R, 1, 2, 0>(a, v, grid_cap, s);
     }
 }
 
 }  // namespace
+
+bool variant_compiled(const Variant& v) {
+    const int f = variant_flags(v);
+#define SHMR_F(UU, FL) \
+    if (v.u == UU && f == (FL)) return true;
+    SHMR_VARIANTS(SHMR_F)
+#undef SHMR_F
+    return false;
+}
 
 hipError_t launch_apply(const ApplyArgs& a, unsigned rows, const Variant& v, int mode, int grid_cap,
                         hipStream_t stream) {

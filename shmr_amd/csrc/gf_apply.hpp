@@ -50,6 +50,9 @@ struct Variant {
     bool occ8 = false;       // __launch_bounds__ for 8 waves / SIMD
     bool diag = false;       // diagnostics: XOR-only (wrong results)
     int threads = kThreads;  // lanes per workgroup (128, 256, 512)
+    int depth = 3;           // register ring depth: shards of loads in flight + 1 (1, 2, 3, 5, 9)
+    int wgs_per_cu = 0;      // > 0: cap resident workgroups per CU (LDS padding)
+    int occ = 0;             // > 0: register budget for this many waves per SIMD (6, 7)
 };
 
 // rows in [1, kMaxRowsPerLaunch].  mode 0: full tiles, every shard base
@@ -58,6 +61,9 @@ struct Variant {
 // byte-granular (U = 1; the variant only affects mode 0).
 // grid_cap: -1 one workgroup per tile; 0 balanced persistent grid sized by
 // occupancy; > 0 persistent grid capped at grid_cap.
+// Whether the full-tile kernel for variant v is compiled into the library.
+bool variant_compiled(const Variant& v);
+
 hipError_t launch_apply(const ApplyArgs& a, unsigned rows, const Variant& v, int mode, int grid_cap,
                         hipStream_t stream);
 

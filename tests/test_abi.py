@@ -191,10 +191,21 @@ def test_tuning_api():
             shmr_amd.set_tuning(no_such_knob=1)
     finally:
         shmr_amd.set_tuning(**{"encode.chunks": saved})
-    # the measured policy: 4 output rows -> 2 chunks/lane; k < 8 -> no NT loads
+    # the measured policy: 4 output rows -> 2 chunks/lane; NT loads and stores; ring depth 2
     assert "chunks=2" in shmr_amd.describe_variant(False, 10, 4)
-    assert "nt_load=0" in shmr_amd.describe_variant(False, 4, 2)
+    assert "nt_load=1 nt_store=1" in shmr_amd.describe_variant(False, 4, 2)
     assert "nt_load=1" in shmr_amd.describe_variant(True, 8, 1)
+    assert "depth=2" in shmr_amd.describe_variant(True, 8, 1)
+
+
+def test_auto_policy_variants_are_compiled():
+    """Every shape the auto policy can pick maps to a compiled kernel."""
+    for decode in (False, True):
+        for k in range(1, 33):
+            for rows in range(1, 5):
+                d = shmr_amd.describe_variant(decode, k, rows)
+                assert "compiled=1" in d, (decode, k, rows, d)
+    assert "depth=2" in shmr_amd.describe_variant(False, 8, 3)
 
 
 def test_native_library_is_required():

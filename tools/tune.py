@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--pad", type=int, default=0, help="extra bytes per shard pitch (de-alias 2^n strides)")
     ap.add_argument("--diag", action="store_true", help="also time the XOR-only ceiling kernel")
     ap.add_argument("--ref", action="store_true", help="also time torch copy / xor references")
+    ap.add_argument("--same-pattern", action="store_true", help="decode: every block loses the same shards")
     a = ap.parse_args()
     if a.config in CFG:
         k, p, block, er, B = CFG[a.config]
@@ -67,17 +68,18 @@ def main():
         shards = torch.zeros((B, k + p, pitch), dtype=torch.uint8, device=dev)
         shards[:, :k, :S] = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=dev, generator=g)
         present = np.ones((B, k + p), np.uint8)
-        b = np.arange(B)
+        rows = np.arange(B)
+        b = rows * (0 if a.same_pattern else 1)
         if er == 1:
-            present[b, b % k] = 0
+            present[rows, b % k] = 0
         else:
-            present[b, b % 10] = 0
-            present[b, (b + 3) % 10] = 0
+            present[rows, b % 10] = 0
+            present[rows, (b + 3) % 10] = 0
         algo = B * (k + er) * S
 
         def run():
             rs.reconstruct_batch_dev(shards, present, shard_len=S)
-    base = {"chunks": 1, "nt_load": 0, "nt_store": 0, "scalar_tabs": 0, "occ8": 0, "grid": -1, "diag": 0,
+    base = {"chunks": 1, "nt_load": 0, "nt_store": 0, "scalar_tabs": 0, "occ8": 0, "grid": -1, "diag": 0, "depth": 3, "wgs_per_cu": 0, "occ": 0,
             "threads": 256}
     variants = []
     for spec in a.variants.split(";"):
