@@ -60,6 +60,20 @@ public:
         return reconstruct_inner(shards, true);
     }
 
+    // In-place forms over caller buffers (the Block Cache layout: shard i at
+    // shards[i], all `len` bytes).  encode writes shards[k..]; reconstruct
+    // writes the absent shards (present[i] == 0) and needs every pointer valid.
+    EcStatus encode_in_place(uint8_t* const* shards, size_t n, size_t len) const {
+        std::vector<size_t> lens(n, len);
+        return EcStatus{shmr_ec_encode(h_, shards, lens.data(), n)};
+    }
+    EcStatus reconstruct_in_place(uint8_t* const* shards, const uint8_t* present, size_t n, size_t len,
+                                  bool data_only) const {
+        std::vector<size_t> lens(n);
+        for (size_t i = 0; i < n; ++i) lens[i] = present[i] ? len : 0;
+        return EcStatus{shmr_ec_reconstruct(h_, shards, lens.data(), present, n, data_only)};
+    }
+
 private:
     explicit ReedSolomon(shmr_ec_t* h) : h_(h) {}
 

@@ -9,8 +9,13 @@
 #include <algorithm>
 #include <atomic>
 #include <cerrno>
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <map>
+#include <new>
 #include <thread>
+#include <tuple>
 
 namespace shmr {
 
@@ -20,7 +25,7 @@ ShmrError fs_error(int err) { return ShmrError{ShmrError::FsError, err}; }
 ShmrError ec_error(int code) { return ShmrError{ShmrError::EcError, code}; }
 
 // write_path (block.rs:611-634): pwrite at offset 0, then fsync.
-Status write_path(int fd, const uint8_t* buf, size_t len) {
+Status write_path(int fd, const uint8_t* buf, size_t len, bool sync = true) {
     size_t done = 0;
     while (done < len) {
         const ssize_t n = ::pwrite(fd, buf + done, len - done, off_t(done));
@@ -30,25 +35,8 @@ Status write_path(int fd, const uint8_t* buf, size_t len) {
         }
         done += size_t(n);
     }
-    if (::fsync(fd) != 0) return fs_error(errno);
+    if (sync && ::fsync(fd) != 0) return fs_error(errno);
     return std::nullopt;
-}
-
-// Read::read_to_end from the handle's current cursor.
-int read_to_end(int fd, std::vector<uint8_t>* out, bool from_start) {
-    out->clear();
-    uint8_t tmp[1 << 16];
-    off_t off = 0;
-    for (;;) {
-        const ssize_t n = from_start ? ::pread(fd, tmp, sizeof(tmp), off) : ::read(fd, tmp, sizeof(tmp));
-        if (n < 0) {
-            if (errno == EINTR) continue;
-            return errno;
-        }
-        if (n == 0) return 0;
-        out->insert(out->end(), tmp, tmp + n);
-        off += n;
-    }
 }
 
 // Runs fn(i) for i < n on up to `threads` threads (the reference's rayon fan-out).
@@ -202,6 +190,168 @@ Status VirtualPath::create(const ShmrFsConfig& cfg) const {
 std::string VirtualPath::to_string() const { return pool + "(" + bucket + "):" + filename; }
 
 // ---------------------------------------------------------------------------
+// Block Cache buffer: `len` logical bytes (the reference's Vec<u8> length)
+// inside one allocation of `cap` bytes, pinned when asked.  Bytes past `len`
+// are scratch (zero padding, parity slots); growing `len` zero-fills.
+// ---------------------------------------------------------------------------
+namespace {
+
+// Process-wide free lists of Block Cache allocations, by exact capacity
+// (blocks of one topology share it): pinning memory costs far more than
+// copying into it, so buffers dropped by drop_buffer are kept for the next
+// block instead of being returned to the driver.
+class BufferPool {
+public:
+    static BufferPool& get() {
+        static BufferPool* p = new BufferPool();   // leaked: outlives static destructors
+        return *p;
+    }
+    uint8_t* take(size_t cap, bool pinned) {
+        std::lock_guard<std::mutex> lock(mu_);
+        auto& m = pinned ? pinned_ : pageable_;
+        auto it = m.find(cap);
+        if (it == m.end()) return nullptr;
+        uint8_t* p = it->second;
+        m.erase(it);
+        cached_ -= cap;
+        return p;
+    }
+    // Returns false if the pool is full (the caller frees).
+    bool give(uint8_t* p, size_t cap, bool pinned) {
+        std::lock_guard<std::mutex> lock(mu_);
+        if (cached_ + cap > limit_) return false;
+        (pinned ? pinned_ : pageable_).emplace(cap, p);
+        cached_ += cap;
+        return true;
+    }
+    size_t trim() {
+        std::lock_guard<std::mutex> lock(mu_);
+        size_t freed = cached_;
+        for (auto& kv : pinned_) shmr_ec_host_free(kv.second);
+        for (auto& kv : pageable_) std::free(kv.second);
+        pinned_.clear();
+        pageable_.clear();
+        cached_ = 0;
+        return freed;
+    }
+
+private:
+    std::mutex mu_;
+    std::multimap<size_t, uint8_t*> pinned_, pageable_;
+    size_t cached_ = 0;
+    size_t limit_ = size_t(16) << 30;
+};
+
+class BlockBuffer {
+public:
+    BlockBuffer() = default;
+    BlockBuffer(const BlockBuffer&) = delete;
+    BlockBuffer& operator=(const BlockBuffer&) = delete;
+    ~BlockBuffer() { release(); }
+
+    size_t size() const { return len_; }
+    bool empty() const { return len_ == 0; }
+    uint8_t* data() { return p_; }
+    const uint8_t* data() const { return p_; }
+    bool pinned() const { return pinned_alloc_; }
+    void want_pinned(bool p) { want_pinned_ = p; }
+
+    void reserve(size_t cap) {
+        if (cap <= cap_) return;
+        bool pinned = false;
+        uint8_t* q = nullptr;
+        if (want_pinned_) {
+            q = BufferPool::get().take(cap, true);
+            if (q) {
+                pinned = true;
+            } else {
+                void* v = nullptr;
+                if (shmr_ec_host_alloc(cap, &v) == SHMR_EC_OK) {
+                    q = static_cast<uint8_t*>(v);
+                    pinned = true;
+                }
+            }
+        }
+        if (!q) q = BufferPool::get().take(cap, false);
+        if (!q) q = static_cast<uint8_t*>(std::aligned_alloc(4096, (cap + 4095) & ~size_t(4095)));
+        if (!q) throw std::bad_alloc();
+        if (len_) std::memcpy(q, p_, len_);
+        free_mem();
+        p_ = q;
+        cap_ = cap;
+        pinned_alloc_ = pinned;
+    }
+    // Grows the logical length, zero-filling the new bytes (Vec::resize).
+    void resize(size_t n) {
+        reserve(n);
+        if (n > len_) std::memset(p_ + len_, 0, n - len_);
+        len_ = n;
+    }
+    // Sets the logical length without initialising: for loads that overwrite
+    // every byte of [0, n) before anyone reads it.
+    void set_len_uninit(size_t n) {
+        reserve(n);
+        len_ = n;
+    }
+    void release() {
+        free_mem();
+        p_ = nullptr;
+        len_ = cap_ = 0;
+    }
+
+private:
+    void free_mem() {
+        if (!p_) return;
+        if (!BufferPool::get().give(p_, cap_, pinned_alloc_)) {
+            if (pinned_alloc_) shmr_ec_host_free(p_);
+            else std::free(p_);
+        }
+        pinned_alloc_ = false;
+    }
+    uint8_t* p_ = nullptr;
+    size_t len_ = 0, cap_ = 0;
+    bool want_pinned_ = false, pinned_alloc_ = false;
+};
+
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Reads shard file `fd` into its S-byte slot the way load_block treats the
+// result of read_to_end (block.rs:540-553): returns 0 and sets *present for a
+// readable file; a file of length != S is zero-padded/truncated to S and
+// flagged (*odd = true).  The reference reads from the handle's cursor and
+// leaves it at EOF; pread_from_start reads from offset 0 instead.
+int read_slot(int fd, uint8_t* slot, size_t S, bool from_start, bool* odd) {
+    size_t got = 0;
+    while (got < S) {
+        const ssize_t n = from_start ? ::pread(fd, slot + got, S - got, off_t(got)) : ::read(fd, slot + got, S - got);
+        if (n < 0) {
+            if (errno == EINTR) continue;
+            return errno;
+        }
+        if (n == 0) break;
+        got += size_t(n);
+    }
+    bool longer = false;
+    if (got == S) {   // probe: is there more than S bytes?
+        uint8_t b;
+        ssize_t n;
+        do {
+            n = from_start ? ::pread(fd, &b, 1, off_t(S)) : ::read(fd, &b, 1);
+        } while (n < 0 && errno == EINTR);
+        if (n < 0) return errno;
+        longer = n > 0;
+    }
+    if (!from_start && longer) ::lseek(fd, 0, SEEK_END);   // read_to_end drains the handle
+    if (got < S) std::memset(slot + got, 0, S - got);
+    *odd = got != S || longer;
+    return 0;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
 // VirtualBlock
 // ---------------------------------------------------------------------------
 struct VirtualBlock::State {
@@ -211,7 +361,7 @@ struct VirtualBlock::State {
     std::atomic<bool> should_flush{false};
     std::atomic<bool> buffer_loaded{false};
     std::mutex buf_mu;
-    std::vector<uint8_t> buffer;
+    BlockBuffer buffer;
     // A handle recorded as missing (VfsOptions::missing_shard_is_erasure) is
     // recreated on the next flush, which repairs the shard file.
     Status ensure_fd(size_t i, const ShmrFsConfig& cfg) {
@@ -231,7 +381,39 @@ struct VirtualBlock::State {
     ~State() { close_handles(); }
 };
 
+namespace {
+
+// The Erasure arm's shard set, in place (block.rs:404-423): data chunks of S
+// at i*S (the buffer itself), the last one zero-padded, then zero data shards
+// up to k, then p parity slots -- i.e. the buffer zero-extended to k*S with
+// parity at k*S.  Caller holds the buffer lock.
+Status prepare_erasure(BlockBuffer& buf, const BlockTopology& t, size_t S) {
+    if (buf.size() > size_t(t.data) * S) {
+        // block.rs:421 computes `data - nchunks` in u8: the reference panics
+        // (debug) or overwrites a data chunk with parity (release).
+        return ec_error(SHMR_EC_TOO_MANY_DATA_SHARDS);
+    }
+    const size_t len = buf.size();
+    buf.reserve((size_t(t.data) + t.parity) * S);
+    std::memset(buf.data() + len, 0, size_t(t.data) * S - len);
+    return std::nullopt;
+}
+
+void shard_ptrs(BlockBuffer& buf, size_t n, size_t S, uint8_t** out) {
+    for (size_t i = 0; i < n; ++i) out[i] = buf.data() + i * S;
+}
+
+}  // namespace
+
 VirtualBlock::VirtualBlock() : st_(std::make_shared<State>()) {}
+
+void VirtualBlock::set_options(const VfsOptions& o) {
+    opt_ = o;
+    std::lock_guard<std::mutex> lock(st_->buf_mu);
+    st_->buffer.want_pinned(o.pinned_buffers);
+}
+
+size_t VirtualBlock::shard_size() const { return calculate_shard_size(size, topology.data); }
 
 Status VirtualBlock::create(uint64_t ino, uint64_t idx, std::shared_ptr<const ShmrFsConfig> cfg, uint64_t size,
                             BlockTopology topology, VirtualBlock* out) {
@@ -282,7 +464,7 @@ Status VirtualBlock::read(uint64_t pos, uint8_t* buf, size_t len, size_t* nread)
     const auto& data = st_->buffer;
     if (data.size() < pos) return ShmrError{ShmrError::OutOfSpace};
     const size_t n = std::min<size_t>(data.size() - pos, len);
-    std::memcpy(buf, data.data() + pos, n);
+    if (n) std::memcpy(buf, data.data() + pos, n);
     *nread = n;
     return std::nullopt;
 }
@@ -294,56 +476,16 @@ Status VirtualBlock::write(uint64_t pos, const uint8_t* buf, size_t len, size_t*
     {
         std::lock_guard<std::mutex> lock(st_->buf_mu);
         auto& buffer = st_->buffer;
+        // one allocation for the block's lifetime: (k+p)*S for Erasure
+        buffer.reserve(topology.kind == BlockTopology::Erasure
+                           ? std::max<size_t>(size, (size_t(topology.data) + topology.parity) * shard_size())
+                           : size_t(size));
         const size_t end = size_t(pos) + len;
-        if (buffer.size() < end) buffer.resize(end, 0);   // grow to pos+len only, not to size
+        if (buffer.size() < end) buffer.resize(end);   // grow to pos+len only, not to size
         if (len) std::memcpy(buffer.data() + pos, buf, len);
     }
     st_->should_flush.store(false);   // the reference stores false here (block.rs:367)
     *nwritten = len;
-    return std::nullopt;
-}
-
-bool VirtualBlock::erasure_shards_for_sync(bool force, std::vector<std::vector<uint8_t>>* shards, Status* st) const {
-    *st = std::nullopt;
-    if (topology.kind != BlockTopology::Erasure) return false;
-    if (!force && !st_->should_flush.load()) return false;
-    std::lock_guard<std::mutex> lock(st_->buf_mu);
-    const auto& buffer = st_->buffer;
-    if (buffer.empty()) return false;
-    const unsigned data = topology.data, parity = topology.parity;
-    EcStatus es;
-    if (!ReedSolomon::create(data, parity, &es)) {   // ReedSolomon::new(data, parity)? (block.rs:405)
-        *st = ec_error(es.code);
-        return false;
-    }
-    const size_t S = calculate_shard_size(size, topology.data);   // block.rs:406
-    shards->clear();
-    for (size_t off = 0; off < buffer.size(); off += S) {           // buffer.chunks(S), zero padded
-        const size_t n = std::min(S, buffer.size() - off);
-        shards->emplace_back(S, 0);
-        std::memcpy(shards->back().data(), buffer.data() + off, n);
-    }
-    if (shards->size() > data) {
-        // block.rs:421 computes `data - nchunks` in u8: the reference panics
-        // (debug) or overwrites a data chunk with parity (release).
-        *st = ec_error(SHMR_EC_TOO_MANY_DATA_SHARDS);
-        return false;
-    }
-    const size_t extra = parity + (data - shards->size());          // block.rs:421-423
-    for (size_t i = 0; i < extra; ++i) shards->emplace_back(S, 0);
-    return true;
-}
-
-Status VirtualBlock::write_shards(const std::vector<std::vector<uint8_t>>& shards) const {
-    if (!st_->shard_loaded.load()) {
-        if (auto e = open_handles()) return e;
-    }
-    std::lock_guard<std::mutex> lock(st_->handles_mu);
-    for (size_t i = 0; i < shards.size() && i < st_->handles.size(); ++i) {   // block.rs:436-439
-        if (auto e = st_->ensure_fd(i, *cfg_)) return e;
-        if (auto e = write_path(st_->handles[i].second, shards[i].data(), shards[i].size())) return e;
-    }
-    st_->should_flush.store(false);
     return std::nullopt;
 }
 
@@ -353,29 +495,36 @@ Status VirtualBlock::sync_data(bool force) const {
     if (!st_->shard_loaded.load()) {
         if (auto e = open_handles()) return e;
     }
-    if (topology.kind == BlockTopology::Erasure) {
-        std::vector<std::vector<uint8_t>> shards;
-        Status st;
-        if (!erasure_shards_for_sync(true, &shards, &st)) return st;   // empty buffer: nothing written
-        EcStatus es;
-        auto r = ReedSolomon::create(topology.data, topology.parity, &es);
-        if (!r) return ec_error(es.code);
-        es = r->encode(shards);   // block.rs:427 (.unwrap() in the reference)
-        if (!es.ok()) return ec_error(es.code);
-        return write_shards(shards);
-    }
     std::lock_guard<std::mutex> lock(st_->buf_mu);
-    if (st_->buffer.empty()) return std::nullopt;   // block.rs:389-391
+    auto& buffer = st_->buffer;
+    if (buffer.empty()) return std::nullopt;   // block.rs:389-391
     std::lock_guard<std::mutex> hl(st_->handles_mu);
-    if (topology.kind == BlockTopology::Single) {
-        if (auto e = st_->ensure_fd(0, *cfg_)) return e;
-        if (auto e = write_path(st_->handles[0].second, st_->buffer.data(), st_->buffer.size())) return e;
+    const size_t nh = st_->handles.size();
+    std::vector<Status> res(nh);
+    if (topology.kind == BlockTopology::Erasure) {
+        EcStatus es;
+        auto r = ReedSolomon::create(topology.data, topology.parity, &es);   // block.rs:405
+        if (!r) return ec_error(es.code);
+        const size_t S = shard_size();                                      // block.rs:406
+        if (auto e = prepare_erasure(buffer, topology, S)) return e;
+        const size_t n = size_t(topology.data) + topology.parity;
+        std::vector<uint8_t*> ptrs(n);
+        shard_ptrs(buffer, n, S, ptrs.data());
+        es = r->encode_in_place(ptrs.data(), n, S);   // block.rs:427 (.unwrap() in the reference)
+        if (!es.ok()) return ec_error(es.code);
+        parallel_for(std::min(n, nh), 16, [&](size_t i) {   // block.rs:436-439, in parallel
+            res[i] = st_->ensure_fd(i, *cfg_);
+            if (!res[i]) res[i] = write_path(st_->handles[i].second, ptrs[i], S, opt_.fsync_shards);
+        });
     } else {
-        for (size_t i = 0; i < topology.n && i < st_->handles.size(); ++i) {
-            if (auto e = st_->ensure_fd(i, *cfg_)) return e;
-            if (auto e = write_path(st_->handles[i].second, st_->buffer.data(), st_->buffer.size())) return e;
-        }
+        const size_t copies = topology.kind == BlockTopology::Single ? 1 : std::min<size_t>(topology.n, nh);
+        parallel_for(copies, 16, [&](size_t i) {
+            res[i] = st_->ensure_fd(i, *cfg_);
+            if (!res[i]) res[i] = write_path(st_->handles[i].second, buffer.data(), buffer.size(), opt_.fsync_shards);
+        });
     }
+    for (auto& e : res)
+        if (e) return e;
     st_->should_flush.store(false);
     return std::nullopt;
 }
@@ -389,12 +538,10 @@ Status VirtualBlock::open_handles() const {
         fs::path file;
         if (auto e = shard.resolve(*cfg_, &file, nullptr)) return e;
         const int fd = ::open(file.c_str(), O_RDWR);
-        if (fd < 0) {
-            if (!opt_.missing_shard_is_erasure) {
-                const int err = errno;
-                st_->close_handles();
-                return fs_error(err);
-            }
+        if (fd < 0 && !opt_.missing_shard_is_erasure) {
+            const int err = errno;
+            st_->close_handles();
+            return fs_error(err);
         }
         st_->handles.emplace_back(shard, fd);
     }
@@ -409,9 +556,10 @@ Status VirtualBlock::load_block() const {
     }
     std::lock_guard<std::mutex> lock(st_->buf_mu);
     auto& buffer = st_->buffer;
-    if (buffer.size() < size) buffer.resize(size, 0);
     std::lock_guard<std::mutex> hl(st_->handles_mu);
     if (topology.kind == BlockTopology::Single) {
+        buffer.reserve(size);
+        if (buffer.size() < size) buffer.resize(size);
         const int fd = st_->handles[0].second;
         const ssize_t n = fd < 0 ? 0 : ::read(fd, buffer.data(), buffer.size());   // one read() call
         if (n < 0) return fs_error(errno);
@@ -419,34 +567,31 @@ Status VirtualBlock::load_block() const {
         return fs_error(ENOSYS);   // todo!("Implement Mirrored Read") in the reference
     } else {
         if (topology.version != 1) return fs_error(ENOSYS);   // unimplemented!()
-        const size_t S = calculate_shard_size(size, topology.data);
         EcStatus es;
         auto r = ReedSolomon::create(topology.data, topology.parity, &es);
         if (!r) return ec_error(es.code);
-        bool missing = false;
-        std::vector<std::optional<std::vector<uint8_t>>> ec(st_->handles.size());
-        for (size_t i = 0; i < st_->handles.size(); ++i) {
+        const size_t S = shard_size();
+        const size_t n = st_->handles.size();
+        buffer.reserve(std::max<size_t>(size, n * S));
+        if (buffer.size() < size) buffer.set_len_uninit(size);   // every slot byte is overwritten below
+        std::vector<uint8_t*> ptrs(n);
+        shard_ptrs(buffer, n, S, ptrs.data());
+        std::vector<uint8_t> present(n, 0), odd(n, 0);
+        parallel_for(n, 16, [&](size_t i) {
             const int fd = st_->handles[i].second;
-            std::vector<uint8_t> b;
-            if (fd < 0 || read_to_end(fd, &b, opt_.pread_from_start) != 0) {   // Err -> None
-                missing = true;
-                continue;
+            bool o = false;
+            if (fd >= 0 && read_slot(fd, ptrs[i], S, opt_.pread_from_start, &o) == 0) {   // Err -> None
+                present[i] = !(o && opt_.short_shard_is_erasure);
+                odd[i] = o;
             }
-            if (b.size() != S) {   // len != S: zero-pad, stays present (block.rs:548-551)
-                missing = true;
-                if (opt_.short_shard_is_erasure) continue;
-                b.resize(S, 0);
-            }
-            ec[i] = std::move(b);
-        }
+        });
+        bool missing = false;
+        for (size_t i = 0; i < n; ++i) missing |= !present[i] || odd[i];
         if (missing) {
-            es = r->reconstruct(ec);   // block.rs:560 (.unwrap() in the reference)
+            es = r->reconstruct_in_place(ptrs.data(), present.data(), n, S, false);   // block.rs:560 (unwrap)
             if (!es.ok()) return ec_error(es.code);
         }
-        std::vector<uint8_t> all;
-        all.reserve(ec.size() * S);
-        for (auto& s : ec) all.insert(all.end(), s->begin(), s->end());
-        std::memcpy(buffer.data(), all.data(), size_t(size));   // ec_data[..size]
+        buffer.resize(size);   // ec_data[..size] (block.rs:576); the bytes are already in place
     }
     st_->buffer_loaded.store(true);
     return std::nullopt;
@@ -456,7 +601,7 @@ Status VirtualBlock::load_block() const {
 Status VirtualBlock::drop_buffer() const {
     if (auto e = sync_data(true)) return e;
     std::lock_guard<std::mutex> lock(st_->buf_mu);
-    st_->buffer = std::vector<uint8_t>();
+    st_->buffer.release();
     st_->buffer_loaded.store(false);
     return std::nullopt;
 }
@@ -474,10 +619,21 @@ Status VirtualBlock::drop_handles() const {
 
 std::vector<uint8_t> VirtualBlock::buffer_snapshot() const {
     std::lock_guard<std::mutex> lock(st_->buf_mu);
-    return st_->buffer;
+    const auto& b = st_->buffer;
+    return std::vector<uint8_t>(b.data(), b.data() + b.size());
 }
 
 bool VirtualBlock::buffer_loaded() const { return st_->buffer_loaded.load(); }
+
+size_t VirtualBlock::buffered_len() const {
+    std::lock_guard<std::mutex> lock(st_->buf_mu);
+    return st_->buffer.size();
+}
+
+bool VirtualBlock::buffer_pinned() const {
+    std::lock_guard<std::mutex> lock(st_->buf_mu);
+    return st_->buffer.pinned();
+}
 
 // ---------------------------------------------------------------------------
 // VirtualFile (mod.rs:63-272)
@@ -494,26 +650,76 @@ void VirtualFile::populate(std::shared_ptr<const ShmrFsConfig> cfg) {
     cfg_ = std::move(cfg);
 }
 
+void VirtualFile::set_options(const VfsOptions& o) {
+    opt_ = o;
+    for (auto& b : blocks) b.set_options(o);
+}
+
 Status VirtualFile::allocate_block() {
     if (!cfg_) return fs_error(EINVAL);
     VirtualBlock b;
     if (auto e = VirtualBlock::create(ino, blocks.size() + 1, cfg_, block_size, BlockTopology::single(), &b))
         return e;   // the next block number is len + 1 (mod.rs:119-127)
+    b.set_options(opt_);
     blocks.push_back(b);
     return std::nullopt;
 }
 
+// The blocks VirtualFile::read's chunk loop visits for (pos, len).
+std::vector<size_t> VirtualFile::blocks_for_range(uint64_t pos, size_t len) const {
+    std::vector<size_t> out;
+    const uint64_t start_chunk = pos / chunk_size;
+    const uint64_t end_chunk = len / chunk_size + start_chunk;
+    for (uint64_t c = start_chunk; c <= end_chunk; ++c) {
+        const size_t b = size_t(c * chunk_size / block_size);
+        if (b < blocks.size() && (out.empty() || out.back() != b)) out.push_back(b);
+    }
+    return out;
+}
+
 // mod.rs:137-180.  Chunks map to (block, block_pos) from chunk_idx * chunk_size,
 // ignoring pos % chunk_size, exactly as the reference does.
-Status VirtualFile::read(uint64_t pos, uint8_t* buf, size_t len, size_t* nread) const {
+Status VirtualFile::read(uint64_t pos, uint8_t* buf, size_t len, size_t* nread) {
     *nread = 0;
     if (!cfg_) return fs_error(EINVAL);
     if (len == 0 || size == 0) return std::nullopt;
     if (pos > size) return ShmrError{ShmrError::EndOfFile};
+    if (auto e = load_blocks(blocks_for_range(pos, len))) return e;
     const uint64_t start_chunk = pos / chunk_size;
     const uint64_t end_chunk = len / chunk_size + start_chunk;
+    // Plan: runs of consecutive chunks inside one block.  When the block holds
+    // every byte of a run, the reference's per-chunk copies are one contiguous
+    // copy (same bytes, same count) at a known offset, and such runs are
+    // copied in parallel; the first run that could come up short (or fail)
+    // and everything after it is done chunk by chunk, in order, as the
+    // reference does.
+    struct Run {
+        size_t blk;
+        uint64_t block_pos;
+        size_t off, len;
+    };
+    std::vector<Run> runs;
+    uint64_t c = start_chunk;
     size_t done = 0;
-    for (uint64_t c = start_chunk; c <= end_chunk; ++c) {
+    for (; c <= end_chunk;) {
+        const uint64_t block_idx = c * chunk_size / block_size;
+        const uint64_t block_pos = c * chunk_size % block_size;
+        if (block_idx >= blocks.size()) break;
+        const uint64_t run = std::min<uint64_t>(end_chunk - c + 1, (block_size - block_pos + chunk_size - 1) / chunk_size);
+        const size_t want = size_t(std::min<uint64_t>(uint64_t(done) + run * chunk_size, len)) - done;
+        if (want > 0 && blocks[block_idx].buffered_len() < block_pos + want) break;
+        if (want > 0) runs.push_back({size_t(block_idx), block_pos, done, want});
+        done += want;
+        c += run;
+    }
+    std::vector<Status> res(runs.size());
+    parallel_for(runs.size(), runs.size() > 4 ? 8 : 1, [&](size_t i) {
+        size_t n = 0;
+        res[i] = blocks[runs[i].blk].read(runs[i].block_pos, buf + runs[i].off, runs[i].len, &n);
+    });
+    for (auto& e : res)
+        if (e) return e;
+    for (; c <= end_chunk; ++c) {   // the reference's loop for the rest
         const uint64_t block_idx = c * chunk_size / block_size;
         const uint64_t block_pos = c * chunk_size % block_size;
         const size_t end = size_t(std::min<uint64_t>(done + chunk_size, len));
@@ -534,8 +740,39 @@ Status VirtualFile::write(uint64_t pos, const uint8_t* buf, size_t len, size_t* 
     const uint64_t start_chunk = pos / chunk_size;
     const uint64_t end_chunk = len / chunk_size + start_chunk;
     const uint64_t chk_per_blk = block_size / chunk_size;
+    // Plan runs of consecutive chunks inside one block (allocating blocks in
+    // the reference's order); runs that fit their block are one contiguous
+    // write each, done in parallel.  From the first run that does not fit,
+    // the rest goes chunk by chunk so OutOfSpace leaves exactly the bytes the
+    // reference's loop leaves.
+    struct Run {
+        size_t blk;
+        uint64_t block_pos;
+        size_t off, len;
+    };
+    std::vector<Run> runs;
+    uint64_t c = start_chunk;
     size_t written = 0;
-    for (uint64_t c = start_chunk; c <= end_chunk; ++c) {
+    for (; c <= end_chunk;) {
+        while (blocks.size() * chk_per_blk <= c)
+            if (auto e = allocate_block()) return e;
+        const uint64_t block_idx = c * chunk_size / block_size;
+        const uint64_t block_pos = c * chunk_size % block_size;
+        const uint64_t run = std::min<uint64_t>(end_chunk - c + 1, (block_size - block_pos + chunk_size - 1) / chunk_size);
+        const size_t want = size_t(std::min<uint64_t>(uint64_t(written) + run * chunk_size, len)) - written;
+        if (block_pos + want > blocks[block_idx].size) break;
+        runs.push_back({size_t(block_idx), block_pos, written, want});
+        written += want;
+        c += run;
+    }
+    std::vector<Status> res(runs.size());
+    parallel_for(runs.size(), runs.size() > 4 ? 8 : 1, [&](size_t i) {
+        size_t n = 0;
+        res[i] = blocks[runs[i].blk].write(runs[i].block_pos, buf + runs[i].off, runs[i].len, &n);
+    });
+    for (auto& e : res)
+        if (e) return e;
+    for (; c <= end_chunk; ++c) {   // the reference's loop for the rest
         while (blocks.size() * chk_per_blk <= c)
             if (auto e = allocate_block()) return e;
         const uint64_t block_idx = c * chunk_size / block_size;
@@ -550,17 +787,28 @@ Status VirtualFile::write(uint64_t pos, const uint8_t* buf, size_t len, size_t* 
     return std::nullopt;
 }
 
-// mod.rs:91-103, MI355X-batched: Erasure blocks of the same (k, p) are
-// encoded in one pipelined GPU call, then every block's shard files are
-// written from a thread pool (the rayon fan-out); errors are reported after
-// every block was attempted.
-Status VirtualFile::sync_data(bool force, const std::vector<int>& devices) const {
+namespace {
+
+// Locks held over a batch: every block's buffer lock, then its handle lock,
+// in block order (the order VirtualBlock::sync_data / load_block take them).
+struct BatchLocks {
+    std::vector<std::unique_lock<std::mutex>> held;
+};
+
+struct Group {
+    unsigned k = 0, p = 0;
+    size_t S = 0;
+    std::vector<size_t> members;   // block indices
+};
+
+}  // namespace
+
+// mod.rs:91-103, MI355X-batched.
+Status VirtualFile::sync_data(bool force) {
+    last_sync = IoStats{};
+    const double t0 = now_s();
     std::vector<Status> results(blocks.size());
-    struct Group {
-        std::vector<size_t> members;
-        std::vector<std::vector<std::vector<uint8_t>>> shards;
-    };
-    std::map<std::pair<unsigned, unsigned>, Group> groups;
+    std::map<std::tuple<unsigned, unsigned, size_t>, Group> groups;
     std::vector<size_t> others;
     for (size_t i = 0; i < blocks.size(); ++i) {
         const VirtualBlock& b = blocks[i];
@@ -568,39 +816,180 @@ Status VirtualFile::sync_data(bool force, const std::vector<int>& devices) const
             others.push_back(i);
             continue;
         }
-        std::vector<std::vector<uint8_t>> sh;
-        Status st;
-        if (!b.erasure_shards_for_sync(force, &sh, &st)) {
-            results[i] = st;
-            continue;
+        if (!force && !b.st_->should_flush.load()) continue;
+        if (!b.st_->shard_loaded.load()) {
+            if ((results[i] = b.open_handles())) continue;
         }
-        Group& g = groups[{b.topology.data, b.topology.parity}];
+        const size_t S = b.shard_size();
+        Group& g = groups[{b.topology.data, b.topology.parity, S}];
+        g.k = b.topology.data;
+        g.p = b.topology.parity;
+        g.S = S;
         g.members.push_back(i);
-        g.shards.push_back(std::move(sh));
     }
+    BatchLocks locks;
     for (auto& kv : groups) {
         Group& g = kv.second;
-        EcStatus es;
-        auto r = ReedSolomon::create(kv.first.first, kv.first.second, &es);
-        const size_t t = size_t(kv.first.first) + kv.first.second;
-        // one batch per shard length (blocks of a file share it)
-        std::map<size_t, std::vector<size_t>> by_len;
-        for (size_t j = 0; j < g.members.size(); ++j) by_len[g.shards[j][0].size()].push_back(j);
-        for (auto& lv : by_len) {
-            std::vector<uint8_t*> ptrs;
-            for (size_t j : lv.second)
-                for (size_t i = 0; i < t; ++i) ptrs.push_back(g.shards[j][i].data());
-            int rc = r ? shmr_ec_encode_blocks_host(r->handle(), ptrs.data(), lv.second.size(), lv.first,
-                                                    devices.data(), int(devices.size()))
-                       : es.code;
-            if (rc != SHMR_EC_OK)
-                for (size_t j : lv.second) results[g.members[j]] = ec_error(rc);
+        std::vector<size_t> live;
+        for (size_t i : g.members) {
+            VirtualBlock& b = blocks[i];
+            locks.held.emplace_back(b.st_->buf_mu);
+            if (b.st_->buffer.empty()) continue;   // block.rs:389-391: nothing to write
+            if ((results[i] = prepare_erasure(b.st_->buffer, b.topology, g.S))) continue;
+            locks.held.emplace_back(b.st_->handles_mu);
+            live.push_back(i);
         }
-        parallel_for(g.members.size(), 16, [&](size_t j) {
-            if (!results[g.members[j]]) results[g.members[j]] = blocks[g.members[j]].write_shards(g.shards[j]);
-        });
+        g.members.swap(live);
     }
+    last_sync.prepare_s = now_s() - t0;
+    // one pipelined multi-GPU encode per (k, p, S)
+    const double t1 = now_s();
+    for (auto& kv : groups) {
+        Group& g = kv.second;
+        if (g.members.empty()) continue;
+        const size_t n = size_t(g.k) + g.p;
+        std::vector<uint8_t*> ptrs(g.members.size() * n);
+        for (size_t j = 0; j < g.members.size(); ++j) shard_ptrs(blocks[g.members[j]].st_->buffer, n, g.S, &ptrs[j * n]);
+        EcStatus es;
+        auto r = ReedSolomon::create(g.k, g.p, &es);
+        const int rc = r ? shmr_ec_encode_blocks_host(r->handle(), ptrs.data(), g.members.size(), g.S, devices.data(),
+                                                      int(devices.size()))
+                         : es.code;
+        if (rc != SHMR_EC_OK)
+            for (size_t i : g.members) results[i] = ec_error(rc);
+        last_sync.blocks += g.members.size();
+    }
+    last_sync.codec_s = now_s() - t1;
+    // every shard file of the batch, written in parallel (block.rs:436-439)
+    const double t2 = now_s();
+    struct Task {
+        size_t blk, shard, S;
+    };
+    std::vector<Task> tasks;
+    for (auto& kv : groups)
+        for (size_t i : kv.second.members)
+            if (!results[i])
+                for (size_t s = 0; s < size_t(kv.second.k) + kv.second.p && s < blocks[i].st_->handles.size(); ++s)
+                    tasks.push_back({i, s, kv.second.S});
+    std::vector<Status> task_res(tasks.size());
+    parallel_for(tasks.size(), 32, [&](size_t t) {
+        const Task& tk = tasks[t];
+        auto& st = *blocks[tk.blk].st_;
+        task_res[t] = st.ensure_fd(tk.shard, *cfg_);
+        if (!task_res[t])
+            task_res[t] = write_path(st.handles[tk.shard].second, st.buffer.data() + tk.shard * tk.S, tk.S,
+                                     blocks[tk.blk].opt_.fsync_shards);
+    });
+    for (size_t t = 0; t < tasks.size(); ++t)
+        if (task_res[t] && !results[tasks[t].blk]) results[tasks[t].blk] = task_res[t];
+    for (auto& kv : groups)
+        for (size_t i : kv.second.members)
+            if (!results[i]) blocks[i].st_->should_flush.store(false);
+    locks.held.clear();
+    last_sync.io_s = now_s() - t2;
     parallel_for(others.size(), 16, [&](size_t j) { results[others[j]] = blocks[others[j]].sync_data(force); });
+    for (auto& r : results)
+        if (r) return r;
+    return std::nullopt;
+}
+
+// Batched load_block (block.rs:496-584) over several blocks: the same rules
+// per block, one reconstruct call per (k, p, S) for the blocks with erasures.
+Status VirtualFile::load_blocks(const std::vector<size_t>& block_indices) {
+    last_load = IoStats{};
+    const double t0 = now_s();
+    std::vector<Status> results(blocks.size());
+    std::map<std::tuple<unsigned, unsigned, size_t>, Group> groups;
+    std::vector<size_t> others;
+    for (size_t i : block_indices) {
+        if (i >= blocks.size()) return ShmrError{ShmrError::BlockIndexOutOfBounds};
+        const VirtualBlock& b = blocks[i];
+        if (b.st_->buffer_loaded.load()) continue;
+        if (b.topology.kind != BlockTopology::Erasure || b.topology.version != 1) {
+            others.push_back(i);   // Single, Mirror (ENOSYS) and unknown versions: per block
+            continue;
+        }
+        if (!b.st_->shard_loaded.load()) {
+            if ((results[i] = b.open_handles())) continue;
+        }
+        const size_t S = b.shard_size();
+        Group& g = groups[{b.topology.data, b.topology.parity, S}];
+        g.k = b.topology.data;
+        g.p = b.topology.parity;
+        g.S = S;
+        g.members.push_back(i);
+    }
+    BatchLocks locks;
+    struct Task {
+        size_t blk, shard, S;
+        uint8_t* slot;
+        int fd;
+    };
+    std::vector<Task> tasks;
+    std::map<size_t, size_t> first_task;   // block -> index of its shard 0 task
+    for (auto& kv : groups) {
+        Group& g = kv.second;
+        const size_t n = size_t(g.k) + g.p;
+        for (size_t i : g.members) {
+            auto& st = *blocks[i].st_;
+            locks.held.emplace_back(st.buf_mu);
+            locks.held.emplace_back(st.handles_mu);
+            st.buffer.reserve(std::max<size_t>(blocks[i].size, n * g.S));
+            if (st.buffer.size() < blocks[i].size) st.buffer.set_len_uninit(blocks[i].size);   // slots overwritten
+            first_task[i] = tasks.size();
+            for (size_t s = 0; s < n; ++s)
+                tasks.push_back({i, s, g.S, st.buffer.data() + s * g.S, s < st.handles.size() ? st.handles[s].second : -1});
+        }
+    }
+    last_load.prepare_s = now_s() - t0;
+    const double t1 = now_s();
+    std::vector<uint8_t> present(tasks.size(), 0), odd(tasks.size(), 0);
+    parallel_for(tasks.size(), 32, [&](size_t t) {
+        const Task& tk = tasks[t];
+        const VfsOptions& o = blocks[tk.blk].opt_;
+        bool od = false;
+        if (tk.fd >= 0 && read_slot(tk.fd, tk.slot, tk.S, o.pread_from_start, &od) == 0) {
+            present[t] = !(od && o.short_shard_is_erasure);
+            odd[t] = od;
+        }
+    });
+    last_load.io_s = now_s() - t1;
+    const double t2 = now_s();
+    for (auto& kv : groups) {
+        Group& g = kv.second;
+        const size_t n = size_t(g.k) + g.p;
+        std::vector<size_t> need;
+        for (size_t i : g.members) {
+            bool missing = false;
+            for (size_t s = 0; s < n; ++s) missing |= !present[first_task[i] + s] || odd[first_task[i] + s];
+            if (missing) need.push_back(i);
+        }
+        if (!need.empty()) {
+            std::vector<uint8_t*> ptrs(need.size() * n);
+            std::vector<uint8_t> pres(need.size() * n);
+            for (size_t j = 0; j < need.size(); ++j)
+                for (size_t s = 0; s < n; ++s) {
+                    ptrs[j * n + s] = tasks[first_task[need[j]] + s].slot;
+                    pres[j * n + s] = present[first_task[need[j]] + s];
+                }
+            EcStatus es;
+            auto r = ReedSolomon::create(g.k, g.p, &es);
+            const int rc = r ? shmr_ec_reconstruct_blocks_host(r->handle(), ptrs.data(), pres.data(), need.size(), g.S,
+                                                               0, devices.data(), int(devices.size()))
+                             : es.code;
+            if (rc != SHMR_EC_OK)
+                for (size_t i : need) results[i] = ec_error(rc);
+            last_load.blocks += need.size();
+        }
+        for (size_t i : g.members) {
+            if (results[i]) continue;
+            blocks[i].st_->buffer.resize(blocks[i].size);   // ec_data[..size]
+            blocks[i].st_->buffer_loaded.store(true);
+        }
+    }
+    last_load.codec_s = now_s() - t2;
+    locks.held.clear();
+    parallel_for(others.size(), 16, [&](size_t j) { results[others[j]] = blocks[others[j]].load_block(); });
     for (auto& r : results)
         if (r) return r;
     return std::nullopt;
@@ -609,6 +998,12 @@ Status VirtualFile::sync_data(bool force, const std::vector<int>& devices) const
 Status VirtualFile::drop_buffers() const {
     for (auto& b : blocks)
         if (auto e = b.drop_buffer()) return e;
+    return std::nullopt;
+}
+
+Status VirtualFile::drop_handles() const {
+    for (auto& b : blocks)
+        if (auto e = b.drop_handles()) return e;
     return std::nullopt;
 }
 
@@ -624,5 +1019,39 @@ Status VirtualFile::replace_block(size_t block_idx, VirtualBlock new_block) {
     blocks[block_idx] = new_block;
     return std::nullopt;
 }
+
+Status VirtualFile::rewrite_erasure(uint8_t data, uint8_t parity) {
+    if (!cfg_) return fs_error(EINVAL);
+    std::vector<size_t> todo;
+    for (size_t i = 0; i < blocks.size(); ++i) {
+        const auto& t = blocks[i].topology;
+        if (!(t.kind == BlockTopology::Erasure && t.version == 1 && t.data == data && t.parity == parity))
+            todo.push_back(i);
+    }
+    if (todo.empty()) return std::nullopt;
+    if (auto e = load_blocks(todo)) return e;
+    VirtualFile staged;   // the new blocks, flushed as one batch
+    staged.cfg_ = cfg_;
+    staged.opt_ = opt_;
+    staged.devices = devices;
+    for (size_t i : todo) {
+        VirtualBlock& old = blocks[i];
+        VirtualBlock nb;
+        if (auto e = VirtualBlock::create(ino, old.idx, cfg_, old.size, BlockTopology::erasure(1, data, parity), &nb))
+            return e;
+        nb.set_options(opt_);
+        std::vector<uint8_t> buf(old.size, 0);   // replace_block's full-size copy (mod.rs:253-262)
+        size_t n = 0;
+        if (auto e = old.read(0, buf.data(), buf.size(), &n)) return e;
+        if (auto e = nb.write(0, buf.data(), buf.size(), &n)) return e;
+        staged.blocks.push_back(nb);
+    }
+    if (auto e = staged.sync_data(true)) return e;
+    last_sync = staged.last_sync;
+    for (size_t j = 0; j < todo.size(); ++j) blocks[todo[j]] = staged.blocks[j];
+    return std::nullopt;
+}
+
+size_t block_cache_trim() { return BufferPool::get().trim(); }
 
 }  // namespace shmr

@@ -1,9 +1,18 @@
 // C++ host mirror of the reference's StorageBlock layer (src/vfs/{block,mod,path}.rs,
 // src/config.rs) around the MI355X codec.  Same types, method names and error
-// behaviour as the reference; the Erasure arms call shmr::ReedSolomon (GPU) and
-// VirtualFile::sync_data batches every Erasure block of a flush into one
-// pipelined GPU call (shmr_ec_encode_blocks_host) instead of one encode per
-// block.  Deviations from the reference are opt-in (VfsOptions).
+// behaviour as the reference; the Erasure arms call shmr::ReedSolomon (GPU).
+//
+// Block Cache layout: an Erasure block's buffer is one
+// allocation of (k+p)*S bytes -- the data shards are already contiguous at i*S
+// in the reference's buffer, so sync encodes and writes the shard files
+// straight from it (no chunks().to_vec() copies), and load reads every shard
+// file into its slot and reconstructs in place.  With VfsOptions::pinned_buffers
+// the allocation is pinned host memory, which the GPU DMAs without staging.
+// VirtualFile::sync_data / read batch every Erasure block of the operation into
+// one pipelined multi-GPU call (shmr_ec_encode_blocks_host /
+// shmr_ec_reconstruct_blocks_host) and fan the shard-file I/O out over a
+// thread pool (parallel pwrite+fsync, row 3).  Deviations from the reference
+// are opt-in (VfsOptions).
 #pragma once
 
 #include <cstdint>
@@ -99,6 +108,20 @@ struct VfsOptions {
     // load_block: a shard whose length is not S is an erasure (the reference
     // zero-pads it and keeps it present, block.rs:548-551).
     bool short_shard_is_erasure = false;
+    // Block Cache buffers in pinned host memory (shmr_ec_host_alloc); falls
+    // back to pageable memory when no device is present.
+    bool pinned_buffers = false;
+    // fsync every shard file after writing it (write_path, block.rs:633).
+    // Benchmarks may turn it off to separate the device path from the disk.
+    bool fsync_shards = true;
+};
+
+// Where a VirtualFile flush / batched load spent its time (last call).
+struct IoStats {
+    double prepare_s = 0;   // opening handles, padding buffers
+    double codec_s = 0;     // batched GPU encode / reconstruct (PCIe included)
+    double io_s = 0;        // shard-file reads or writes (+ fsync)
+    size_t blocks = 0;      // Erasure blocks in the batch
 };
 
 // VirtualBlock (src/vfs/block.rs:119-634).  Copies share state, like the
@@ -118,7 +141,7 @@ public:
                                    std::shared_ptr<const ShmrFsConfig> cfg, uint64_t size, BlockTopology topology,
                                    VirtualBlock* out);
     void populate(std::shared_ptr<const ShmrFsConfig> cfg) { cfg_ = std::move(cfg); }
-    void set_options(const VfsOptions& o) { opt_ = o; }
+    void set_options(const VfsOptions& o);
 
     Status read(uint64_t pos, uint8_t* buf, size_t len, size_t* nread) const;
     Status write(uint64_t pos, const uint8_t* buf, size_t len, size_t* nwritten) const;
@@ -129,23 +152,24 @@ public:
     // Test hooks (the reference's tests read these fields directly).
     std::vector<uint8_t> buffer_snapshot() const;
     bool buffer_loaded() const;
-
-    // --- used by VirtualFile's batched flush ---
-    // For an Erasure block that needs syncing: the k+p shards exactly as the
-    // Erasure arm builds them before encode (block.rs:406-423).  false if the
-    // block has nothing to flush or is not Erasure.
-    bool erasure_shards_for_sync(bool force, std::vector<std::vector<uint8_t>>* shards, Status* st) const;
-    // Writes already-encoded shards to the shard files (block.rs:436-439).
-    Status write_shards(const std::vector<std::vector<uint8_t>>& shards) const;
+    bool buffer_pinned() const;
+    size_t buffered_len() const;   // the buffer's current length
 
 private:
+    friend class VirtualFile;
     struct State;
     Status open_handles() const;
     Status load_block() const;
+    size_t shard_size() const;   // S of an Erasure block (mod.rs:16-18)
     std::shared_ptr<State> st_;
     std::shared_ptr<const ShmrFsConfig> cfg_;
     VfsOptions opt_;
 };
+
+// Frees the Block Cache allocations kept for reuse (dropped buffers are pooled
+// by capacity, up to 16 GiB, because pinning memory costs more than filling
+// it).  Returns the bytes freed.
+size_t block_cache_trim();
 
 // VirtualFile (src/vfs/mod.rs:35-272)
 class VirtualFile {
@@ -158,19 +182,35 @@ public:
 
     static VirtualFile new_with(uint64_t ino, uint64_t size);
     void populate(std::shared_ptr<const ShmrFsConfig> cfg);
+    void set_options(const VfsOptions& o);   // this file's blocks, present and future
 
-    Status read(uint64_t pos, uint8_t* buf, size_t len, size_t* nread) const;
+    std::vector<int> devices = {0};   // GPUs for the batched calls (blocks round-robin)
+    IoStats last_sync, last_load;     // instrumentation of the last batched flush / load
+
+    // read (mod.rs:137-180): the blocks the range touches are first loaded as
+    // one batch (load_blocks), then copied out chunk by chunk as the reference.
+    Status read(uint64_t pos, uint8_t* buf, size_t len, size_t* nread);
     Status write(uint64_t pos, const uint8_t* buf, size_t len, size_t* nwritten);
     // sync_data (mod.rs:91-103): every block is flushed, errors reported after
-    // all were attempted.  Erasure blocks of the same (k, p) are encoded in
-    // one batched GPU call over `devices`.
-    Status sync_data(bool force, const std::vector<int>& devices = {0}) const;
+    // all were attempted.  Erasure blocks with the same (k, p, S) are encoded in
+    // one batched GPU call, their k+p shard files written in parallel.
+    Status sync_data(bool force);
+    // Loads every listed block that is not buffered; Erasure blocks with
+    // erasures are reconstructed in one batched GPU call per (k, p, S).
+    Status load_blocks(const std::vector<size_t>& block_indices);
     Status drop_buffers() const;
+    Status drop_handles() const;
     Status replace_block(size_t block_idx, VirtualBlock new_block);
+    // Rewrites every block that is not Erasure(1, k, p) into a new Erasure
+    // block (the file-level form of replace_block; the reference's D-Bus
+    // RewriteFile is todo!(), dbus.rs:46): batched load, batched encode.
+    Status rewrite_erasure(uint8_t data, uint8_t parity);
 
 private:
     Status allocate_block();
+    std::vector<size_t> blocks_for_range(uint64_t pos, size_t len) const;
     std::shared_ptr<const ShmrFsConfig> cfg_;
+    VfsOptions opt_;
 };
 
 }  // namespace shmr

@@ -243,6 +243,99 @@ void test_virtual_file_2_4_mb() {   // mod.rs:351-370
     CHECK(std::equal(f.begin(), f.end(), data.begin()));
 }
 
+// The reference's chunk loops (mod.rs:137-242), restated literally over a
+// plain model of Single blocks that are never flushed: random writes and reads
+// (unaligned positions, partial buffers, short reads) must leave the same
+// bytes and return the same counts as VirtualFile's merged-run copies.
+struct ChunkModel {
+    uint64_t chunk = VFS_DEFAULT_BLOCK_SIZE, bs;
+    std::vector<std::vector<uint8_t>> buf;
+    std::vector<bool> loaded;
+    uint64_t size = 0;
+    explicit ChunkModel(uint64_t block_size) : bs(block_size) {}
+    bool write(uint64_t pos, const uint8_t* d, size_t len, size_t* out) {
+        *out = 0;
+        if (len == 0) return true;
+        const uint64_t sc = pos / chunk, ec = len / chunk + sc, per = bs / chunk;
+        size_t w = 0;
+        for (uint64_t c = sc; c <= ec; ++c) {
+            while (buf.size() * per <= c) {
+                buf.emplace_back();
+                loaded.push_back(false);
+            }
+            const uint64_t b = c * chunk / bs, bp = c * chunk % bs;
+            const size_t end = size_t(std::min<uint64_t>(w + chunk, len));
+            if (bp + (end - w) > bs) return false;   // OutOfSpace
+            if (buf[b].size() < bp + (end - w)) buf[b].resize(bp + (end - w), 0);
+            std::memcpy(buf[b].data() + bp, d + w, end - w);
+            w = end;
+        }
+        size = std::max<uint64_t>(size, pos + len);
+        *out = w;
+        return true;
+    }
+    bool read(uint64_t pos, uint8_t* d, size_t len, size_t* out) {
+        *out = 0;
+        if (len == 0 || size == 0) return true;
+        if (pos > size) return false;   // EndOfFile
+        const uint64_t sc = pos / chunk, ec = len / chunk + sc;
+        size_t r = 0;
+        for (uint64_t c = sc; c <= ec; ++c) {
+            const uint64_t b = c * chunk / bs, bp = c * chunk % bs;
+            const size_t end = size_t(std::min<uint64_t>(r + chunk, len));
+            if (b >= buf.size()) return false;
+            if (end == r) continue;   // VirtualBlock::read of 0 bytes: Ok(0), no load
+            if (!loaded[b]) {   // load_block: resize to size; the empty shard file reads 0 bytes
+                if (buf[b].size() < bs) buf[b].resize(bs, 0);
+                loaded[b] = true;
+            }
+            if (buf[b].size() < bp) return false;   // OutOfSpace
+            const size_t n = std::min<size_t>(buf[b].size() - bp, end - r);
+            std::memcpy(d + r, buf[b].data() + bp, n);
+            r += n;
+        }
+        *out = r;
+        return true;
+    }
+};
+
+void test_virtual_file_chunk_model() {
+    auto cfg = test_config();
+    for (int trial = 0; trial < 4; ++trial) {
+        const uint64_t bs = trial % 2 ? 64 * 1024 : 16 * 1024;
+        VirtualFile vf = VirtualFile::new_with(40 + trial, 0);
+        vf.populate(cfg);
+        vf.block_size = bs;
+        ChunkModel m(bs);
+        std::mt19937_64 rng(777 + trial);
+        for (int op = 0; op < 300; ++op) {
+            const bool is_write = vf.blocks.empty() || rng() % 3 != 0;
+            const uint64_t span = vf.blocks.size() * bs + 2 * bs;
+            uint64_t pos = rng() % span;
+            if (rng() % 4 == 0) pos -= pos % VFS_DEFAULT_BLOCK_SIZE;
+            size_t len = size_t(rng() % (3 * bs));
+            if (rng() % 5 == 0) len = size_t(rng() % 5000);
+            if (is_write) {
+                auto d = random_data(len);
+                size_t a = 0, b = 0;
+                const bool okm = m.write(pos, d.data(), len, &b);
+                Status st = vf.write(pos, d.data(), len, &a);
+                CHECK(okm == !st);
+                if (!okm) break;   // both stopped mid-file; states may differ only past the failure
+                CHECK(a == b && vf.size == m.size && vf.blocks.size() == m.buf.size());
+            } else {
+                std::vector<uint8_t> x(len, 0xEE), y(len, 0xEE);
+                size_t a = 0, b = 0;
+                const bool okm = m.read(pos, y.data(), len, &b);
+                Status st = vf.read(pos, x.data(), len, &a);
+                CHECK(okm == !st);
+                if (okm) CHECK(a == b && x == y);
+            }
+        }
+        for (size_t i = 0; i < m.buf.size(); ++i) CHECK(vf.blocks[i].buffer_snapshot() == m.buf[i]);
+    }
+}
+
 void test_virtual_file_errors() {
     auto cfg = test_config();
     VirtualFile vf = VirtualFile::new_with(77, 0);
@@ -387,6 +480,76 @@ void test_replace_block_erasure() {
     CHECK(rb == data);
 }
 
+// Batched load with erasures: one shard file per block removed (data and
+// parity positions), pinned Block-Cache buffers; one reconstruct call.
+void test_virtual_file_batched_reconstruct() {
+    auto cfg = test_config();
+    auto in = read_input();
+    const uint64_t bs = 1024 * 1024;
+    const size_t nblk = in.size() / bs;
+    CHECK(nblk * bs == in.size() && nblk > 0);
+    VirtualFile vf = VirtualFile::new_with(15, 0);
+    vf.populate(cfg);
+    VfsOptions o;
+    o.missing_shard_is_erasure = true;
+    o.pread_from_start = true;
+    o.short_shard_is_erasure = true;
+    o.pinned_buffers = true;
+    for (size_t i = 0; i < nblk; ++i) {
+        VirtualBlock b;
+        CHECK_OK(VirtualBlock::create(15, i + 1, cfg, bs, BlockTopology::erasure(1, 8, 3), &b));
+        vf.blocks.push_back(b);
+    }
+    vf.set_options(o);
+    size_t n = 0;
+    CHECK_OK(vf.write(0, in.data(), in.size(), &n));
+    CHECK(vf.blocks[0].buffer_pinned());
+    CHECK_OK(vf.sync_data(true));
+    CHECK(vf.last_sync.blocks == nblk);
+    for (size_t i = 0; i < nblk; ++i) print_shards(*cfg, i, vf.blocks[i]);
+    CHECK_OK(vf.drop_buffers());
+    CHECK_OK(vf.drop_handles());
+    for (size_t i = 0; i < nblk; ++i) {
+        fs::remove(shard_file(*cfg, vf.blocks[i], i % 11));
+        if (i % 3 == 0) fs::resize_file(shard_file(*cfg, vf.blocks[i], (i + 5) % 11), 100);   // short -> erasure
+    }
+    std::vector<uint8_t> rb(in.size());
+    CHECK_OK(vf.read(0, rb.data(), rb.size(), &n));
+    CHECK(n == in.size());
+    CHECK(vf.last_load.blocks == nblk);   // every block needed a reconstruct, one batch
+    CHECK(rb == in);
+    // the flush after the repair rewrites the lost shard files
+    CHECK_OK(vf.drop_buffers());
+    for (size_t i = 0; i < nblk; ++i)
+        CHECK(fs::exists(shard_file(*cfg, vf.blocks[i], i % 11)) &&
+              fsize(shard_file(*cfg, vf.blocks[i], i % 11)) == calculate_shard_size(bs, 8));
+}
+
+// rewrite_erasure: Single blocks -> Erasure(1, 4, 2), batched.
+void test_rewrite_erasure() {
+    auto cfg = test_config();
+    auto in = read_input();
+    VirtualFile vf = VirtualFile::new_with(16, 0);
+    vf.populate(cfg);
+    size_t n = 0;
+    CHECK_OK(vf.write(0, in.data(), in.size(), &n));
+    const size_t nblk = vf.blocks.size();
+    CHECK_OK(vf.sync_data(true));
+    CHECK_OK(vf.rewrite_erasure(4, 2));
+    CHECK(vf.blocks.size() == nblk);
+    for (size_t i = 0; i < nblk; ++i) {
+        CHECK(vf.blocks[i].topology.kind == BlockTopology::Erasure && vf.blocks[i].topology.data == 4);
+        print_shards(*cfg, i, vf.blocks[i]);
+    }
+    CHECK(vf.last_sync.blocks == nblk);
+    CHECK_OK(vf.drop_buffers());
+    CHECK_OK(vf.drop_handles());
+    std::vector<uint8_t> rb(in.size());
+    CHECK_OK(vf.read(0, rb.data(), rb.size(), &n));
+    CHECK(rb == in);
+    CHECK_OK(vf.rewrite_erasure(4, 2));   // already Erasure(1, 4, 2): no-op
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -408,10 +571,13 @@ int main(int argc, char** argv) {
         {"virtual_file_1", test_virtual_file_1},
         {"virtual_file_2_4_mb", test_virtual_file_2_4_mb},
         {"virtual_file_errors", test_virtual_file_errors},
+        {"virtual_file_chunk_model", test_virtual_file_chunk_model},
         {"erasure_block_sync_load", test_erasure_block_sync_load},
         {"erasure_block_missing_shards", test_erasure_block_missing_shards},
         {"virtual_file_erasure_batch", test_virtual_file_erasure_batch},
         {"replace_block_erasure", test_replace_block_erasure},
+        {"virtual_file_batched_reconstruct", test_virtual_file_batched_reconstruct},
+        {"rewrite_erasure", test_rewrite_erasure},
     };
     auto it = cases.find(name);
     if (it == cases.end()) {

@@ -56,6 +56,7 @@ CPU_CASES = [
     "virtual_file_1",
     "virtual_file_2_4_mb",
     "virtual_file_errors",
+    "virtual_file_chunk_model",
 ]
 
 
@@ -124,3 +125,30 @@ def test_replace_block_erasure(tmp_path, gpu):
     assert len(files) == 6
     for i, f in enumerate(files):
         assert np.array_equal(read(f), want[i]), f"shard {i}"
+
+
+@pytest.mark.gpu
+def test_virtual_file_batched_reconstruct(tmp_path, gpu):
+    nblk, k, p = 12, 8, 3
+    data = np.concatenate([O.seeded_block(O.BENCH_SEED, 400 + i, MiB) for i in range(nblk)])
+    shards = run_case("virtual_file_batched_reconstruct", tmp_path, data)
+    assert sorted(shards) == list(range(nblk))
+    # after the read the repair flush rewrote every shard: all must equal the oracle's
+    for b in range(nblk):
+        want = O.sync_data_erasure(data[b * MiB:(b + 1) * MiB].tobytes(), MiB, k, p)
+        for i, f in enumerate(shards[b]):
+            assert np.array_equal(read(f), want[i]), f"block {b} shard {i}"
+
+
+@pytest.mark.gpu
+def test_rewrite_erasure(tmp_path, gpu):
+    data = O.seeded_block(O.BENCH_SEED, 500, 2 * MiB + 12345)
+    shards = run_case("rewrite_erasure", tmp_path, data)
+    for b, files in sorted(shards.items()):
+        buf = np.zeros(MiB, np.uint8)   # each old Single block loads as a full 1 MiB buffer
+        part = data[b * MiB:(b + 1) * MiB]
+        buf[:len(part)] = part
+        want = O.sync_data_erasure(buf.tobytes(), MiB, 4, 2)
+        assert len(files) == 6
+        for i, f in enumerate(files):
+            assert np.array_equal(read(f), want[i]), f"block {b} shard {i}"
