@@ -170,10 +170,13 @@ int shmr_ec_set_device(shmr_ec_t* rs, int device);
  * per workgroup: 128, 256, 512), "depth" (register ring depth = shards of
  * loads in flight + 1: 1, 2, 3, 5, 9), "wgs_per_cu" (0 = no cap, else the
  * most workgroups resident per CU, enforced by LDS padding), "occ" (0, 6, 7:
- * register budget for that many waves per SIMD), "diag" (0/1:
+ * register budget for that many waves per SIMD), "early" (0/1: issue the
+ * first data loads before the plan's LDS staging completes), "spre" (0/1:
+ * coefficient tables and shard offsets by scalar loads one shard ahead, no
+ * LDS), "diag" (0/1:
  * XOR-only diagnostic kernel, WRONG results, for ceiling measurements).
  * Prefix "encode." or "decode." to set one operation class only.
- * "chunks", "nt_load", "nt_store", "depth" and "occ" default to -2 (auto): a per-shape policy
+ * "chunks", "nt_load", "nt_store", "depth", "occ", "early" and "spre" default to -2 (auto): a per-shape policy
  * of the fastest variants measured on MI355X; any other value pins the knob,
  * and setting -2 returns it to the policy. */
 int shmr_ec_set_tuning(const char* key, int value);

@@ -27,6 +27,8 @@ struct Tuning {
     std::atomic<int> depth{kAuto};
     std::atomic<int> wgs_per_cu{0};
     std::atomic<int> occ{kAuto};
+    std::atomic<int> early{kAuto};
+    std::atomic<int> spre{kAuto};
 };
 Tuning g_tune[2];   // [kEncode], [kDecode]
 
@@ -36,14 +38,17 @@ Tuning g_tune[2];   // [kEncode], [kDecode]
 // that lift RS(8,3) from 5 to 6 waves/SIMD), RS(4,2) 78 % vs 77 %, RS(10,4)
 // 71 % vs 70 %, reconstruct RS(8,3) 72 % vs 71 %; deeper rings (5, 9) and
 // occupancy caps lose.  With depth 2, NT loads + NT stores win everywhere;
-// encodes with 4 rows per launch (RS(10,4)) use U = 2.
+// encodes with 4 rows per launch (RS(10,4)) use U = 2.  Encodes with k < 8
+// (short-lived workgroups) issue their first data loads ahead of the plan
+// staging ("early": RS(4,2) 83 % vs 80 %; neutral at k = 8, -2 % on decode).
+// Scalar-loaded tables ("spre", 7-8 waves/SIMD) lose 3-6 % everywhere.
 kern::Variant variant_policy(OpClass op, unsigned k, unsigned rows) {
-    (void)k;
     kern::Variant v;
     v.u = (op == kEncode && rows >= 4) ? 2 : 1;
     v.nt_store = true;
     v.nt_load = true;
     v.depth = 2;
+    v.early = op == kEncode && k < 8;
     return v;
 }
 
@@ -100,6 +105,10 @@ int set_tuning(const char* key, int value) {
         } else if (k == "occ") {
             if (value != 0 && value != 6 && value != 7 && value != kAuto) return SHMR_EC_INVALID_ARGUMENT;
             T.occ = value;
+        } else if (k == "early") {
+            T.early = value == kAuto ? kAuto : (value != 0);
+        } else if (k == "spre") {
+            T.spre = value == kAuto ? kAuto : (value != 0);
         } else {
             return SHMR_EC_INVALID_ARGUMENT;
         }
@@ -123,6 +132,8 @@ int get_tuning(const char* key) {
     if (k == "depth") return T.depth;
     if (k == "wgs_per_cu") return T.wgs_per_cu;
     if (k == "occ") return T.occ;
+    if (k == "early") return T.early;
+    if (k == "spre") return T.spre;
     return SHMR_EC_INVALID_ARGUMENT;
 }
 
@@ -139,6 +150,8 @@ kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows) {
     if (T.depth.load() != kAuto) v.depth = T.depth.load();
     v.wgs_per_cu = T.wgs_per_cu.load();
     if (T.occ.load() != kAuto) v.occ = T.occ.load();
+    if (T.early.load() != kAuto) v.early = T.early.load() != 0;
+    if (T.spre.load() != kAuto) v.spre = T.spre.load() != 0;
     return v;
 }
 
@@ -199,6 +212,8 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
         int rc = plan_on_device(plan, dev, &dplan);
         if (rc) return rc;
     }
+    bool identity = true;   // encode plans (and decodes that lost only parity) read shard t as input t
+    for (uint32_t t = 0; t < plan.k; ++t) identity = identity && plan.in_idx[t] == t;
     kern::Variant tail;   // tail / unaligned launches: U = 1, plain loads
     const int cap = grid_mode(op);
     const bool aligned = aligned16(uintptr_t(L.in_base)) && aligned16(uintptr_t(L.out_base)) &&
@@ -228,6 +243,7 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
         a.row0 = row0;
         a.plan = dplan;
         a.tab_off = tab_off;
+        a.in_identity = bs.d_plans ? 0u : uint32_t(identity);
         if (!aligned) {
             const uint64_t tb1 = kern::tile_bytes(1);
             a.col_base = 0;

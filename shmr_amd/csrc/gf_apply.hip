@@ -47,6 +47,8 @@ constexpr int kDepth5 = 128;     // 4 shards of loads in flight (default 2)
 constexpr int kDepth9 = 256;     // 8 shards of loads in flight
 constexpr int kDepth2 = 512;     // 1 shard of loads in flight
 constexpr int kDepth1 = 1024;    // no look-ahead (load, wait, multiply)
+constexpr int kEarly = 1 << 16;  // first data loads issued before the plan's LDS staging completes
+constexpr int kSPre = 1 << 17;   // tables + offsets by scalar loads one shard ahead, no LDS
 // Bits 12-15: occupancy target in waves per SIMD (0 = compiler's choice);
 // the register allocator must then fit 512 / target VGPRs.
 constexpr int kOccShift = 12;
@@ -309,6 +311,219 @@ __device__ __forceinline__ void stage_plan(const ApplyArgs& a, const uint8_t* pl
     c.s_out_off = s_out_off;
 }
 
+// ---- early-prefetch tile (flag kEarly) -------------------------------------
+// A workgroup lives for one 4 KiB tile, so its prologue matters: the plain
+// path stages the plan into LDS (global loads -> ds_write -> barrier) before
+// its first data load can issue.  Here the plan's first-pass loads go out
+// first, then the first NB-1 data loads (their shard offsets come from scalar
+// loads of the plan's in_idx), and only then are the plan registers written
+// to LDS -- the compiler's wait for them is vmcnt(NB-1), which leaves the data
+// loads in flight across the LDS barrier (a raw s_barrier: lgkmcnt(0) only).
+
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0), vmcnt/expcnt untouched
+    __builtin_amdgcn_s_barrier();
+}
+
+struct StageRegs {
+    u32x4 tab;
+    uint64_t in_off, out_off;
+};
+
+// First pass of stage_plan (entry threadIdx.x of each array), loaded into
+// registers with clamped indices so every load is unconditional.
+// Global address space: vector loads on vmcnt only (a generic pointer would
+// make them flat loads, which also count on lgkmcnt and serialise against
+// the scalar loads of the prologue).
+typedef __attribute__((address_space(1))) const u32x4 gu32x4;
+typedef __attribute__((address_space(1))) const uint16_t gu16;
+
+template <int R>
+__device__ __forceinline__ void stage_issue(const ApplyArgs& a, const uint8_t* plan, StageRegs& s) {
+    const uint32_t k = a.k, i = threadIdx.x;
+    const uint32_t n16 = k * R * 2;
+    const uint32_t ic = i < n16 ? i : n16 - 1;
+    const uint32_t e = ic >> 1, half = ic & 1;
+    const uint32_t t = e / R, r = e - t * R;
+    s.tab = ((const gu32x4*)(uintptr_t)(plan + a.tab_off))[(size_t(t) * a.m + a.row0 + r) * 2 + half];
+    const gu16* in_idx = (const gu16*)(uintptr_t)(plan + 8);
+    s.in_off = uint64_t(in_idx[i < k ? i : k - 1]) * a.in_spitch;
+    s.out_off = uint64_t(in_idx[k + a.row0 + (i < uint32_t(R) ? i : R - 1)] - a.out_bias) * a.out_spitch;
+}
+
+template <int R, int TH>
+__device__ __forceinline__ void stage_commit(const ApplyArgs& a, const uint8_t* plan, uint8_t* smem, Ctx& c,
+                                             const StageRegs& s) {
+    const uint32_t k = a.k, i = threadIdx.x;
+    u32x4* s_tab = reinterpret_cast<u32x4*>(smem);
+    uint64_t* s_in_off = reinterpret_cast<uint64_t*>(smem + size_t(k) * R * 32);
+    uint64_t* s_out_off = s_in_off + k;
+    const uint32_t n16 = k * R * 2;
+    if (i < n16) s_tab[i] = s.tab;
+    if (i < k) s_in_off[i] = s.in_off;
+    if (i < uint32_t(R)) s_out_off[i] = s.out_off;
+    // entries beyond the first TH (large k * R): plain staging
+    const u32x4* ptab = reinterpret_cast<const u32x4*>(plan + a.tab_off);
+    const uint16_t* in_idx = reinterpret_cast<const uint16_t*>(plan + 8);
+    for (uint32_t j = i + TH; j < n16; j += TH) {
+        const uint32_t e = j >> 1, half = j & 1;
+        const uint32_t t = e / R, r = e - t * R;
+        s_tab[j] = ptab[(size_t(t) * a.m + a.row0 + r) * 2 + half];
+    }
+    for (uint32_t t = i + TH; t < k; t += TH) s_in_off[t] = uint64_t(in_idx[t]) * a.in_spitch;
+    c.s_tab = s_tab;
+    c.s_in_off = s_in_off;
+    c.s_out_off = s_out_off;
+}
+
+template <int R, int U, int MODE, int F>
+__device__ __forceinline__ void early_tile(const ApplyArgs& a, const uint8_t* plan, uint8_t* smem, bool first,
+                                           const uint8_t* ib, uint8_t* ob, uint64_t col0) {
+    constexpr int TH = threads_of<F>();
+    constexpr int NB = depth_of<F>();
+    const uint32_t k = a.k;
+    const uint64_t len = a.len;
+    const uint32_t tid = threadIdx.x;
+    const uint16_t* in_idx = reinterpret_cast<const uint16_t*>(plan + 8);
+    StageRegs sr;
+    stage_issue<R>(a, plan, sr);
+    __builtin_amdgcn_sched_barrier(0);
+    u32x4 ring[NB][U];
+#pragma unroll
+    for (int i = 0; i < NB - 1; ++i) {
+        const uint32_t t = uint32_t(i) < k ? uint32_t(i) : k - 1;
+        const uint8_t* base = ib + uint64_t(plan_u16(in_idx, t)) * a.in_spitch;
+#pragma unroll
+        for (int u = 0; u < U; ++u) ring[i][u] = ld<MODE, F>(base, col0 + (uint64_t(u) * TH + tid) * 16, len);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (!first) lds_barrier();   // the previous tile's LDS readers are done
+    Ctx c{};
+    stage_commit<R, TH>(a, plan, smem, c, sr);
+    lds_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+
+    uint32_t acc[U][R][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[u][r][j] = 0u;
+    auto load = [&](u32x4 (&buf)[U], uint32_t t) {
+        const uint32_t tt = t < k ? t : k - 1;
+        const uint8_t* base = ib + c.s_in_off[tt];
+#pragma unroll
+        for (int u = 0; u < U; ++u) buf[u] = ld<MODE, F>(base, col0 + (uint64_t(u) * TH + tid) * 16, len);
+    };
+    auto consume = [&](const u32x4 (&buf)[U], uint32_t t) {
+        Tab tb[R];
+        read_tabs<R, F>(a, c, t, tb);
+#pragma unroll
+        for (int u = 0; u < U; ++u) mac<R, F>(acc[u], buf[u], tb);
+    };
+    for (uint32_t t = 0; t < k; t += NB) {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            load(ring[(i + NB - 1) % NB], t + i + NB - 1);
+            __builtin_amdgcn_sched_barrier(0);
+            if (t + i < k) consume(ring[i], t + i);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        uint8_t* o = ob + c.s_out_off[r];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            st<MODE, F>(o, col0 + (uint64_t(u) * TH + tid) * 16, len,
+                        u32x4{acc[u][r][0], acc[u][r][1], acc[u][r][2], acc[u][r][3]});
+    }
+}
+
+// ---- scalar-table tile (flag kSPre) --------------------------------------
+// No LDS: shard offsets (in_idx) and the coefficient tables are wave-uniform,
+// so they come from the plan image by scalar loads (constant address space)
+// into SGPRs; only the table words v_perm cannot take from an SGPR are copied
+// to VGPRs.  Frees the ~5 VGPRs per row the LDS-staged tables occupy and
+// removes the staging prologue and barrier.  Per step: issue the data load
+// for shard t+NB-1 (its offset was fetched during the previous step), the
+// scalar loads of shard t's tables and of the next offset, then multiply
+// shard t -- the scalar latency (a K$ hit) hides under the data wait.
+template <int R>
+__device__ __forceinline__ void s_tabs(const ApplyArgs& a, const uint8_t* plan, uint32_t t, Tab (&tb)[R]) {
+    const cu32* e0 = as_const<cu32>(plan + a.tab_off) + (size_t(t) * a.m + a.row0) * 8;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const cu32* e = e0 + r * 8;
+        tb[r] = Tab{e[0], e[1], e[2], e[3], e[4]};
+    }
+}
+
+template <int R, int U, int MODE, int F, bool IDENT>
+__device__ __forceinline__ void spre_tile(const ApplyArgs& a, const uint8_t* plan, const uint8_t* ib, uint8_t* ob,
+                                          uint64_t col0) {
+    constexpr int TH = threads_of<F>();
+    constexpr int NB = depth_of<F>();
+    const uint32_t k = a.k;
+    const uint64_t len = a.len;
+    const uint32_t tid = threadIdx.x;
+    const uint16_t* in_idx = reinterpret_cast<const uint16_t*>(plan + 8);
+    auto in_off = [&](uint32_t t) {
+        const uint32_t tt = t < k ? t : k - 1;
+        if constexpr (IDENT) return uint64_t(tt) * a.in_spitch;   // pure scalar arithmetic
+        else return uint64_t(plan_u16(in_idx, tt)) * a.in_spitch;
+    };
+    uint32_t acc[U][R][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[u][r][j] = 0u;
+    auto load = [&](u32x4 (&buf)[U], uint64_t off) {
+        const uint8_t* base = ib + off;
+#pragma unroll
+        for (int u = 0; u < U; ++u) buf[u] = ld<MODE, F>(base, col0 + (uint64_t(u) * TH + tid) * 16, len);
+    };
+    u32x4 ring[NB][U];
+#pragma unroll
+    for (int i = 0; i < NB - 1; ++i) load(ring[i], in_off(i));
+    uint64_t next_off = in_off(NB - 1);
+    __builtin_amdgcn_sched_barrier(0);
+    for (uint32_t t = 0; t < k; t += NB) {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            load(ring[(i + NB - 1) % NB], next_off);   // shard t+i+NB-1
+            __builtin_amdgcn_sched_barrier(0);
+            next_off = in_off(t + i + NB);
+            // Unconditional multiply (a branch here lets the compiler sink
+            // the look-ahead load into it, collapsing the ring): past the
+            // last shard the tables are zeroed, so the product is 0.
+            {
+                const bool live = t + i < k;
+                Tab tb[R];
+                s_tabs<R>(a, plan, live ? t + i : k - 1, tb);
+                const uint32_t msk = live ? ~0u : 0u;
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    tb[r] = Tab{tb[r].t0lo & msk, tb[r].t0hi & msk, tb[r].t1lo & msk, tb[r].t1hi & msk, tb[r].t2 & msk};
+#pragma unroll
+                for (int u = 0; u < U; ++u) mac<R, F>(acc[u], ring[i][u], tb);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        uint8_t* o = ob + uint64_t(plan_u16(in_idx, k + a.row0 + r) - a.out_bias) * a.out_spitch;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            st<MODE, F>(o, col0 + (uint64_t(u) * TH + tid) * 16, len,
+                        u32x4{acc[u][r][0], acc[u][r][1], acc[u][r][2], acc[u][r][3]});
+    }
+}
+
 // The second __launch_bounds__ argument is amdgpu_waves_per_eu (minimum).
 template <int R, int U, int MODE, int F>
 __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) void gf_apply_kernel(const ApplyArgs a) {
@@ -318,6 +533,34 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
     // Multi-plan launches (reconstruct batches with several erasure patterns)
     // pick the plan per block; single-plan launches stage it once.
     const bool multi = a.plan_table != nullptr;
+    if constexpr ((F & (kEarly | kSPre)) != 0) {
+        const uint32_t tpb = a.tiles_per_block;
+        const uint64_t tb = uint64_t(TH) * 16 * U;
+        for (uint64_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+            const uint64_t j = tile / tpb;
+            const uint64_t cc = tile - j * tpb;
+            const uint64_t blk = a.blk_list ? uint64_t(as_const<cu32>(a.blk_list)[j]) : a.blk_first + j * a.blk_stride;
+            uint64_t pa = reinterpret_cast<uint64_t>(a.plan);
+            if (multi) {   // plan_table[blk_plan[j]] through scalar loads
+                const uint32_t pi = plan_u16(a.blk_plan, uint32_t(j));
+                const cu32* pt = as_const<cu32>(a.plan_table);
+                pa = uint64_t(pt[2 * pi]) | (uint64_t(pt[2 * pi + 1]) << 32);
+            }
+            const uint8_t* plan = reinterpret_cast<const uint8_t*>(pa);
+            if constexpr ((F & kSPre) != 0) {
+                if (a.in_identity)
+                    spre_tile<R, U, MODE, F, true>(a, plan, a.in_base + blk * a.in_bpitch,
+                                                   a.out_base + blk * a.out_bpitch, a.col_base + cc * tb);
+                else
+                    spre_tile<R, U, MODE, F, false>(a, plan, a.in_base + blk * a.in_bpitch,
+                                                    a.out_base + blk * a.out_bpitch, a.col_base + cc * tb);
+            }
+            else
+                early_tile<R, U, MODE, F>(a, plan, smem, tile == blockIdx.x, a.in_base + blk * a.in_bpitch,
+                                          a.out_base + blk * a.out_bpitch, a.col_base + cc * tb);
+        }
+        return;
+    }
     Ctx c{};
     if (!multi) {
         if constexpr (kLds) {
@@ -356,7 +599,7 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
 template <int R, int U, int MODE, int F>
 hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStream_t stream) {
     auto kern = gf_apply_kernel<R, U, MODE, F>;
-    size_t lds = (F & kScalarTabs) ? 0 : size_t(a.k) * R * 32 + size_t(a.k) * 8 + size_t(R) * 8;
+    size_t lds = (F & (kScalarTabs | kSPre)) ? 0 : size_t(a.k) * R * 32 + size_t(a.k) * 8 + size_t(R) * 8;
     // Optional occupancy cap: pad the LDS allocation so at most wgs_per_cu
     // workgroups fit in a CU's 160 KiB.
     if (v.wgs_per_cu > 0) {
@@ -431,13 +674,21 @@ hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStr
     X(1, kNtLoad | kNtStore | kDepth2 | (7 << kOccShift)) \
     X(1, kNtLoad | kNtStore | (6 << kOccShift)) \
     X(1, kNtLoad | kNtStore | (7 << kOccShift)) \
-    X(2, kNtLoad | kNtStore | kDepth2 | (6 << kOccShift))
+    X(2, kNtLoad | kNtStore | kDepth2 | (6 << kOccShift)) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly) \
+    X(1, kNtLoad | kNtStore | kEarly) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | (6 << kOccShift)) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSPre) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSPre) \
+    X(1, kNtLoad | kNtStore | kSPre)
 
 int variant_flags(const Variant& v) {
     return (v.nt_load ? kNtLoad : 0) | (v.nt_store ? kNtStore : 0) | (v.scalar_tabs ? kScalarTabs : 0) |
            (v.occ8 ? kOcc8 : 0) | (v.diag ? kDiagXor : 0) | (v.threads == 128 ? kTh128 : 0) |
            (v.threads == 512 ? kTh512 : 0) | (v.depth == 5 ? kDepth5 : 0) | (v.depth == 9 ? kDepth9 : 0) |
-           (v.depth == 2 ? kDepth2 : 0) | (v.depth == 1 ? kDepth1 : 0) | ((v.occ & 15) << kOccShift);
+           (v.depth == 2 ? kDepth2 : 0) | (v.depth == 1 ? kDepth1 : 0) | ((v.occ & 15) << kOccShift) |
+           (v.early ? kEarly : 0) | (v.spre ? kSPre : 0);
 }
 
 template <int R>

@@ -39,6 +39,7 @@ struct ApplyArgs {
     const uint8_t* const* plan_table;
     const uint16_t* blk_plan;
     uint32_t tab_off;        // byte offset of the PermTab array in the image
+    uint32_t in_identity;    // every plan of the launch reads input t from shard t (in_idx[t] == t)
 };
 
 // Compiled-in kernel variant for full tiles (see gf_apply.hip dispatch_full).
@@ -53,6 +54,8 @@ struct Variant {
     int depth = 3;           // register ring depth: shards of loads in flight + 1 (1, 2, 3, 5, 9)
     int wgs_per_cu = 0;      // > 0: cap resident workgroups per CU (LDS padding)
     int occ = 0;             // > 0: register budget for this many waves per SIMD (6, 7)
+    bool early = false;      // first data loads before the plan's LDS staging completes
+    bool spre = false;       // tables/offsets by scalar loads one shard ahead (no LDS)
 };
 
 // rows in [1, kMaxRowsPerLaunch].  mode 0: full tiles, every shard base

@@ -196,6 +196,9 @@ def test_tuning_api():
     assert "nt_load=1 nt_store=1" in shmr_amd.describe_variant(False, 4, 2)
     assert "nt_load=1" in shmr_amd.describe_variant(True, 8, 1)
     assert "depth=2" in shmr_amd.describe_variant(True, 8, 1)
+    assert "early=1" in shmr_amd.describe_variant(False, 4, 2)
+    assert "early=0" in shmr_amd.describe_variant(False, 8, 3)
+    assert "early=0" in shmr_amd.describe_variant(True, 4, 2)
 
 
 def test_auto_policy_variants_are_compiled():
