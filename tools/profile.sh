@@ -18,5 +18,7 @@ for C in FETCH_SIZE WRITE_SIZE; do
     > "$OUT/$C.log" 2>&1
   rc=$?; echo "pmc $C rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
+# merge into a copy of the tracked table (gpurun_out/ is not pushed to the box)
+[ -f "$ROOT/gpurun_out/pmc_traffic.json" ] || cp "$ROOT/profiles/pmc_traffic.json" "$ROOT/gpurun_out/pmc_traffic.json"
 python3 "$ROOT/tools/pmc_traffic.py" "$OUT" --config "$CFG" --blocks "$BLOCKS" --algo-bytes "$ALGO" \
   --merge "$ROOT/gpurun_out/pmc_traffic.json"
