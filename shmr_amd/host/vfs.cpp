@@ -12,6 +12,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <future>
 #include <map>
 #include <new>
 #include <thread>
@@ -655,6 +656,11 @@ void VirtualFile::set_options(const VfsOptions& o) {
     for (auto& b : blocks) b.set_options(o);
 }
 
+size_t VirtualFile::batch_bytes(bool load) const {
+    if (pipeline_batch_bytes != kAutoBatch) return pipeline_batch_bytes;
+    return (opt_.pinned_buffers && !load) ? size_t(128) << 20 : 0;
+}
+
 Status VirtualFile::allocate_block() {
     if (!cfg_) return fs_error(EINVAL);
     VirtualBlock b;
@@ -842,51 +848,76 @@ Status VirtualFile::sync_data(bool force) {
         g.members.swap(live);
     }
     last_sync.prepare_s = now_s() - t0;
-    // one pipelined multi-GPU encode per (k, p, S)
-    const double t1 = now_s();
+    // Batches of ~64 MiB of data per (k, p, S): the encode of batch b+1 (one
+    // pipelined multi-GPU call) overlaps the shard-file writes of batch b
+    // (every (block, shard) file of the batch in parallel, block.rs:436-439).
+    struct Batch {
+        const Group* g;
+        size_t b, e;   // members [b, e)
+    };
+    std::vector<Batch> batches;
     for (auto& kv : groups) {
-        Group& g = kv.second;
-        if (g.members.empty()) continue;
-        const size_t n = size_t(g.k) + g.p;
-        std::vector<uint8_t*> ptrs(g.members.size() * n);
-        for (size_t j = 0; j < g.members.size(); ++j) shard_ptrs(blocks[g.members[j]].st_->buffer, n, g.S, &ptrs[j * n]);
+        const Group& g = kv.second;
+        const size_t bb = batch_bytes(false);
+        const size_t per = bb == 0 ? g.members.size() : std::max<size_t>(1, bb / std::max<size_t>(1, size_t(g.k) * g.S));
+        for (size_t b = 0; b < g.members.size(); b += per) batches.push_back({&g, b, std::min(g.members.size(), b + per)});
+    }
+    auto encode_batch = [&](const Batch& bt) {
+        const Group& g = *bt.g;
+        const size_t n = size_t(g.k) + g.p, nb = bt.e - bt.b;
+        std::vector<uint8_t*> ptrs(nb * n);
+        for (size_t j = 0; j < nb; ++j) shard_ptrs(blocks[g.members[bt.b + j]].st_->buffer, n, g.S, &ptrs[j * n]);
         EcStatus es;
         auto r = ReedSolomon::create(g.k, g.p, &es);
-        const int rc = r ? shmr_ec_encode_blocks_host(r->handle(), ptrs.data(), g.members.size(), g.S, devices.data(),
+        const int rc = r ? shmr_ec_encode_blocks_host(r->handle(), ptrs.data(), nb, g.S, devices.data(),
                                                       int(devices.size()))
                          : es.code;
         if (rc != SHMR_EC_OK)
-            for (size_t i : g.members) results[i] = ec_error(rc);
-        last_sync.blocks += g.members.size();
-    }
-    last_sync.codec_s = now_s() - t1;
-    // every shard file of the batch, written in parallel (block.rs:436-439)
-    const double t2 = now_s();
-    struct Task {
-        size_t blk, shard, S;
+            for (size_t j = bt.b; j < bt.e; ++j) results[g.members[j]] = ec_error(rc);
     };
-    std::vector<Task> tasks;
-    for (auto& kv : groups)
-        for (size_t i : kv.second.members)
-            if (!results[i])
-                for (size_t s = 0; s < size_t(kv.second.k) + kv.second.p && s < blocks[i].st_->handles.size(); ++s)
-                    tasks.push_back({i, s, kv.second.S});
-    std::vector<Status> task_res(tasks.size());
-    parallel_for(tasks.size(), 32, [&](size_t t) {
-        const Task& tk = tasks[t];
-        auto& st = *blocks[tk.blk].st_;
-        task_res[t] = st.ensure_fd(tk.shard, *cfg_);
-        if (!task_res[t])
-            task_res[t] = write_path(st.handles[tk.shard].second, st.buffer.data() + tk.shard * tk.S, tk.S,
-                                     blocks[tk.blk].opt_.fsync_shards);
-    });
-    for (size_t t = 0; t < tasks.size(); ++t)
-        if (task_res[t] && !results[tasks[t].blk]) results[tasks[t].blk] = task_res[t];
-    for (auto& kv : groups)
-        for (size_t i : kv.second.members)
-            if (!results[i]) blocks[i].st_->should_flush.store(false);
+    auto write_batch = [&](const Batch& bt) {
+        const Group& g = *bt.g;
+        struct Task {
+            size_t blk, shard;
+        };
+        std::vector<Task> tasks;
+        for (size_t j = bt.b; j < bt.e; ++j) {
+            const size_t i = g.members[j];
+            if (results[i]) continue;
+            for (size_t sh = 0; sh < size_t(g.k) + g.p && sh < blocks[i].st_->handles.size(); ++sh) tasks.push_back({i, sh});
+        }
+        std::vector<Status> task_res(tasks.size());
+        parallel_for(tasks.size(), 32, [&](size_t t) {
+            auto& st = *blocks[tasks[t].blk].st_;
+            task_res[t] = st.ensure_fd(tasks[t].shard, *cfg_);
+            if (!task_res[t])
+                task_res[t] = write_path(st.handles[tasks[t].shard].second, st.buffer.data() + tasks[t].shard * g.S,
+                                         g.S, blocks[tasks[t].blk].opt_.fsync_shards);
+        });
+        for (size_t t = 0; t < tasks.size(); ++t)
+            if (task_res[t] && !results[tasks[t].blk]) results[tasks[t].blk] = task_res[t];
+        for (size_t j = bt.b; j < bt.e; ++j)
+            if (!results[g.members[j]]) blocks[g.members[j]].st_->should_flush.store(false);
+    };
+    const double t1 = now_s();
+    double io_busy = 0;
+    std::future<void> writer;
+    for (const Batch& bt : batches) {
+        const double te = now_s();
+        encode_batch(bt);
+        last_sync.codec_s += now_s() - te;
+        last_sync.blocks += bt.e - bt.b;
+        if (writer.valid()) writer.get();
+        writer = std::async(std::launch::async, [&, bt] {
+            const double tw = now_s();
+            write_batch(bt);
+            io_busy += now_s() - tw;
+        });
+    }
+    if (writer.valid()) writer.get();
+    last_sync.io_s = io_busy;
+    last_sync.total_s = now_s() - t1;
     locks.held.clear();
-    last_sync.io_s = now_s() - t2;
     parallel_for(others.size(), 16, [&](size_t j) { results[others[j]] = blocks[others[j]].sync_data(force); });
     for (auto& r : results)
         if (r) return r;
@@ -942,35 +973,53 @@ Status VirtualFile::load_blocks(const std::vector<size_t>& block_indices) {
         }
     }
     last_load.prepare_s = now_s() - t0;
-    const double t1 = now_s();
-    std::vector<uint8_t> present(tasks.size(), 0), odd(tasks.size(), 0);
-    parallel_for(tasks.size(), 32, [&](size_t t) {
-        const Task& tk = tasks[t];
-        const VfsOptions& o = blocks[tk.blk].opt_;
-        bool od = false;
-        if (tk.fd >= 0 && read_slot(tk.fd, tk.slot, tk.S, o.pread_from_start, &od) == 0) {
-            present[t] = !(od && o.short_shard_is_erasure);
-            odd[t] = od;
-        }
-    });
-    last_load.io_s = now_s() - t1;
-    const double t2 = now_s();
+    // Batches of ~64 MiB per (k, p, S): the shard-file reads of batch b+1
+    // overlap the reconstruct of batch b (one pipelined multi-GPU call for
+    // the blocks of b that have an erasure).
+    struct Batch {
+        const Group* g;
+        size_t b, e;   // members [b, e)
+    };
+    std::vector<Batch> batches;
     for (auto& kv : groups) {
-        Group& g = kv.second;
+        const Group& g = kv.second;
+        const size_t bb = batch_bytes(true);
+        const size_t per = bb == 0 ? g.members.size() : std::max<size_t>(1, bb / std::max<size_t>(1, size_t(g.k) * g.S));
+        for (size_t b = 0; b < g.members.size(); b += per) batches.push_back({&g, b, std::min(g.members.size(), b + per)});
+    }
+    std::vector<uint8_t> present(tasks.size(), 0), odd(tasks.size(), 0);
+    auto read_batch = [&](const Batch& bt) {
+        const size_t n = size_t(bt.g->k) + bt.g->p;
+        const size_t t0b = first_task[bt.g->members[bt.b]];
+        const size_t nt = (bt.e - bt.b) * n;   // a batch's tasks are contiguous
+        parallel_for(nt, 32, [&](size_t q) {
+            const size_t t = t0b + q;
+            const Task& tk = tasks[t];
+            const VfsOptions& o = blocks[tk.blk].opt_;
+            bool od = false;
+            if (tk.fd >= 0 && read_slot(tk.fd, tk.slot, tk.S, o.pread_from_start, &od) == 0) {
+                present[t] = !(od && o.short_shard_is_erasure);
+                odd[t] = od;
+            }
+        });
+    };
+    auto reconstruct_batch = [&](const Batch& bt) {
+        const Group& g = *bt.g;
         const size_t n = size_t(g.k) + g.p;
         std::vector<size_t> need;
-        for (size_t i : g.members) {
+        for (size_t j = bt.b; j < bt.e; ++j) {
+            const size_t i = g.members[j];
             bool missing = false;
-            for (size_t s = 0; s < n; ++s) missing |= !present[first_task[i] + s] || odd[first_task[i] + s];
+            for (size_t sh = 0; sh < n; ++sh) missing |= !present[first_task[i] + sh] || odd[first_task[i] + sh];
             if (missing) need.push_back(i);
         }
         if (!need.empty()) {
             std::vector<uint8_t*> ptrs(need.size() * n);
             std::vector<uint8_t> pres(need.size() * n);
             for (size_t j = 0; j < need.size(); ++j)
-                for (size_t s = 0; s < n; ++s) {
-                    ptrs[j * n + s] = tasks[first_task[need[j]] + s].slot;
-                    pres[j * n + s] = present[first_task[need[j]] + s];
+                for (size_t sh = 0; sh < n; ++sh) {
+                    ptrs[j * n + sh] = tasks[first_task[need[j]] + sh].slot;
+                    pres[j * n + sh] = present[first_task[need[j]] + sh];
                 }
             EcStatus es;
             auto r = ReedSolomon::create(g.k, g.p, &es);
@@ -981,13 +1030,33 @@ Status VirtualFile::load_blocks(const std::vector<size_t>& block_indices) {
                 for (size_t i : need) results[i] = ec_error(rc);
             last_load.blocks += need.size();
         }
-        for (size_t i : g.members) {
+        for (size_t j = bt.b; j < bt.e; ++j) {
+            const size_t i = g.members[j];
             if (results[i]) continue;
             blocks[i].st_->buffer.resize(blocks[i].size);   // ec_data[..size]
             blocks[i].st_->buffer_loaded.store(true);
         }
+    };
+    const double t1 = now_s();
+    double io_busy = 0;
+    std::future<void> reader;
+    auto start_read = [&](size_t bi) {
+        reader = std::async(std::launch::async, [&, bi] {
+            const double tr = now_s();
+            read_batch(batches[bi]);
+            io_busy += now_s() - tr;
+        });
+    };
+    if (!batches.empty()) start_read(0);
+    for (size_t bi = 0; bi < batches.size(); ++bi) {
+        reader.get();
+        if (bi + 1 < batches.size()) start_read(bi + 1);
+        const double tc = now_s();
+        reconstruct_batch(batches[bi]);
+        last_load.codec_s += now_s() - tc;
     }
-    last_load.codec_s = now_s() - t2;
+    last_load.io_s = io_busy;
+    last_load.total_s = now_s() - t1;
     locks.held.clear();
     parallel_for(others.size(), 16, [&](size_t j) { results[others[j]] = blocks[others[j]].load_block(); });
     for (auto& r : results)

@@ -41,12 +41,13 @@ struct Result {
 };
 
 Result run_once(const std::shared_ptr<const ShmrFsConfig>& cfg, uint64_t ino, const std::vector<uint8_t>& src,
-                uint64_t block_bytes, const VfsOptions& opt) {
+                uint64_t block_bytes, const VfsOptions& opt, size_t batch_bytes) {
     Result r;
     const size_t nblk = src.size() / block_bytes;
     VirtualFile vf = VirtualFile::new_with(ino, 0);
     vf.populate(cfg);
     vf.block_size = block_bytes;
+    vf.pipeline_batch_bytes = batch_bytes;
     for (size_t i = 0; i < nblk; ++i) {
         VirtualBlock b;
         DIE_IF(VirtualBlock::create(ino, i + 1, cfg, block_bytes, BlockTopology::erasure(1, 8, 3), &b));
@@ -129,7 +130,9 @@ int main(int argc, char** argv) {
     }
     const double GiB = double(1ull << 30);
     const double bytes = double(src.size());
-    for (int pinned = 1; pinned >= 0; --pinned) {
+    const size_t batch_mib[] = {VirtualFile::kAutoBatch, 0};
+    for (int pinned = 1; pinned >= 0; --pinned)
+    for (size_t bm : batch_mib) {
         VfsOptions o;
         o.missing_shard_is_erasure = true;
         o.pread_from_start = true;
@@ -139,7 +142,7 @@ int main(int argc, char** argv) {
         Result best;
         best.sync_s = best.read_s = best.write_s = best.per_block_sync_s = 1e30;
         for (int rep = 0; rep < reps + 1; ++rep) {   // rep 0 warms plans, staging, clocks
-            Result r = run_once(cfg, 1000 + rep, src, block_bytes, o);
+            Result r = run_once(cfg, 1000 + rep, src, block_bytes, o, bm == VirtualFile::kAutoBatch ? bm : bm << 20);
             if (rep == 0) continue;
             if (r.sync_s < best.sync_s) {
                 best.sync_s = r.sync_s;
@@ -153,15 +156,18 @@ int main(int argc, char** argv) {
             best.per_block_sync_s = std::min(best.per_block_sync_s, r.per_block_sync_s);
         }
         std::printf(
-            "{\"buffers\": \"%s\", \"file_MiB\": %llu, \"block_MiB\": %llu, \"topology\": \"Erasure(1, 8, 3)\", "
+            "{\"buffers\": \"%s\", \"batch\": \"%s\", \"file_MiB\": %llu, \"block_MiB\": %llu, \"topology\": \"Erasure(1, 8, 3)\", "
             "\"fsync\": %d, \"reps\": %d, \"unit\": \"GiB/s of file data (best rep)\", "
             "\"write_GiBps\": %.2f, \"sync_GiBps\": %.2f, \"sync_encode_GiBps\": %.2f, \"sync_shard_io_GiBps\": %.2f, "
-            "\"per_block_sync_GiBps\": %.2f, \"read_with_erasure_GiBps\": %.2f, \"read_reconstruct_GiBps\": %.2f, "
-            "\"read_shard_io_GiBps\": %.2f, \"reconstructed_blocks\": %zu, \"verified\": true}\n",
-            pinned ? "pinned" : "pageable", (unsigned long long)file_mib, (unsigned long long)block_mib, int(do_fsync),
+            "\"sync_pipeline_GiBps\": %.2f, \"per_block_sync_GiBps\": %.2f, \"read_with_erasure_GiBps\": %.2f, "
+            "\"read_reconstruct_GiBps\": %.2f, \"read_shard_io_GiBps\": %.2f, \"read_pipeline_GiBps\": %.2f, "
+            "\"reconstructed_blocks\": %zu, \"verified\": true}\n",
+            pinned ? "pinned" : "pageable", bm == VirtualFile::kAutoBatch ? "auto" : "one batch",
+            (unsigned long long)file_mib, (unsigned long long)block_mib, int(do_fsync),
             reps, bytes / best.write_s / GiB, bytes / best.sync_s / GiB, bytes / best.sync.codec_s / GiB,
-            bytes / best.sync.io_s / GiB, bytes / best.per_block_sync_s / GiB, bytes / best.read_s / GiB,
-            bytes / best.load.codec_s / GiB, bytes / best.load.io_s / GiB, best.load.blocks);
+            bytes / best.sync.io_s / GiB, bytes / best.sync.total_s / GiB, bytes / best.per_block_sync_s / GiB,
+            bytes / best.read_s / GiB, bytes / best.load.codec_s / GiB, bytes / best.load.io_s / GiB,
+            bytes / best.load.total_s / GiB, best.load.blocks);
         std::fflush(stdout);
     }
     return 0;

@@ -501,6 +501,7 @@ void test_virtual_file_batched_reconstruct() {
         vf.blocks.push_back(b);
     }
     vf.set_options(o);
+    vf.pipeline_batch_bytes = 3 * 1024 * 1024;   // 3 blocks per batch: exercises the pipelined batches
     size_t n = 0;
     CHECK_OK(vf.write(0, in.data(), in.size(), &n));
     CHECK(vf.blocks[0].buffer_pinned());
