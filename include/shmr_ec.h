@@ -153,10 +153,20 @@ int shmr_ec_reconstruct_blocks_host(shmr_ec_t* rs, uint8_t* const* host_shards, 
                                     size_t nblocks, size_t shard_len, int data_only,
                                     const int* devices, int ndev);
 
-/* Pinned (page-locked) host memory for Block Cache buffers: the host-buffer
- * entry points DMA it directly without a staging copy. */
+/* Mapped (page-locked, device-visible from every GPU) host memory for Block
+ * Cache buffers.  When every shard a host-buffer call touches (shmr_ec_encode,
+ * shmr_ec_reconstruct, the *_blocks_host batches) lies in memory from
+ * shmr_ec_host_alloc or a range given to shmr_ec_host_register, the kernels
+ * read and write those buffers in place across PCIe (zero-copy: no staging
+ * copies, no device buffers); otherwise the call stages through device memory. */
 int shmr_ec_host_alloc(size_t bytes, void** out);
 void shmr_ec_host_free(void* p);
+
+/* Page-locks and maps an existing host range (e.g. a Rust Vec<u8> Block Cache
+ * buffer) for zero-copy use; shmr_ec_host_unregister(p) with the same p undoes
+ * it.  The range must stay allocated while registered. */
+int shmr_ec_host_register(void* p, size_t bytes);
+int shmr_ec_host_unregister(void* p);
 
 /* ---- configuration -------------------------------------------------------- */
 
@@ -192,6 +202,10 @@ int shmr_ec_cache_stats(const shmr_ec_t* rs, uint64_t* hits, uint64_t* misses);
 
 /* Number of visible GPUs (0 when none; never fails). */
 int shmr_ec_device_count(void);
+
+/* Blocks the host-buffer entry points served zero-copy (mapped memory) and
+ * through device staging since the library was loaded.  Either may be NULL. */
+int shmr_ec_path_stats(uint64_t* zero_copy_blocks, uint64_t* staged_blocks);
 
 #ifdef __cplusplus
 }

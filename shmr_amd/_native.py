@@ -51,6 +51,9 @@ SIGNATURES = [
      [ctypes.c_void_p, _u8pp, _u8p, _sz, _sz, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     ("shmr_ec_host_alloc", ctypes.c_int, [_sz, ctypes.POINTER(ctypes.c_void_p)]),
     ("shmr_ec_host_free", None, [ctypes.c_void_p]),
+    ("shmr_ec_host_register", ctypes.c_int, [ctypes.c_void_p, _sz]),
+    ("shmr_ec_host_unregister", ctypes.c_int, [ctypes.c_void_p]),
+    ("shmr_ec_path_stats", ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     ("shmr_ec_set_device", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("shmr_ec_set_tuning", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
     ("shmr_ec_get_tuning", ctypes.c_int, [ctypes.c_char_p]),

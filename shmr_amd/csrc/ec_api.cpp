@@ -144,18 +144,57 @@ int shmr_ec_cache_stats(const shmr_ec_t* rs, uint64_t* hits, uint64_t* misses) {
 
 int shmr_ec_device_count(void) { return core::device_count(); }
 
+int shmr_ec_path_stats(uint64_t* zero_copy_blocks, uint64_t* staged_blocks) {
+    core::path_stats(zero_copy_blocks, staged_blocks);
+    return SHMR_EC_OK;
+}
+
 // ---- pinned host memory (Block Cache buffers) --------------------------------
+// Mapped + portable: every GPU of the node can address it, so the host-buffer
+// entry points run their kernels on it in place (zero-copy).
 int shmr_ec_host_alloc(size_t bytes, void** out) {
     if (!out) return SHMR_EC_INVALID_ARGUMENT;
     *out = nullptr;
     int rc = core::check_device(0);
     if (rc) return rc;
-    if (hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return SHMR_EC_OUT_OF_MEMORY;
+    const size_t n = bytes ? bytes : 1;
+    if (hipHostMalloc(out, n, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) {
+        *out = nullptr;
+        return SHMR_EC_OUT_OF_MEMORY;
+    }
+    void* dev = nullptr;
+    if (hipHostGetDevicePointer(&dev, *out, 0) == hipSuccess && dev) core::mapped_add(*out, n, dev);
+    else (void)hipGetLastError();   // still pinned: the staged DMA path takes it
     return SHMR_EC_OK;
 }
 
 void shmr_ec_host_free(void* p) {
-    if (p) (void)hipHostFree(p);
+    if (!p) return;
+    core::mapped_remove(p);
+    (void)hipHostFree(p);
+}
+
+int shmr_ec_host_register(void* p, size_t bytes) {
+    if (!p || bytes == 0) return SHMR_EC_INVALID_ARGUMENT;
+    int rc = core::check_device(0);
+    if (rc) return rc;
+    if (hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable) != hipSuccess) {
+        (void)hipGetLastError();
+        return SHMR_EC_DEVICE_ERROR;
+    }
+    void* dev = nullptr;
+    if (hipHostGetDevicePointer(&dev, p, 0) != hipSuccess || !dev) {
+        (void)hipGetLastError();
+        (void)hipHostUnregister(p);
+        return SHMR_EC_DEVICE_ERROR;
+    }
+    core::mapped_add(p, bytes, dev);
+    return SHMR_EC_OK;
+}
+
+int shmr_ec_host_unregister(void* p) {
+    if (!p || !core::mapped_remove(p)) return SHMR_EC_INVALID_ARGUMENT;
+    return hipHostUnregister(p) == hipSuccess ? SHMR_EC_OK : SHMR_EC_DEVICE_ERROR;
 }
 
 // ---- host-buffer encode (ReedSolomon::encode) --------------------------------------
@@ -175,6 +214,13 @@ int shmr_ec_encode(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_le
     const int dev = rs->device;
     int rc = core::check_device(dev);
     if (rc) return rc;
+    {   // shards in mapped memory: the kernel encodes them in place (zero-copy)
+        const core::HostJob job{c, core::kEncode, false, shards, nullptr, 1, len, 0, 1};
+        bool handled = false;
+        rc = core::run_mapped_job(job, &dev, 1, &handled);
+        if (handled || rc) return rc;
+    }
+    core::count_blocks(false, 1);
     core::DeviceScope scope(dev);
     if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
     const uint64_t pitch = core::round_up(len, 256);
@@ -226,6 +272,13 @@ int shmr_ec_reconstruct(shmr_ec_t* rs, uint8_t* const* shards, const size_t* sha
     const int dev = rs->device;
     int rc = core::check_device(dev);
     if (rc) return rc;
+    {   // shards in mapped memory: rebuilt in place by the kernel (zero-copy)
+        const core::HostJob job{c, core::kDecode, data_only != 0, shards, present, 1, len, 0, 1};
+        bool handled = false;
+        rc = core::run_mapped_job(job, &dev, 1, &handled);
+        if (handled || rc) return rc;
+    }
+    core::count_blocks(false, 1);
     core::DeviceScope scope(dev);
     if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
     const uint64_t pitch = core::round_up(len, 256);

@@ -42,13 +42,18 @@ Tuning g_tune[2];   // [kEncode], [kDecode]
 // (short-lived workgroups) issue their first data loads ahead of the plan
 // staging ("early": RS(4,2) 83 % vs 80 %; neutral at k = 8, -2 % on decode).
 // Scalar-loaded tables ("spre", 7-8 waves/SIMD) lose 3-6 % everywhere.
-kern::Variant variant_policy(OpClass op, unsigned k, unsigned rows) {
+//
+// Zero-copy launches over mapped host memory (the kernel's loads and stores
+// cross PCIe) are bound by the link, not HBM: there plain (temporal) loads
+// measured 72 GB/s of RS(8,3) encode traffic vs 64 with nontemporal loads
+// (tools/pcie_probe.py), and the shard-pointer tile has no early prologue.
+kern::Variant variant_policy(OpClass op, unsigned k, unsigned rows, bool host_mapped) {
     kern::Variant v;
     v.u = (op == kEncode && rows >= 4) ? 2 : 1;
     v.nt_store = true;
-    v.nt_load = true;
+    v.nt_load = !host_mapped;
     v.depth = 2;
-    v.early = op == kEncode && k < 8;
+    v.early = op == kEncode && k < 8 && !host_mapped;
     return v;
 }
 
@@ -137,9 +142,9 @@ int get_tuning(const char* key) {
     return SHMR_EC_INVALID_ARGUMENT;
 }
 
-kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows) {
+kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_mapped) {
     const Tuning& T = g_tune[op];
-    kern::Variant v = variant_policy(op, k, rows);
+    kern::Variant v = variant_policy(op, k, rows, host_mapped);
     if (T.u.load() != kAuto) v.u = T.u.load();
     if (T.nt_load.load() != kAuto) v.nt_load = T.nt_load.load() != 0;
     if (T.nt_store.load() != kAuto) v.nt_store = T.nt_store.load() != 0;
@@ -216,12 +221,19 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
     for (uint32_t t = 0; t < plan.k; ++t) identity = identity && plan.in_idx[t] == t;
     kern::Variant tail;   // tail / unaligned launches: U = 1, plain loads
     const int cap = grid_mode(op);
-    const bool aligned = aligned16(uintptr_t(L.in_base)) && aligned16(uintptr_t(L.out_base)) &&
-                         aligned16(L.in_bpitch) && aligned16(L.in_spitch) && aligned16(L.out_bpitch) &&
-                         aligned16(L.out_spitch);
+    const bool ptrs = L.d_ptrs != nullptr;
+    const bool aligned = ptrs ? L.ptrs_aligned
+                              : aligned16(uintptr_t(L.in_base)) && aligned16(uintptr_t(L.out_base)) &&
+                                    aligned16(L.in_bpitch) && aligned16(L.in_spitch) && aligned16(L.out_bpitch) &&
+                                    aligned16(L.out_spitch);
     for (uint32_t row0 = 0; row0 < plan.m; row0 += kern::kMaxRowsPerLaunch) {
         const uint32_t rows = std::min<uint32_t>(kern::kMaxRowsPerLaunch, plan.m - row0);
-        const kern::Variant var = resolve_variant(op, plan.k, rows);
+        kern::Variant var = resolve_variant(op, plan.k, rows, L.host_mapped);
+        if (ptrs) {   // only the plain LDS-staged tile reads a shard-pointer table
+            var.early = false;
+            var.spre = false;
+            var.scalar_tabs = false;
+        }
         const uint64_t tb = kern::tile_bytes(var.u, var.threads);
         kern::ApplyArgs a{};
         a.in_base = L.in_base;
@@ -244,6 +256,8 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
         a.plan = dplan;
         a.tab_off = tab_off;
         a.in_identity = bs.d_plans ? 0u : uint32_t(identity);
+        a.shard_ptrs = L.d_ptrs;
+        a.total = L.total;
         if (!aligned) {
             const uint64_t tb1 = kern::tile_bytes(1);
             a.col_base = 0;
@@ -291,6 +305,12 @@ int validate_presence(const Codec& c, const uint8_t* present, uint64_t nblocks) 
 int reconstruct_on_device(Codec& c, int dev, uint8_t* d_shards, uint64_t shard_pitch, uint64_t block_pitch,
                           const uint8_t* present, uint64_t nblocks, uint64_t len, bool data_only,
                           hipStream_t stream) {
+    const Layout L{d_shards, d_shards, block_pitch, shard_pitch, block_pitch, shard_pitch, 0};
+    return reconstruct_on_device(c, dev, L, present, nblocks, len, data_only, stream);
+}
+
+int reconstruct_on_device(Codec& c, int dev, const Layout& L, const uint8_t* present, uint64_t nblocks, uint64_t len,
+                          bool data_only, hipStream_t stream) {
     const unsigned k = c.k(), t = k + c.p();
     std::map<std::vector<uint8_t>, std::vector<uint64_t>> groups;   // pattern -> blocks
     for (uint64_t b = 0; b < nblocks; ++b) {
@@ -304,7 +324,6 @@ int reconstruct_on_device(Codec& c, int dev, uint8_t* d_shards, uint64_t shard_p
         groups[key].push_back(b);
     }
     if (groups.empty()) return SHMR_EC_OK;
-    const Layout L{d_shards, d_shards, block_pitch, shard_pitch, block_pitch, shard_pitch, 0};
     // Patterns with the same number of rebuilt shards share one multi-plan
     // launch set: the kernel picks each block's plan from a device table, so a
     // batch with many erasure patterns is still one launch (plus a tail).
@@ -383,11 +402,11 @@ int reconstruct_on_device(Codec& c, int dev, uint8_t* d_shards, uint64_t shard_p
 // ===========================================================================
 // Upload ring
 // ===========================================================================
-UploadRing* UploadRing::for_device(int dev, int* rc) {
+UploadRing* UploadRing::for_device(int dev, int* rc, Kind kind) {
     static std::mutex mu;
-    static auto* rings = new std::map<int, UploadRing*>;   // leaked: outlives static teardown
+    static auto* rings = new std::map<std::pair<int, int>, UploadRing*>;   // leaked: outlives static teardown
     std::lock_guard<std::mutex> lock(mu);
-    auto& r = (*rings)[dev];
+    auto& r = (*rings)[{dev, int(kind)}];
     if (!r) {
         auto* ring = new UploadRing;
         if (hipHostMalloc(reinterpret_cast<void**>(&ring->host_), kSlots * kSlotBytes, hipHostMallocDefault) !=

@@ -36,7 +36,7 @@ constexpr int kAuto = -2;
 
 int set_tuning(const char* key, int value);
 int get_tuning(const char* key);
-kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows);
+kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_mapped = false);
 int grid_mode(OpClass op);
 
 // ---- devices --------------------------------------------------------------
@@ -70,6 +70,14 @@ struct Layout {
     uint8_t* out_base;
     uint64_t in_bpitch, in_spitch, out_bpitch, out_spitch;
     uint32_t out_bias;   // subtracted from plan out_idx (encode into a parity-only buffer)
+    // Shard-pointer layout (bases/pitches unused): shard i of block b at
+    // d_ptrs[b * total + i], a device-visible table.  ptrs_aligned: every
+    // address the launch touches is 16-byte aligned.  host_mapped: the shards
+    // are mapped host memory (zero-copy; selects the PCIe variant policy).
+    const uint64_t* d_ptrs = nullptr;
+    uint32_t total = 0;
+    bool ptrs_aligned = false;
+    bool host_mapped = false;
 };
 
 // Blocks covered by one launch set: {first + j * stride} or, with d_list, the
@@ -96,6 +104,10 @@ int reconstruct_on_device(Codec& c, int dev, uint8_t* d_shards, uint64_t shard_p
                           const uint8_t* present, uint64_t nblocks, uint64_t len, bool data_only,
                           hipStream_t stream);
 
+// Same over any layout (e.g. a shard-pointer table).
+int reconstruct_on_device(Codec& c, int dev, const Layout& L, const uint8_t* present, uint64_t nblocks, uint64_t len,
+                          bool data_only, hipStream_t stream);
+
 // Validation shared by every reconstruct entry point.
 int validate_presence(const Codec& c, const uint8_t* present, uint64_t nblocks);
 
@@ -107,7 +119,11 @@ class UploadRing {
 public:
     static constexpr int kSlots = 32;
     static constexpr size_t kSlotBytes = 256 * 1024;
-    static UploadRing* for_device(int dev, int* rc);
+    // Ring kTables carries multi-plan tables, kPointers shard-pointer tables:
+    // a caller holding a kPointers slot may acquire a kTables slot, never the
+    // reverse, so concurrent callers cannot deadlock on slots.
+    enum Kind { kTables = 0, kPointers = 1 };
+    static UploadRing* for_device(int dev, int* rc, Kind kind = kTables);
     int acquire(uint8_t** host, uint8_t** dev, int* slot);
     int upload(int slot, size_t bytes, hipStream_t stream);
     int release_after(int slot, hipStream_t stream);

@@ -288,7 +288,8 @@ __device__ __forceinline__ void do_tile(const ApplyArgs& a, const Ctx& c, const 
 // Stages rows [row0, row0 + R) of a plan image into LDS:
 // [tables k*R*32 B][in_off k*8 B][out_off R*8 B].
 template <int R, int TH>
-__device__ __forceinline__ void stage_plan(const ApplyArgs& a, const uint8_t* plan, uint8_t* smem, Ctx& c) {
+__device__ __forceinline__ void stage_plan(const ApplyArgs& a, const uint8_t* plan, uint8_t* smem, Ctx& c,
+                                           uint64_t blk) {
     const uint32_t k = a.k;
     c.g_in_idx = reinterpret_cast<const uint16_t*>(plan + 8);
     c.g_out_idx = c.g_in_idx + k;
@@ -303,9 +304,15 @@ __device__ __forceinline__ void stage_plan(const ApplyArgs& a, const uint8_t* pl
         const uint32_t t = e / R, r = e - t * R;
         s_tab[i] = ptab[(size_t(t) * a.m + a.row0 + r) * 2 + half];
     }
-    for (uint32_t t = threadIdx.x; t < k; t += TH) s_in_off[t] = uint64_t(c.g_in_idx[t]) * a.in_spitch;
-    for (uint32_t r = threadIdx.x; r < uint32_t(R); r += TH)
-        s_out_off[r] = uint64_t(c.g_out_idx[a.row0 + r] - a.out_bias) * a.out_spitch;
+    if (a.shard_ptrs) {   // absolute shard addresses (in/out bases are 0)
+        const uint64_t* bp = a.shard_ptrs + blk * a.total;
+        for (uint32_t t = threadIdx.x; t < k; t += TH) s_in_off[t] = bp[c.g_in_idx[t]];
+        for (uint32_t r = threadIdx.x; r < uint32_t(R); r += TH) s_out_off[r] = bp[c.g_out_idx[a.row0 + r]];
+    } else {
+        for (uint32_t t = threadIdx.x; t < k; t += TH) s_in_off[t] = uint64_t(c.g_in_idx[t]) * a.in_spitch;
+        for (uint32_t r = threadIdx.x; r < uint32_t(R); r += TH)
+            s_out_off[r] = uint64_t(c.g_out_idx[a.row0 + r] - a.out_bias) * a.out_spitch;
+    }
     c.s_tab = s_tab;
     c.s_in_off = s_in_off;
     c.s_out_off = s_out_off;
@@ -561,10 +568,12 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
         }
         return;
     }
+    // Shard-pointer launches restage per tile (the offsets depend on the block).
+    const bool restage = multi || a.shard_ptrs != nullptr;
     Ctx c{};
-    if (!multi) {
+    if (!restage) {
         if constexpr (kLds) {
-            stage_plan<R, TH>(a, a.plan, smem, c);
+            stage_plan<R, TH>(a, a.plan, smem, c, 0);
             __syncthreads();
         } else {
             c.g_in_idx = reinterpret_cast<const uint16_t*>(a.plan + 8);
@@ -578,11 +587,11 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
         const uint64_t j = tile / tpb;
         const uint64_t cc = tile - j * tpb;
         const uint64_t blk = a.blk_list ? uint64_t(a.blk_list[j]) : a.blk_first + j * a.blk_stride;
-        if (multi) {
-            const uint8_t* plan = a.plan_table[a.blk_plan[j]];
+        if (restage) {
+            const uint8_t* plan = multi ? a.plan_table[a.blk_plan[j]] : a.plan;
             if constexpr (kLds) {
                 __syncthreads();   // previous tile's LDS reads are done
-                stage_plan<R, TH>(a, plan, smem, c);
+                stage_plan<R, TH>(a, plan, smem, c, blk);
                 __syncthreads();
             } else {
                 c.g_in_idx = reinterpret_cast<const uint16_t*>(plan + 8);

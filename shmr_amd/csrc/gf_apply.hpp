@@ -40,6 +40,13 @@ struct ApplyArgs {
     const uint16_t* blk_plan;
     uint32_t tab_off;        // byte offset of the PermTab array in the image
     uint32_t in_identity;    // every plan of the launch reads input t from shard t (in_idx[t] == t)
+    // Shard-pointer launches (shard_ptrs != nullptr; in/out bases and pitches
+    // are then 0): shard i of block b is at address shard_ptrs[b * total + i]
+    // -- e.g. Block-Cache buffers in mapped (pinned) host memory, which the
+    // kernel reads and writes across PCIe without a staging copy.  Only the
+    // plain LDS-staged tile supports it (no early / spre / scalar_tabs).
+    const uint64_t* shard_ptrs;
+    uint32_t total;
 };
 
 // Compiled-in kernel variant for full tiles (see gf_apply.hip dispatch_full).

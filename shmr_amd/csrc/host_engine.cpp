@@ -5,8 +5,12 @@
 // through NS staging sets so the H2D copy of chunk c+1, the kernel of chunk c
 // and the D2H copy of chunk c-1 overlap on separate streams.
 //
-// Host buffers in pinned memory (shmr_ec_host_alloc, the MI355X-native Block
-// Cache) are DMA'd directly; pageable buffers (plain Vec<u8>/malloc) are first
+// Host buffers in mapped memory (shmr_ec_host_alloc -- the MI355X-native Block
+// Cache -- or ranges given to shmr_ec_host_register) skip all of that: the
+// kernels read the data shards and write the rebuilt/parity shards in place
+// across PCIe through a device table of shard pointers (zero-copy; measured
+// 1.5x the staged DMA pipeline, tools/pcie_probe.py).  Other pinned buffers
+// are DMA'd directly; pageable buffers (plain Vec<u8>/malloc) are first
 // gathered into a pinned mirror by a crew of copy threads.
 #include <algorithm>
 #include <atomic>
@@ -183,7 +187,199 @@ int copy_runs(uint8_t* const* host, const std::vector<unsigned>& idx, uint8_t* d
     return SHMR_EC_OK;
 }
 
+struct MappedRange {
+    size_t bytes;
+    uintptr_t dev;
+};
+std::mutex g_mapped_mu;
+std::map<uintptr_t, MappedRange>& mapped_ranges() {
+    static auto* m = new std::map<uintptr_t, MappedRange>;   // leaked: outlives static teardown
+    return *m;
+}
+
+// Input / output shard indices of block b of a job (the first k present
+// shards in index order are the inputs, as the crate's reconstruct picks them).
+void job_io(const HostJob& job, size_t b, std::vector<unsigned>& in, std::vector<unsigned>& out) {
+    const unsigned k = job.codec.k(), t = k + job.codec.p();
+    in.clear();
+    out.clear();
+    if (job.op == kEncode) {
+        for (unsigned i = 0; i < k; ++i) in.push_back(i);
+        for (unsigned i = k; i < t; ++i) out.push_back(i);
+        return;
+    }
+    const uint8_t* pr = job.present + b * t;
+    unsigned np = 0;
+    for (unsigned i = 0; i < t; ++i) np += pr[i] ? 1 : 0;
+    if (np == t) return;   // nothing to rebuild
+    for (unsigned i = 0; i < t; ++i) {
+        if (pr[i]) {
+            if (in.size() < k) in.push_back(i);
+        } else if (i < k || !job.data_only) {
+            out.push_back(i);
+        }
+    }
+}
+
+// Translation under g_mapped_mu (held by the caller); `hint` caches the
+// range of the previous hit (a batch's shards usually share one allocation).
+bool translate_locked(const void* p, size_t len, uint64_t* dev, std::map<uintptr_t, MappedRange>::const_iterator* hint) {
+    const auto& m = mapped_ranges();
+    const uintptr_t a = uintptr_t(p);
+    auto inside = [&](std::map<uintptr_t, MappedRange>::const_iterator it) {
+        return a >= it->first && a - it->first <= it->second.bytes && len <= it->second.bytes - (a - it->first);
+    };
+    if (!p) return false;
+    if (*hint == m.end() || !inside(*hint)) {
+        auto it = m.upper_bound(a);
+        if (it == m.begin()) return false;
+        --it;
+        if (!inside(it)) return false;
+        *hint = it;
+    }
+    *dev = uint64_t((*hint)->second.dev + (a - (*hint)->first));
+    return true;
+}
+
+// Device addresses of every shard the job touches (0 for untouched ones);
+// false if any touched shard is not in mapped host memory.
+bool map_job(const HostJob& job, std::vector<uint64_t>* dptrs, bool* aligned) {
+    const unsigned t = job.codec.k() + job.codec.p();
+    dptrs->assign(job.nblocks * t, 0);
+    *aligned = true;
+    std::vector<unsigned> in, out;
+    std::lock_guard<std::mutex> lock(g_mapped_mu);
+    if (mapped_ranges().empty()) return false;
+    auto hint = mapped_ranges().cend();
+    for (size_t b = 0; b < job.nblocks; ++b) {
+        job_io(job, b, in, out);
+        for (const auto* v : {&in, &out})
+            for (unsigned i : *v) {
+                uint64_t d = 0;
+                if (!translate_locked(job.host_shards[b * t + i], job.len, &d, &hint)) return false;
+                (*dptrs)[b * t + i] = d;
+                *aligned = *aligned && (d & 15u) == 0;
+            }
+    }
+    return true;
+}
+
+// Zero-copy: per device, the blocks' shard-pointer tables go up through the
+// device's pointer ring and the kernels run on the host buffers in place.
+int run_mapped(const HostJob& job, const std::vector<uint64_t>& dptrs, bool aligned, const int* devices, int ndev) {
+    Codec& c = job.codec;
+    const unsigned t = c.k() + c.p();
+    std::vector<int> results(size_t(ndev), SHMR_EC_OK);
+    auto worker = [&](int di) {
+        int& result = results[size_t(di)];
+        const int dev = devices[di];
+        DeviceScope scope(dev);
+        if (!scope.ok()) {
+            result = SHMR_EC_DEVICE_ERROR;
+            return;
+        }
+        std::vector<size_t> mine;
+        for (size_t b = size_t(di); b < job.nblocks; b += size_t(ndev)) mine.push_back(b);
+        if (mine.empty()) return;
+        int rc = SHMR_EC_OK;
+        StagingLease lease;   // a pooled stream (no device buffer)
+        lease.s = StagingPool::get().acquire(dev, 0, &rc);
+        if (!lease.s) {
+            result = rc;
+            return;
+        }
+        const hipStream_t stream = lease.s->stream;
+        UploadRing* ring = UploadRing::for_device(dev, &rc, UploadRing::kPointers);
+        if (!ring) {
+            result = rc;
+            return;
+        }
+        const size_t per_chunk = UploadRing::kSlotBytes / (sizeof(uint64_t) * t);
+        std::vector<uint8_t> present;
+        for (size_t c0 = 0; c0 < mine.size() && rc == SHMR_EC_OK; c0 += per_chunk) {
+            const size_t n = std::min(per_chunk, mine.size() - c0);
+            uint8_t *hslot = nullptr, *dslot = nullptr;
+            int slot = -1;
+            rc = ring->acquire(&hslot, &dslot, &slot);
+            if (rc) break;
+            uint64_t* tab = reinterpret_cast<uint64_t*>(hslot);
+            for (size_t j = 0; j < n; ++j)
+                std::memcpy(tab + j * t, dptrs.data() + mine[c0 + j] * t, t * sizeof(uint64_t));
+            rc = ring->upload(slot, n * t * sizeof(uint64_t), stream);
+            Layout L{nullptr, nullptr, 0, 0, 0, 0, 0};
+            L.d_ptrs = reinterpret_cast<const uint64_t*>(dslot);
+            L.total = t;
+            L.ptrs_aligned = aligned;
+            L.host_mapped = true;
+            if (rc == SHMR_EC_OK) {
+                if (job.op == kEncode) {
+                    rc = encode_on_device(c, dev, L, n, job.len, stream);
+                } else {
+                    present.resize(n * t);
+                    for (size_t j = 0; j < n; ++j)
+                        std::memcpy(present.data() + j * t, job.present + mine[c0 + j] * t, t);
+                    rc = reconstruct_on_device(c, dev, L, present.data(), n, job.len, job.data_only, stream);
+                }
+            }
+            const int rc2 = ring->release_after(slot, stream);
+            if (rc == SHMR_EC_OK) rc = rc2;
+        }
+        if (hipStreamSynchronize(stream) != hipSuccess && rc == SHMR_EC_OK) rc = SHMR_EC_DEVICE_ERROR;
+        result = rc;
+    };
+    std::vector<std::thread> th;
+    for (int d = 1; d < ndev; ++d) th.emplace_back(worker, d);
+    worker(0);
+    for (auto& x : th) x.join();
+    for (int r : results)
+        if (r) return r;
+    return SHMR_EC_OK;
+}
+
 }  // namespace
+
+namespace {
+std::atomic<uint64_t> g_zero_copy_blocks{0}, g_staged_blocks{0};
+}
+
+void count_blocks(bool zero_copy, uint64_t nblocks) {
+    (zero_copy ? g_zero_copy_blocks : g_staged_blocks).fetch_add(nblocks, std::memory_order_relaxed);
+}
+
+void path_stats(uint64_t* zero_copy_blocks, uint64_t* staged_blocks) {
+    if (zero_copy_blocks) *zero_copy_blocks = g_zero_copy_blocks.load();
+    if (staged_blocks) *staged_blocks = g_staged_blocks.load();
+}
+
+void mapped_add(const void* host, size_t bytes, const void* dev) {
+    std::lock_guard<std::mutex> lock(g_mapped_mu);
+    mapped_ranges()[uintptr_t(host)] = MappedRange{bytes, uintptr_t(dev)};
+}
+
+bool mapped_remove(const void* host) {
+    std::lock_guard<std::mutex> lock(g_mapped_mu);
+    return mapped_ranges().erase(uintptr_t(host)) != 0;
+}
+
+bool mapped_translate(const void* p, size_t len, uint64_t* dev) {
+    std::lock_guard<std::mutex> lock(g_mapped_mu);
+    auto hint = mapped_ranges().cend();
+    return translate_locked(p, len, dev, &hint);
+}
+
+int run_mapped_job(const HostJob& job, const int* devices, int ndev, bool* handled) {
+    *handled = false;
+    if (job.op == kDecode) {
+        const int rc = validate_presence(job.codec, job.present, job.nblocks);
+        if (rc) return rc;
+    }
+    std::vector<uint64_t> dptrs;
+    bool aligned = true;
+    if (!map_job(job, &dptrs, &aligned)) return SHMR_EC_OK;
+    *handled = true;
+    count_blocks(true, job.nblocks);
+    return run_mapped(job, dptrs, aligned, devices, ndev);
+}
 
 int copy_threads_default() {
     const unsigned hw = std::thread::hardware_concurrency();
@@ -200,6 +396,12 @@ int run_host_job(const HostJob& job, const int* devices, int ndev) {
         int rc = validate_presence(c, job.present, job.nblocks);
         if (rc) return rc;
     }
+    {
+        bool handled = false;
+        const int rc = run_mapped_job(job, devices, ndev, &handled);
+        if (handled || rc) return rc;
+    }
+    count_blocks(false, job.nblocks);
     const bool pinned = is_pinned(job.host_shards[0]);
     std::vector<int> results(size_t(ndev), SHMR_EC_OK);
 
@@ -237,26 +439,7 @@ int run_host_job(const HostJob& job, const int* devices, int ndev) {
         std::vector<uint8_t> present;
 
         // input / output shard indices of one block
-        auto io = [&](size_t b, std::vector<unsigned>& in, std::vector<unsigned>& out) {
-            in.clear();
-            out.clear();
-            if (job.op == kEncode) {
-                for (unsigned i = 0; i < k; ++i) in.push_back(i);
-                for (unsigned i = k; i < t; ++i) out.push_back(i);
-                return;
-            }
-            const uint8_t* pr = job.present + b * t;
-            unsigned np = 0;
-            for (unsigned i = 0; i < t; ++i) np += pr[i] ? 1 : 0;
-            if (np == t) return;   // nothing to rebuild
-            for (unsigned i = 0; i < t; ++i) {
-                if (pr[i]) {
-                    if (in.size() < k) in.push_back(i);
-                } else if (i < k || !job.data_only) {
-                    out.push_back(i);
-                }
-            }
-        };
+        auto io = [&](size_t b, std::vector<unsigned>& in, std::vector<unsigned>& out) { job_io(job, b, in, out); };
         std::vector<unsigned> in, out;
         // staged mode: pinned mirror -> user output buffers of a finished chunk
         auto drain = [&](StageSet& s) -> int {

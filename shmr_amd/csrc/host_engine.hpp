@@ -23,8 +23,26 @@ struct HostJob {
 
 int copy_threads_default();
 
-// Synchronous.  Validates every block before any device work.
+// Synchronous.  Validates every block before any device work.  When every
+// shard the job touches lies in mapped host memory (below), the kernels read
+// and write the host buffers directly across PCIe (zero-copy, no staging);
+// otherwise blocks are staged through device memory in pipelined chunks.
 int run_host_job(const HostJob& job, const int* devices, int ndev);
+
+// Zero-copy only: *handled = false (and nothing runs) unless every shard the
+// job touches is mapped.  Used by the single-block entry points.
+int run_mapped_job(const HostJob& job, const int* devices, int ndev, bool* handled);
+
+// Registry of mapped (page-locked, device-visible) host memory: allocations of
+// shmr_ec_host_alloc and ranges given to shmr_ec_host_register.
+void mapped_add(const void* host, size_t bytes, const void* dev);
+bool mapped_remove(const void* host);
+// Device address of [p, p + len) if the whole range lies in one mapped range.
+bool mapped_translate(const void* p, size_t len, uint64_t* dev);
+
+// Blocks served by each host-buffer path since load (introspection/tests).
+void count_blocks(bool zero_copy, uint64_t nblocks);
+void path_stats(uint64_t* zero_copy_blocks, uint64_t* staged_blocks);
 
 }  // namespace core
 }  // namespace shmr

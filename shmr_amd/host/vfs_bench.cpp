@@ -141,6 +141,8 @@ int main(int argc, char** argv) {
         o.fsync_shards = do_fsync;
         Result best;
         best.sync_s = best.read_s = best.write_s = best.per_block_sync_s = 1e30;
+        uint64_t zc0 = 0, st0 = 0, zc1 = 0, st1 = 0;
+        shmr_ec_path_stats(&zc0, &st0);
         for (int rep = 0; rep < reps + 1; ++rep) {   // rep 0 warms plans, staging, clocks
             Result r = run_once(cfg, 1000 + rep, src, block_bytes, o, bm == VirtualFile::kAutoBatch ? bm : bm << 20);
             if (rep == 0) continue;
@@ -155,14 +157,16 @@ int main(int argc, char** argv) {
             best.write_s = std::min(best.write_s, r.write_s);
             best.per_block_sync_s = std::min(best.per_block_sync_s, r.per_block_sync_s);
         }
+        shmr_ec_path_stats(&zc1, &st1);
         std::printf(
-            "{\"buffers\": \"%s\", \"batch\": \"%s\", \"file_MiB\": %llu, \"block_MiB\": %llu, \"topology\": \"Erasure(1, 8, 3)\", "
+            "{\"buffers\": \"%s\", \"codec_blocks_zero_copy\": %llu, \"codec_blocks_staged\": %llu, \"batch\": \"%s\", \"file_MiB\": %llu, \"block_MiB\": %llu, \"topology\": \"Erasure(1, 8, 3)\", "
             "\"fsync\": %d, \"reps\": %d, \"unit\": \"GiB/s of file data (best rep)\", "
             "\"write_GiBps\": %.2f, \"sync_GiBps\": %.2f, \"sync_encode_GiBps\": %.2f, \"sync_shard_io_GiBps\": %.2f, "
             "\"sync_pipeline_GiBps\": %.2f, \"per_block_sync_GiBps\": %.2f, \"read_with_erasure_GiBps\": %.2f, "
             "\"read_reconstruct_GiBps\": %.2f, \"read_shard_io_GiBps\": %.2f, \"read_pipeline_GiBps\": %.2f, "
             "\"reconstructed_blocks\": %zu, \"verified\": true}\n",
-            pinned ? "pinned" : "pageable", bm == VirtualFile::kAutoBatch ? "auto" : "one batch",
+            pinned ? "mapped Block Cache (shmr_ec_host_alloc)" : "pageable", (unsigned long long)(zc1 - zc0),
+            (unsigned long long)(st1 - st0), bm == VirtualFile::kAutoBatch ? "auto" : "one batch",
             (unsigned long long)file_mib, (unsigned long long)block_mib, int(do_fsync),
             reps, bytes / best.write_s / GiB, bytes / best.sync_s / GiB, bytes / best.sync.codec_s / GiB,
             bytes / best.sync.io_s / GiB, bytes / best.sync.total_s / GiB, bytes / best.per_block_sync_s / GiB,

@@ -20,7 +20,7 @@ import numpy as np
 from ._native import _u8p, lib
 
 __all__ = ["Error", "ReedSolomon", "calculate_shard_size", "device_count", "set_tuning", "get_tuning", "describe_variant",
-           "PinnedBuffer"]
+           "PinnedBuffer", "host_register", "host_unregister", "path_stats"]
 
 
 class Error(Exception):
@@ -256,3 +256,21 @@ class PinnedBuffer:
             self.array = None
             lib().shmr_ec_host_free(p)
             self._p = None
+
+
+def host_register(arr: np.ndarray) -> None:
+    """Page-lock and map an existing C-contiguous host array for zero-copy
+    use by the host-buffer entry points (shmr_ec_host_register)."""
+    a = _writable_u8(arr.reshape(-1).view(np.uint8))
+    _check(lib().shmr_ec_host_register(ctypes.c_void_p(a.ctypes.data), a.nbytes))
+
+
+def host_unregister(arr: np.ndarray) -> None:
+    _check(lib().shmr_ec_host_unregister(ctypes.c_void_p(arr.ctypes.data)))
+
+
+def path_stats():
+    """(zero_copy_blocks, staged_blocks) served by the host-buffer entry points."""
+    z, st = ctypes.c_uint64(), ctypes.c_uint64()
+    _check(lib().shmr_ec_path_stats(ctypes.byref(z), ctypes.byref(st)))
+    return int(z.value), int(st.value)

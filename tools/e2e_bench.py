@@ -6,11 +6,17 @@ Cache, shard files on disk).  These numbers include H2D and D2H copies and are
 reported in DESIGN.md; they are never bench.py's headline ``value``.
 
 Measured (GiB/s of file data, RS(8,3), 4 MiB StorageBlocks):
-  * host_batch_encode_{pageable,pinned}  shmr_ec_encode_blocks_host over B blocks
+  * host_batch_encode_{pageable,pinned_dma,mapped}  shmr_ec_encode_blocks_host
+      over B blocks: pageable numpy (staged through a pinned mirror by copy
+      threads), torch-pinned (DMA pipeline), mapped Block-Cache buffers from
+      shmr_ec_host_alloc (zero-copy: the kernel reads/writes them over PCIe)
   * host_batch_reconstruct_{...}          1 missing data shard per block
-  * per_block_encode_threads              the literal drop-in call
+  * per_block_encode_threads{,_mapped}    the literal drop-in call
       (shmr_ec_encode per block) from a thread pool, as rayon calls
       ReedSolomon::encode per block (src/vfs/mod.rs:93-96)
+The batch entry points are timed through the C ABI with the shard-pointer
+arrays marshalled once (the Python shim's per-call conversion of B*(k+p) numpy
+views is not the library's cost).
   * virtual_file_roundtrip                 write -> sync_data (encode) -> erase a
       shard per block -> read (reconstruct) over a 256 MiB file, verified
 """
@@ -45,13 +51,17 @@ def timeit(fn, reps):
     return (time.perf_counter() - t0) / reps
 
 
-def make_blocks(B, pinned, rng):
+def make_blocks(B, kind, rng):
     blocks, keep = [], []
     for _ in range(B):
-        if pinned:
+        if kind == "mapped":
             buf = shmr_amd.PinnedBuffer((K + P) * S)
             keep.append(buf)
             a = buf.array
+        elif kind == "pinned_dma":
+            t = torch.empty((K + P) * S, dtype=torch.uint8).pin_memory()
+            keep.append(t)
+            a = t.numpy()
         else:
             a = np.empty((K + P) * S, np.uint8)
         a[:K * S] = rng.integers(0, 256, K * S, dtype=np.uint8)
@@ -72,28 +82,42 @@ def main():
     res = {"k": K, "p": P, "block_bytes": BLOCK, "shard_bytes": S, "blocks": a.blocks, "unit": "GiB/s of data"}
     data_bytes = a.blocks * K * S
 
-    for pinned in (False, True):
-        tag = "pinned" if pinned else "pageable"
-        blocks, keep = make_blocks(a.blocks, pinned, rng)
-        dt = timeit(lambda: rs.encode_blocks_host(blocks), a.reps)
+    import ctypes
+    from shmr_amd._native import _u8p, lib
+    cdev = (ctypes.c_int * 1)(0)
+    for tag in ("pageable", "pinned_dma", "mapped"):
+        blocks, keep = make_blocks(a.blocks, tag, rng)
+        _, _, cp = rs._host_ptrs(blocks)
+        z0, s0 = shmr_amd.path_stats()
+        dt = timeit(lambda: lib().shmr_ec_encode_blocks_host(rs._h, cp, a.blocks, S, cdev, 1), a.reps)
+        z1, s1 = shmr_amd.path_stats()
         res[f"host_batch_encode_{tag}"] = round(data_bytes / dt / GiB, 2)
+        res[f"host_batch_{tag}_path"] = "zero_copy" if z1 > z0 and s1 == s0 else "staged"
+        want = [[x.copy() for x in blk[K:]] for blk in blocks[:4]]
         # one missing data shard per block (config 3 pattern), in place
         present = np.ones((a.blocks, K + P), np.uint8)
         present[np.arange(a.blocks), np.arange(a.blocks) % K] = 0
         ref = [blk[b % K].copy() for b, blk in enumerate(blocks)]
-        dt = timeit(lambda: rs.reconstruct_blocks_host(blocks, present), a.reps)
+        for b, blk in enumerate(blocks):
+            blk[b % K][:] = 0
+        cpres = present.ctypes.data_as(_u8p)
+        dt = timeit(lambda: lib().shmr_ec_reconstruct_blocks_host(rs._h, cp, cpres, a.blocks, S, 0, cdev, 1), a.reps)
         res[f"host_batch_reconstruct_{tag}"] = round(data_bytes / dt / GiB, 2)
         assert all(np.array_equal(blk[b % K], ref[b]) for b, blk in enumerate(blocks))
+        assert all(np.array_equal(x, y) for blk, w in zip(blocks[:4], want) for x, y in zip(blk[K:], w))
         del blocks, keep
 
     # the literal drop-in: one shmr_ec_encode per block from a thread pool
-    blocks, _ = make_blocks(64, False, rng)
     pool = ThreadPoolExecutor(a.threads)
-    dt = timeit(lambda: list(pool.map(lambda blk: rs.encode(blk), blocks)), a.reps)
-    res["per_block_encode_threads"] = round(64 * K * S / dt / GiB, 2)
+    for tag in ("pageable", "mapped"):
+        blocks, keep = make_blocks(64, tag, rng)
+        sfx = "" if tag == "pageable" else "_mapped"
+        dt = timeit(lambda: list(pool.map(lambda blk: rs.encode(blk), blocks)), a.reps)
+        res[f"per_block_encode_threads{sfx}"] = round(64 * K * S / dt / GiB, 2)
+        t1 = timeit(lambda: rs.encode(blocks[0]), a.reps * 4)
+        res[f"per_block_encode_latency_ms{sfx}"] = round(t1 * 1e3, 3)
+        del blocks, keep
     res["per_block_encode_threads_n"] = a.threads
-    t1 = timeit(lambda: rs.encode(blocks[0]), a.reps * 4)
-    res["per_block_encode_latency_ms"] = round(t1 * 1e3, 3)
 
     # VirtualFile round trip: 256 MiB file, write -> sync -> erase -> read
     nblk = 64
