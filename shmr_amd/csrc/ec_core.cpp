@@ -29,6 +29,7 @@ struct Tuning {
     std::atomic<int> occ{kAuto};
     std::atomic<int> early{kAuto};
     std::atomic<int> spre{kAuto};
+    std::atomic<int> xcd{kAuto};
 };
 Tuning g_tune[2];   // [kEncode], [kDecode]
 
@@ -42,6 +43,12 @@ Tuning g_tune[2];   // [kEncode], [kDecode]
 // (short-lived workgroups) issue their first data loads ahead of the plan
 // staging ("early": RS(4,2) 83 % vs 80 %; neutral at k = 8, -2 % on decode).
 // Scalar-loaded tables ("spre", 7-8 waves/SIMD) lose 3-6 % everywhere.
+// XCD-grouped tile order ("xcd") is within +-2 % (RS(8,3) +0.5 %, RS(4,2)
+// -2 %): off.  Also measured and dropped: running the partial last tile of
+// RS(10,4) shards inside the full-tile launch (+5 % time: the extra path costs
+// 4-7 VGPRs) or concurrently on a side stream (+3 %), and uploading multi-plan
+// tables on a side stream (neutral) -- the plain tail launch after the full
+// tiles stays.
 //
 // Zero-copy launches over mapped host memory (the kernel's loads and stores
 // cross PCIe) are bound by the link, not HBM: there plain (temporal) loads
@@ -114,6 +121,8 @@ int set_tuning(const char* key, int value) {
             T.early = value == kAuto ? kAuto : (value != 0);
         } else if (k == "spre") {
             T.spre = value == kAuto ? kAuto : (value != 0);
+        } else if (k == "xcd") {
+            T.xcd = value == kAuto ? kAuto : (value != 0);
         } else {
             return SHMR_EC_INVALID_ARGUMENT;
         }
@@ -139,6 +148,7 @@ int get_tuning(const char* key) {
     if (k == "occ") return T.occ;
     if (k == "early") return T.early;
     if (k == "spre") return T.spre;
+    if (k == "xcd") return T.xcd;
     return SHMR_EC_INVALID_ARGUMENT;
 }
 
@@ -157,6 +167,7 @@ kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_m
     if (T.occ.load() != kAuto) v.occ = T.occ.load();
     if (T.early.load() != kAuto) v.early = T.early.load() != 0;
     if (T.spre.load() != kAuto) v.spre = T.spre.load() != 0;
+    if (T.xcd.load() != kAuto) v.xcd = T.xcd.load() != 0;
     return v;
 }
 

@@ -531,6 +531,12 @@ __device__ __forceinline__ void spre_tile(const ApplyArgs& a, const uint8_t* pla
     }
 }
 
+__device__ __forceinline__ uint64_t first_tile(const ApplyArgs& a) {
+    const uint64_t w = blockIdx.x;
+    if (a.xcd_q != 0 && w < 8 * a.xcd_q) return (w & 7) * a.xcd_q + (w >> 3);
+    return w;
+}
+
 // The second __launch_bounds__ argument is amdgpu_waves_per_eu (minimum).
 template <int R, int U, int MODE, int F>
 __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) void gf_apply_kernel(const ApplyArgs a) {
@@ -543,7 +549,8 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
     if constexpr ((F & (kEarly | kSPre)) != 0) {
         const uint32_t tpb = a.tiles_per_block;
         const uint64_t tb = uint64_t(TH) * 16 * U;
-        for (uint64_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+        bool first = true;
+        for (uint64_t tile = first_tile(a); tile < a.ntiles; tile += gridDim.x) {
             const uint64_t j = tile / tpb;
             const uint64_t cc = tile - j * tpb;
             const uint64_t blk = a.blk_list ? uint64_t(as_const<cu32>(a.blk_list)[j]) : a.blk_first + j * a.blk_stride;
@@ -563,8 +570,9 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
                                                     a.out_base + blk * a.out_bpitch, a.col_base + cc * tb);
             }
             else
-                early_tile<R, U, MODE, F>(a, plan, smem, tile == blockIdx.x, a.in_base + blk * a.in_bpitch,
+                early_tile<R, U, MODE, F>(a, plan, smem, first, a.in_base + blk * a.in_bpitch,
                                           a.out_base + blk * a.out_bpitch, a.col_base + cc * tb);
+            first = false;
         }
         return;
     }
@@ -583,7 +591,7 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
     }
     const uint32_t tpb = a.tiles_per_block;
     const uint64_t tb = uint64_t(TH) * 16 * U;
-    for (uint64_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    for (uint64_t tile = first_tile(a); tile < a.ntiles; tile += gridDim.x) {
         const uint64_t j = tile / tpb;
         const uint64_t cc = tile - j * tpb;
         const uint64_t blk = a.blk_list ? uint64_t(a.blk_list[j]) : a.blk_first + j * a.blk_stride;
@@ -643,7 +651,9 @@ hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStr
     }
     if (grid > a.ntiles) grid = a.ntiles;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL(kern, dim3(uint32_t(grid)), dim3(threads_of<F>()), lds, stream, a);
+    ApplyArgs la = a;
+    la.xcd_q = (v.xcd && grid == a.ntiles) ? a.ntiles / 8 : 0;
+    hipLaunchKernelGGL(kern, dim3(uint32_t(grid)), dim3(threads_of<F>()), lds, stream, la);
     return hipGetLastError();
 }
 

@@ -47,6 +47,12 @@ struct ApplyArgs {
     // plain LDS-staged tile supports it (no early / spre / scalar_tabs).
     const uint64_t* shard_ptrs;
     uint32_t total;
+    // XCD-grouped tile order (one-workgroup-per-tile launches only): the
+    // dispatcher deals workgroup IDs round-robin over the 8 XCDs, so with
+    // xcd_q = ntiles / 8 > 0 workgroup w takes tile (w % 8) * xcd_q + w / 8 and
+    // every XCD streams one contiguous eighth of the batch (tiles >= 8 * xcd_q
+    // keep their own index).  0 = tile w.
+    uint64_t xcd_q;
 };
 
 // Compiled-in kernel variant for full tiles (see gf_apply.hip dispatch_full).
@@ -63,6 +69,7 @@ struct Variant {
     int occ = 0;             // > 0: register budget for this many waves per SIMD (6, 7)
     bool early = false;      // first data loads before the plan's LDS staging completes
     bool spre = false;       // tables/offsets by scalar loads one shard ahead (no LDS)
+    bool xcd = false;        // XCD-grouped tile order (ApplyArgs::xcd_q)
 };
 
 // rows in [1, kMaxRowsPerLaunch].  mode 0: full tiles, every shard base

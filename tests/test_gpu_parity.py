@@ -129,7 +129,8 @@ def test_reconstruct_all_patterns_10_4(gpu):
 
 
 # --------------------------------------------------------------- device batch API
-KNOBS = ("chunks", "nt_load", "nt_store", "scalar_tabs", "occ8", "grid", "threads", "depth", "wgs_per_cu", "occ", "early", "spre")
+KNOBS = ("chunks", "nt_load", "nt_store", "scalar_tabs", "occ8", "grid", "threads", "depth", "wgs_per_cu", "occ", "early", "spre",
+         "xcd")
 
 
 def _dev_encode_check(gpu, k, p, L, B, pitch=None, **knobs):
@@ -160,7 +161,8 @@ def test_encode_batch_dev(gpu, k, p, L, B):
     _dev_encode_check(gpu, k, p, L, B, pitch=(L + 255) // 256 * 256)
 
 
-BASE = dict(chunks=1, nt_load=0, nt_store=0, scalar_tabs=0, occ8=0, grid=-1, threads=256, depth=3, wgs_per_cu=0, occ=0, early=0, spre=0)
+BASE = dict(chunks=1, nt_load=0, nt_store=0, scalar_tabs=0, occ8=0, grid=-1, threads=256, depth=3, wgs_per_cu=0, occ=0, early=0, spre=0,
+            xcd=0)
 VARIANTS = [dict(BASE, **v) for v in (
     {}, dict(nt_load=1), dict(nt_store=1), dict(nt_load=1, nt_store=1),
     dict(scalar_tabs=1, nt_load=1, nt_store=1), dict(occ8=1, nt_load=1, nt_store=1),
@@ -175,7 +177,9 @@ VARIANTS = [dict(BASE, **v) for v in (
     dict(chunks=2, nt_load=1, nt_store=1, depth=2, early=1), dict(nt_load=1, nt_store=1, early=1),
     dict(nt_load=1, nt_store=1, depth=2, early=1, grid=0), dict(nt_load=1, nt_store=1, depth=2, spre=1),
     dict(chunks=2, nt_load=1, nt_store=1, depth=2, spre=1), dict(nt_load=1, nt_store=1, spre=1),
-    dict(nt_load=1, nt_store=1, depth=2, spre=1, grid=0))]
+    dict(nt_load=1, nt_store=1, depth=2, spre=1, grid=0), dict(nt_load=1, nt_store=1, depth=2, xcd=1),
+    dict(nt_load=1, nt_store=1, depth=2, early=1, xcd=1), dict(chunks=2, nt_load=1, nt_store=1, depth=2, xcd=1),
+    dict(nt_load=1, nt_store=1, depth=2, xcd=1, grid=0), dict(chunks=4, nt_load=1, nt_store=1, grid=7))]
 
 
 @pytest.mark.parametrize("knobs", VARIANTS, ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items() if BASE[k] != v) or "base")
