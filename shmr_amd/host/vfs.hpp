@@ -7,7 +7,8 @@
 // in the reference's buffer, so sync encodes and writes the shard files
 // straight from it (no chunks().to_vec() copies), and load reads every shard
 // file into its slot and reconstructs in place.  With VfsOptions::pinned_buffers
-// the allocation is pinned host memory, which the GPU DMAs without staging.
+// the allocation is mapped host memory (shmr_ec_host_alloc) that the GPU kernels
+// read and write in place across PCIe (zero-copy, no staging).
 // VirtualFile::sync_data / read batch every Erasure block of the operation into
 // one pipelined multi-GPU call (shmr_ec_encode_blocks_host /
 // shmr_ec_reconstruct_blocks_host) and fan the shard-file I/O out over a
@@ -108,8 +109,9 @@ struct VfsOptions {
     // load_block: a shard whose length is not S is an erasure (the reference
     // zero-pads it and keeps it present, block.rs:548-551).
     bool short_shard_is_erasure = false;
-    // Block Cache buffers in pinned host memory (shmr_ec_host_alloc); falls
-    // back to pageable memory when no device is present.
+    // Block Cache buffers in mapped host memory (shmr_ec_host_alloc: the codec
+    // runs zero-copy on them); falls back to pageable memory when no device is
+    // present.
     bool pinned_buffers = false;
     // fsync every shard file after writing it (write_path, block.rs:633).
     // Benchmarks may turn it off to separate the device path from the disk.

@@ -5,7 +5,7 @@
 // every host<->device copy; they are reported in DESIGN.md, never as bench.py's
 // value.
 //
-//   shmr_vfs_bench <bucket_dir> [file_MiB=256] [block_MiB=4] [fsync=1] [reps=3]
+//   shmr_vfs_bench <bucket_dir> [file_MiB=256] [block_MiB=4] [fsync=1] [reps=3] [batch_MiB...]
 #include <unistd.h>
 
 #include <atomic>
@@ -106,7 +106,7 @@ Result run_once(const std::shared_ptr<const ShmrFsConfig>& cfg, uint64_t ino, co
 
 int main(int argc, char** argv) {
     if (argc < 2) {
-        std::fprintf(stderr, "usage: %s <bucket_dir> [file_MiB=256] [block_MiB=4] [fsync=1] [reps=3]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s <bucket_dir> [file_MiB=256] [block_MiB=4] [fsync=1] [reps=3] [batch_MiB...]\n", argv[0]);
         return 2;
     }
     const std::string bucket = argv[1];
@@ -130,7 +130,9 @@ int main(int argc, char** argv) {
     }
     const double GiB = double(1ull << 30);
     const double bytes = double(src.size());
-    const size_t batch_mib[] = {VirtualFile::kAutoBatch, 0};
+    // batch sizes: auto policy, one batch, and explicit pipeline batches (MiB)
+    std::vector<size_t> batch_mib = {VirtualFile::kAutoBatch, 0};
+    for (int i = 6; i < argc; ++i) batch_mib.push_back(std::strtoull(argv[i], nullptr, 10));
     for (int pinned = 1; pinned >= 0; --pinned)
     for (size_t bm : batch_mib) {
         VfsOptions o;
@@ -164,14 +166,14 @@ int main(int argc, char** argv) {
             "\"write_GiBps\": %.2f, \"sync_GiBps\": %.2f, \"sync_encode_GiBps\": %.2f, \"sync_shard_io_GiBps\": %.2f, "
             "\"sync_pipeline_GiBps\": %.2f, \"per_block_sync_GiBps\": %.2f, \"read_with_erasure_GiBps\": %.2f, "
             "\"read_reconstruct_GiBps\": %.2f, \"read_shard_io_GiBps\": %.2f, \"read_pipeline_GiBps\": %.2f, "
-            "\"reconstructed_blocks\": %zu, \"verified\": true}\n",
+            "\"reconstructed_blocks\": %zu, \"sync_prepare_ms\": %.2f, \"read_prepare_ms\": %.2f, \"verified\": true}\n",
             pinned ? "mapped Block Cache (shmr_ec_host_alloc)" : "pageable", (unsigned long long)(zc1 - zc0),
-            (unsigned long long)(st1 - st0), bm == VirtualFile::kAutoBatch ? "auto" : "one batch",
+            (unsigned long long)(st1 - st0), bm == VirtualFile::kAutoBatch ? "auto" : bm == 0 ? "one batch" : (std::to_string(bm) + " MiB").c_str(),
             (unsigned long long)file_mib, (unsigned long long)block_mib, int(do_fsync),
             reps, bytes / best.write_s / GiB, bytes / best.sync_s / GiB, bytes / best.sync.codec_s / GiB,
             bytes / best.sync.io_s / GiB, bytes / best.sync.total_s / GiB, bytes / best.per_block_sync_s / GiB,
             bytes / best.read_s / GiB, bytes / best.load.codec_s / GiB, bytes / best.load.io_s / GiB,
-            bytes / best.load.total_s / GiB, best.load.blocks);
+            bytes / best.load.total_s / GiB, best.load.blocks, best.sync.prepare_s * 1e3, best.load.prepare_s * 1e3);
         std::fflush(stdout);
     }
     return 0;
