@@ -231,6 +231,17 @@ def load_traffic(config: str, B: int):
     return rec.get("hbm_bytes_per_launch")
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
 def cpu_baseline(k, p, S, data_t, parity_t, budget_s):
     """CPU restatement of the crate's simd_c AVX2 loop (oracle/, "port"),
     one block per thread as rayon does over VirtualFile blocks; bounded sample
@@ -253,11 +264,12 @@ def cpu_baseline(k, p, S, data_t, parity_t, budget_s):
         "unit": "GiB/s",
         "cores": cores,
         "kind": "port",
-        "sample": f"{nb} blocks x {reps} reps of the same RS({k},{p}) workload, {cores} threads "
+        "sample": f"{nb} blocks x {reps} reps of the same RS({k},{p}) workload ({secs:.1f} s wall, "
+                  f"~{secs * cores:.0f} core-seconds), {cores} threads "
                   f"(one block per thread, AVX2 nibble-pshufb loop restating reed-solomon-erasure "
                   f"6.0.0 simd_c); encode only (erasure_encode_duration scope, block.rs:425-430)",
         "single_core_GiBps": round(k * S / single / 2 ** 30, 3),
-        "cpu_model": platform.processor() or platform.machine(),
+        "cpu_model": cpu_model(),
         "gpu_parity_bit_exact_on_sample": ok,
     }
 

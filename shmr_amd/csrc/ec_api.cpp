@@ -126,12 +126,15 @@ int shmr_ec_describe_variant(int decode, uint32_t data_shards, uint32_t rows, ch
     if (!buf || len == 0 || rows == 0) return SHMR_EC_INVALID_ARGUMENT;
     const core::OpClass op = decode ? core::kDecode : core::kEncode;
     const auto v = core::resolve_variant(op, data_shards, std::min<uint32_t>(rows, shmr::kern::kMaxRowsPerLaunch));
+    auto lean = v;   // the full-tile kernel without fused tails must always exist
+    lean.fuse_tail = false;
+    const bool compiled = shmr::kern::variant_compiled(lean) && (!v.fuse_tail || shmr::kern::variant_compiled(v));
     std::snprintf(buf, len,
                   "chunks=%d nt_load=%d nt_store=%d scalar_tabs=%d occ8=%d threads=%d grid=%d diag=%d depth=%d "
-                  "wgs_per_cu=%d occ=%d early=%d spre=%d xcd=%d compiled=%d",
+                  "wgs_per_cu=%d occ=%d early=%d spre=%d xcd=%d fuse_tail=%d compiled=%d",
                   v.u, int(v.nt_load), int(v.nt_store), int(v.scalar_tabs), int(v.occ8), v.threads,
-                  core::grid_mode(op), int(v.diag), v.depth, v.wgs_per_cu, v.occ, int(v.early), int(v.spre), int(v.xcd),
-                  int(shmr::kern::variant_compiled(v)));
+                  core::grid_mode(op), int(v.diag), v.depth, v.wgs_per_cu, v.occ, int(v.early), int(v.spre), int(v.xcd), int(v.fuse_tail),
+                  int(compiled));
     return SHMR_EC_OK;
 }
 

@@ -30,6 +30,7 @@ struct Tuning {
     std::atomic<int> early{kAuto};
     std::atomic<int> spre{kAuto};
     std::atomic<int> xcd{kAuto};
+    std::atomic<int> fuse_tail{kAuto};
 };
 Tuning g_tune[2];   // [kEncode], [kDecode]
 
@@ -44,11 +45,13 @@ Tuning g_tune[2];   // [kEncode], [kDecode]
 // staging ("early": RS(4,2) 83 % vs 80 %; neutral at k = 8, -2 % on decode).
 // Scalar-loaded tables ("spre", 7-8 waves/SIMD) lose 3-6 % everywhere.
 // XCD-grouped tile order ("xcd") is within +-2 % (RS(8,3) +0.5 %, RS(4,2)
-// -2 %): off.  Also measured and dropped: running the partial last tile of
-// RS(10,4) shards inside the full-tile launch (+5 % time: the extra path costs
-// 4-7 VGPRs) or concurrently on a side stream (+3 %), and uploading multi-plan
-// tables on a side stream (neutral) -- the plain tail launch after the full
-// tiles stays.
+// -2 %): off.  Shard lengths that are not a multiple of the tile (RS(10,4):
+// S = 1,677,722) run each block's partial last tile at the HEAD of the
+// full-tile grid ("fuse_tail"): 5.5-5.8 % less time than a second launch of
+// 64 latency-bound workgroups after the full tiles.  Placed at each block's
+// end instead, the slow partial tiles finished last and the fused launch lost
+// 5 %; a concurrent side-stream tail launch lost 3 %; uploading multi-plan
+// tables on a side stream was neutral.
 //
 // Zero-copy launches over mapped host memory (the kernel's loads and stores
 // cross PCIe) are bound by the link, not HBM: there plain (temporal) loads
@@ -61,6 +64,7 @@ kern::Variant variant_policy(OpClass op, unsigned k, unsigned rows, bool host_ma
     v.nt_load = !host_mapped;
     v.depth = 2;
     v.early = op == kEncode && k < 8 && !host_mapped;
+    v.fuse_tail = true;   // only where len % tile != 0 (RS(10,4): -5.5 % encode, -5.8 % decode time)
     return v;
 }
 
@@ -123,6 +127,8 @@ int set_tuning(const char* key, int value) {
             T.spre = value == kAuto ? kAuto : (value != 0);
         } else if (k == "xcd") {
             T.xcd = value == kAuto ? kAuto : (value != 0);
+        } else if (k == "fuse_tail") {
+            T.fuse_tail = value == kAuto ? kAuto : (value != 0);
         } else {
             return SHMR_EC_INVALID_ARGUMENT;
         }
@@ -149,6 +155,7 @@ int get_tuning(const char* key) {
     if (k == "early") return T.early;
     if (k == "spre") return T.spre;
     if (k == "xcd") return T.xcd;
+    if (k == "fuse_tail") return T.fuse_tail;
     return SHMR_EC_INVALID_ARGUMENT;
 }
 
@@ -168,6 +175,7 @@ kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_m
     if (T.early.load() != kAuto) v.early = T.early.load() != 0;
     if (T.spre.load() != kAuto) v.spre = T.spre.load() != 0;
     if (T.xcd.load() != kAuto) v.xcd = T.xcd.load() != 0;
+    if (T.fuse_tail.load() != kAuto) v.fuse_tail = T.fuse_tail.load() != 0;
     return v;
 }
 
@@ -278,15 +286,25 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
             continue;
         }
         const uint64_t full = len / tb;
+        // Fused tails: the partial last tile of every block leads the
+        // full-tile grid (one launch), if that instantiation is compiled.
+        bool fused = false;
+        if (var.fuse_tail && full > 0 && len % tb != 0) {
+            kern::Variant fv = var;
+            fused = kern::variant_compiled(fv);
+        }
+        var.fuse_tail = fused;
         if (full) {
             a.col_base = 0;
             a.tiles_per_block = uint32_t(full);
-            a.ntiles = nblk * full;
+            a.lead_tails = fused ? nblk : 0;
+            a.ntiles = nblk * full + a.lead_tails;
             const hipError_t e = kern::launch_apply(a, rows, var, 0, cap, stream);
             if (e == hipErrorInvalidValue) return SHMR_EC_INVALID_ARGUMENT;   // variant not compiled
             if (e != hipSuccess) return SHMR_EC_DEVICE_ERROR;
+            a.lead_tails = 0;
         }
-        if (len % tb) {
+        if (len % tb && !fused) {
             const uint64_t tb1 = kern::tile_bytes(1);
             a.col_base = full * tb;
             a.tiles_per_block = uint32_t((len - full * tb + tb1 - 1) / tb1);

@@ -49,6 +49,8 @@ constexpr int kDepth2 = 512;     // 1 shard of loads in flight
 constexpr int kDepth1 = 1024;    // no look-ahead (load, wait, multiply)
 constexpr int kEarly = 1 << 16;  // first data loads issued before the plan's LDS staging completes
 constexpr int kSPre = 1 << 17;   // tables + offsets by scalar loads one shard ahead, no LDS
+constexpr int kFuse = 1 << 18;   // leading partial tiles (ApplyArgs::lead_tails) in a MODE 0 launch; a
+                                 // separate instantiation: the bounds-checked path costs 4-7 VGPRs
 // Bits 12-15: occupancy target in waves per SIMD (0 = compiler's choice);
 // the register allocator must then fit 512 / target VGPRs.
 constexpr int kOccShift = 12;
@@ -537,6 +539,22 @@ __device__ __forceinline__ uint64_t first_tile(const ApplyArgs& a) {
     return w;
 }
 
+// Block j and column tile cc of grid tile `tile` (see ApplyArgs::lead_tails).
+struct TileRef {
+    uint64_t j, cc;
+    bool tail;
+};
+template <int F>
+__device__ __forceinline__ TileRef tile_ref(const ApplyArgs& a, uint64_t tile) {
+    const uint32_t tpb = a.tiles_per_block;
+    if constexpr ((F & kFuse) != 0) {
+        if (tile < a.lead_tails) return TileRef{tile, tpb, true};
+        tile -= a.lead_tails;
+    }
+    const uint64_t j = tile / tpb;
+    return TileRef{j, tile - j * tpb, false};
+}
+
 // The second __launch_bounds__ argument is amdgpu_waves_per_eu (minimum).
 template <int R, int U, int MODE, int F>
 __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) void gf_apply_kernel(const ApplyArgs a) {
@@ -547,12 +565,11 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
     // pick the plan per block; single-plan launches stage it once.
     const bool multi = a.plan_table != nullptr;
     if constexpr ((F & (kEarly | kSPre)) != 0) {
-        const uint32_t tpb = a.tiles_per_block;
         const uint64_t tb = uint64_t(TH) * 16 * U;
         bool first = true;
         for (uint64_t tile = first_tile(a); tile < a.ntiles; tile += gridDim.x) {
-            const uint64_t j = tile / tpb;
-            const uint64_t cc = tile - j * tpb;
+            const TileRef tr = tile_ref<F>(a, tile);
+            const uint64_t j = tr.j, cc = tr.cc;
             const uint64_t blk = a.blk_list ? uint64_t(as_const<cu32>(a.blk_list)[j]) : a.blk_first + j * a.blk_stride;
             uint64_t pa = reinterpret_cast<uint64_t>(a.plan);
             if (multi) {   // plan_table[blk_plan[j]] through scalar loads
@@ -561,17 +578,23 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
                 pa = uint64_t(pt[2 * pi]) | (uint64_t(pt[2 * pi + 1]) << 32);
             }
             const uint8_t* plan = reinterpret_cast<const uint8_t*>(pa);
+            const uint8_t* ib = a.in_base + blk * a.in_bpitch;
+            uint8_t* ob = a.out_base + blk * a.out_bpitch;
+            const uint64_t col = a.col_base + cc * tb;
             if constexpr ((F & kSPre) != 0) {
-                if (a.in_identity)
-                    spre_tile<R, U, MODE, F, true>(a, plan, a.in_base + blk * a.in_bpitch,
-                                                   a.out_base + blk * a.out_bpitch, a.col_base + cc * tb);
-                else
-                    spre_tile<R, U, MODE, F, false>(a, plan, a.in_base + blk * a.in_bpitch,
-                                                    a.out_base + blk * a.out_bpitch, a.col_base + cc * tb);
+                if ((F & kFuse) != 0 && MODE == 0 && tr.tail) {
+                    if (a.in_identity) spre_tile<R, U, 1, F, true>(a, plan, ib, ob, col);
+                    else spre_tile<R, U, 1, F, false>(a, plan, ib, ob, col);
+                } else if (a.in_identity) {
+                    spre_tile<R, U, MODE, F, true>(a, plan, ib, ob, col);
+                } else {
+                    spre_tile<R, U, MODE, F, false>(a, plan, ib, ob, col);
+                }
+            } else if ((F & kFuse) != 0 && MODE == 0 && tr.tail) {
+                early_tile<R, U, 1, F>(a, plan, smem, first, ib, ob, col);
+            } else {
+                early_tile<R, U, MODE, F>(a, plan, smem, first, ib, ob, col);
             }
-            else
-                early_tile<R, U, MODE, F>(a, plan, smem, first, a.in_base + blk * a.in_bpitch,
-                                          a.out_base + blk * a.out_bpitch, a.col_base + cc * tb);
             first = false;
         }
         return;
@@ -589,11 +612,10 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
             c.g_tab = reinterpret_cast<const uint32_t*>(a.plan + a.tab_off);
         }
     }
-    const uint32_t tpb = a.tiles_per_block;
     const uint64_t tb = uint64_t(TH) * 16 * U;
     for (uint64_t tile = first_tile(a); tile < a.ntiles; tile += gridDim.x) {
-        const uint64_t j = tile / tpb;
-        const uint64_t cc = tile - j * tpb;
+        const TileRef tr = tile_ref<F>(a, tile);
+        const uint64_t j = tr.j, cc = tr.cc;
         const uint64_t blk = a.blk_list ? uint64_t(a.blk_list[j]) : a.blk_first + j * a.blk_stride;
         if (restage) {
             const uint8_t* plan = multi ? a.plan_table[a.blk_plan[j]] : a.plan;
@@ -609,7 +631,8 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
         }
         const uint8_t* ib = a.in_base + blk * a.in_bpitch;
         uint8_t* ob = a.out_base + blk * a.out_bpitch;
-        do_tile<R, U, MODE, F>(a, c, ib, ob, a.col_base + cc * tb);
+        if ((F & kFuse) != 0 && MODE == 0 && tr.tail) do_tile<R, U, 1, F>(a, c, ib, ob, a.col_base + cc * tb);
+        else do_tile<R, U, MODE, F>(a, c, ib, ob, a.col_base + cc * tb);
     }
 }
 
@@ -700,14 +723,20 @@ hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStr
     X(1, kNtLoad | kNtStore | kDepth2 | kEarly | (6 << kOccShift)) \
     X(1, kNtLoad | kNtStore | kDepth2 | kSPre) \
     X(2, kNtLoad | kNtStore | kDepth2 | kSPre) \
-    X(1, kNtLoad | kNtStore | kSPre)
+    X(1, kNtLoad | kNtStore | kSPre) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kFuse) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kFuse) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse) \
+    X(1, kNtStore | kDepth2 | kFuse) \
+    X(2, kNtStore | kDepth2 | kFuse)
 
 int variant_flags(const Variant& v) {
     return (v.nt_load ? kNtLoad : 0) | (v.nt_store ? kNtStore : 0) | (v.scalar_tabs ? kScalarTabs : 0) |
            (v.occ8 ? kOcc8 : 0) | (v.diag ? kDiagXor : 0) | (v.threads == 128 ? kTh128 : 0) |
            (v.threads == 512 ? kTh512 : 0) | (v.depth == 5 ? kDepth5 : 0) | (v.depth == 9 ? kDepth9 : 0) |
            (v.depth == 2 ? kDepth2 : 0) | (v.depth == 1 ? kDepth1 : 0) | ((v.occ & 15) << kOccShift) |
-           (v.early ? kEarly : 0) | (v.spre ? kSPre : 0);
+           (v.early ? kEarly : 0) | (v.spre ? kSPre : 0) | (v.fuse_tail ? kFuse : 0);
 }
 
 template <int R>

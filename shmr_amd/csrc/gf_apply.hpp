@@ -53,6 +53,12 @@ struct ApplyArgs {
     // every XCD streams one contiguous eighth of the batch (tiles >= 8 * xcd_q
     // keep their own index).  0 = tile w.
     uint64_t xcd_q;
+    // Fused tails (kernels compiled with the fused-tail flag): the first
+    // lead_tails tiles of the grid are the partial last tiles of blocks
+    // j = 0 .. lead_tails-1 (column col_base + tiles_per_block * tile bytes),
+    // run bounds-checked; tile lead_tails + t is full tile t.  Leading, so the
+    // latency-bound partial tiles start first and finish under the full ones.
+    uint64_t lead_tails;
 };
 
 // Compiled-in kernel variant for full tiles (see gf_apply.hip dispatch_full).
@@ -70,6 +76,7 @@ struct Variant {
     bool early = false;      // first data loads before the plan's LDS staging completes
     bool spre = false;       // tables/offsets by scalar loads one shard ahead (no LDS)
     bool xcd = false;        // XCD-grouped tile order (ApplyArgs::xcd_q)
+    bool fuse_tail = false;  // partial last tiles inside the full-tile launch (ApplyArgs::lead_tails)
 };
 
 // rows in [1, kMaxRowsPerLaunch].  mode 0: full tiles, every shard base

@@ -199,6 +199,8 @@ def test_tuning_api():
     assert "early=1" in shmr_amd.describe_variant(False, 4, 2)
     assert "early=0" in shmr_amd.describe_variant(False, 8, 3)
     assert "early=0" in shmr_amd.describe_variant(True, 4, 2)
+    assert "fuse_tail=1" in shmr_amd.describe_variant(False, 10, 4)
+    assert "fuse_tail=1" in shmr_amd.describe_variant(True, 10, 2)
 
 
 def test_auto_policy_variants_are_compiled():

@@ -1,0 +1,14 @@
+#!/bin/bash
+# rocprofv3 kernel-trace + PMC passes for every bench config (tools/profile.sh),
+# one after the other; stops at the first failure.  Algorithmic bytes per
+# launch: B * (k + rows) * S -- for RS(10,4) (S = 1,677,722, not a multiple of
+# the tile) the partial last tiles run at the head of the same launch.
+# Usage: tools/profile_all.sh <round-tag>
+set -eu
+T=$1
+D="$(cd "$(dirname "$0")" && pwd)"
+bash "$D/profile.sh" "$T" encode83 512 2952790016
+bash "$D/profile.sh" "$T" decode83 512 2415919104
+bash "$D/profile.sh" "$T" encode104 64 $((64 * 14 * 1677722))
+bash "$D/profile.sh" "$T" decode104 64 $((64 * 12 * 1677722))
+bash "$D/profile.sh" "$T" encode42 1024 1610612736
