@@ -347,3 +347,80 @@ def test_sync_data_erasure_via_gpu(gpu):
     ref = O.sync_data_erasure(buf.tobytes(), size, k, p)
     for a, b in zip(shards, ref):
         assert np.array_equal(a, b)
+
+
+# ------------------------------------------------------- maximum shard counts
+@pytest.mark.parametrize("k,p", [(255, 1), (1, 255), (128, 128), (200, 56)])
+def test_max_shard_counts_encode_reconstruct(gpu, k, p):
+    """k + p = 256, the crate's limit (ReedSolomon::new, block.rs:405): encode
+    on the GPU vs the oracle, then lose p shards (the most the code allows)
+    and rebuild them, bit-exact.  p > 4 output rows run as several launches."""
+    L = 4096 + 24
+    rng = np.random.default_rng([k, p])
+    data = rand_shards(rng, k, L)
+    shards = [d.copy() for d in data] + [np.zeros(L, np.uint8) for _ in range(p)]
+    rs = shmr_amd.ReedSolomon(k, p)
+    rs.encode(shards)
+    want = oracle_parity(k, p, data)
+    for a, b in zip(shards[k:], want):
+        assert np.array_equal(a, b)
+    full = [s.copy() for s in shards]
+    lost = rng.choice(k + p, size=p, replace=False)
+    got = [None if i in lost else full[i].copy() for i in range(k + p)]
+    rs.reconstruct(got)
+    for i in range(k + p):
+        assert np.array_equal(got[i], full[i]), i
+
+
+def test_too_many_erasures_on_gpu_path(gpu):
+    """p + 1 absent shards -> TooFewShardsPresent before any device work, and
+    the present buffers are untouched (the reference would panic on unwrap)."""
+    k, p, L = 8, 3, 1000
+    rng = np.random.default_rng(1)
+    shards = rand_shards(rng, k + p, L)
+    keep = [s.copy() for s in shards]
+    for i in (0, 3, 9, 10):
+        shards[i] = None
+    with pytest.raises(shmr_amd.Error) as e:
+        shmr_amd.ReedSolomon(k, p).reconstruct(shards)
+    assert e.value.name == "TooFewShardsPresent"
+    for i in range(k + p):
+        if shards[i] is not None:
+            assert np.array_equal(shards[i], keep[i])
+
+
+@pytest.mark.parametrize("mapped", [False, True])
+def test_blocks_host_device_list_round_robin(gpu, mapped):
+    """devices=[0, 0, 0]: the multi-device worker fan-out (block b ->
+    devices[b % 3], one worker per entry) on the one GPU of the box, staged
+    and zero-copy."""
+    k, p, S, B = 8, 3, 65536 + 48, 10
+    rng = np.random.default_rng(17)
+    keep = None
+    if mapped:
+        keep = shmr_amd.PinnedBuffer(B * (k + p) * S)
+        arr = keep.array.reshape(B, k + p, S)
+        blocks = [[arr[b, i] for i in range(k + p)] for b in range(B)]
+    else:
+        blocks = [[np.zeros(S, np.uint8) for _ in range(k + p)] for _ in range(B)]
+    for blk in blocks:
+        for i in range(k):
+            blk[i][:] = rng.integers(0, 256, S, dtype=np.uint8)
+    rs = shmr_amd.ReedSolomon(k, p)
+    z0, s0 = shmr_amd.path_stats()
+    rs.encode_blocks_host(blocks, devices=[0, 0, 0])
+    z1, s1 = shmr_amd.path_stats()
+    assert (z1 - z0, s1 - s0) == ((B, 0) if mapped else (0, B))
+    for blk in blocks:
+        for got, want in zip(blk[k:], oracle_parity(k, p, blk[:k])):
+            assert np.array_equal(got, want)
+    full = [[x.copy() for x in blk] for blk in blocks]
+    present = np.ones((B, k + p), np.uint8)
+    for b in range(B):
+        present[b, [(b % k), k + (b % p)]] = 0
+        blocks[b][b % k][:] = 0
+        blocks[b][k + b % p][:] = 0
+    rs.reconstruct_blocks_host(blocks, present, devices=[0, 0, 0])
+    for b in range(B):
+        for i in range(k + p):
+            assert np.array_equal(blocks[b][i], full[b][i]), (b, i)
