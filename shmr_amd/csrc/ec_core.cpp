@@ -232,10 +232,11 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
     if (nblk == 0 || plan.m == 0) return SHMR_EC_OK;
     const uint8_t* dplan = nullptr;
     const uint32_t tab_off = plan_tab_off(plan.k, plan.m);
-    if (!bs.d_plans) {
+    if (!bs.d_plans && !bs.segs) {
         int rc = plan_on_device(plan, dev, &dplan);
         if (rc) return rc;
     }
+    if (bs.nseg > kern::kMaxSegs) return SHMR_EC_INVALID_ARGUMENT;
     bool identity = true;   // encode plans (and decodes that lost only parity) read shard t as input t
     for (uint32_t t = 0; t < plan.k; ++t) identity = identity && plan.in_idx[t] == t;
     kern::Variant tail;   // tail / unaligned launches: U = 1, plain loads
@@ -274,7 +275,9 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
         a.row0 = row0;
         a.plan = dplan;
         a.tab_off = tab_off;
-        a.in_identity = bs.d_plans ? 0u : uint32_t(identity);
+        a.in_identity = (bs.d_plans || bs.segs) ? 0u : uint32_t(identity);
+        a.nseg = bs.segs ? bs.nseg : 0;
+        for (uint32_t i = 0; i < a.nseg; ++i) a.segs[i] = bs.segs[i];
         a.shard_ptrs = L.d_ptrs;
         a.total = L.total;
         if (!aligned) {
@@ -389,6 +392,49 @@ int reconstruct_on_device(Codec& c, int dev, const Layout& L, const uint8_t* pre
             rc = launch_set(*grp.plans[0], dev, L, bs, len, stream, kDecode);
             if (rc) return rc;
             continue;
+        }
+        // Few patterns whose blocks form few arithmetic runs (a failed disk,
+        // or the b-mod-k erasures of the benchmark): the runs and their plans
+        // travel in the kernel arguments -- no table upload on the stream and
+        // no dependent table loads in the kernel prologue.
+        {
+            std::vector<kern::Seg> segs;
+            bool fits = true;
+            for (size_t i = 0; i < grp.blocks.size() && fits;) {
+                size_t e = i + 1;
+                const uint32_t st = e < grp.blocks.size() ? grp.blocks[e] - grp.blocks[i] : 1;
+                while (e < grp.blocks.size() && grp.plan_idx[e] == grp.plan_idx[i] &&
+                       grp.blocks[e] > grp.blocks[e - 1] && grp.blocks[e] - grp.blocks[e - 1] == st)
+                    ++e;
+                if (segs.size() == kern::kMaxSegs) {
+                    fits = false;
+                    break;
+                }
+                kern::Seg sg{};
+                sg.start = uint32_t(i);
+                sg.first = grp.blocks[i];
+                sg.stride = e - i > 1 ? st : 1;
+                segs.push_back(sg);
+                // remember the plan index in pad_ until the device pointers are known
+                segs.back().pad_ = grp.plan_idx[i];
+                i = e;
+            }
+            if (fits) {
+                for (auto& sg : segs) {
+                    const uint8_t* dp = nullptr;
+                    rc = plan_on_device(*grp.plans[sg.pad_], dev, &dp);
+                    if (rc) return rc;
+                    sg.plan = dp;
+                    sg.pad_ = 0;
+                }
+                BlockSet bs;
+                bs.n = grp.blocks.size();
+                bs.segs = segs.data();
+                bs.nseg = uint32_t(segs.size());
+                rc = launch_set(*grp.plans[0], dev, L, bs, len, stream, kDecode);
+                if (rc) return rc;
+                continue;
+            }
         }
         if (grp.plans.size() > 65535) return SHMR_EC_INVALID_ARGUMENT;
         std::vector<const uint8_t*> dplans(grp.plans.size());

@@ -88,6 +88,10 @@ struct BlockSet {
     const uint32_t* d_list = nullptr;
     const uint16_t* d_plan_idx = nullptr;
     const uint8_t* const* d_plans = nullptr;
+    // or: up to kern::kMaxSegs arithmetic runs with their device plans, passed
+    // in the kernel arguments (no upload)
+    const kern::Seg* segs = nullptr;
+    uint32_t nseg = 0;
 };
 
 // Enqueues out = rows (x) in over a block set on the current device (= dev).

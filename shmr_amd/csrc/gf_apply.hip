@@ -539,6 +539,19 @@ __device__ __forceinline__ uint64_t first_tile(const ApplyArgs& a) {
     return w;
 }
 
+// Block index and plan of launch block j of a segment launch: binary search
+// over the (kernel-argument, wave-uniform) segment table -- scalar loads.
+__device__ __forceinline__ uint64_t seg_block(const ApplyArgs& a, uint64_t j, const uint8_t** plan) {
+    uint32_t lo = 0, hi = a.nseg;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a.segs[mid].start <= j) lo = mid;
+        else hi = mid;
+    }
+    *plan = a.segs[lo].plan;
+    return uint64_t(a.segs[lo].first) + (j - a.segs[lo].start) * uint64_t(a.segs[lo].stride);
+}
+
 // Block j and column tile cc of grid tile `tile` (see ApplyArgs::lead_tails).
 struct TileRef {
     uint64_t j, cc;
@@ -570,14 +583,18 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
         for (uint64_t tile = first_tile(a); tile < a.ntiles; tile += gridDim.x) {
             const TileRef tr = tile_ref<F>(a, tile);
             const uint64_t j = tr.j, cc = tr.cc;
-            const uint64_t blk = a.blk_list ? uint64_t(as_const<cu32>(a.blk_list)[j]) : a.blk_first + j * a.blk_stride;
-            uint64_t pa = reinterpret_cast<uint64_t>(a.plan);
-            if (multi) {   // plan_table[blk_plan[j]] through scalar loads
-                const uint32_t pi = plan_u16(a.blk_plan, uint32_t(j));
-                const cu32* pt = as_const<cu32>(a.plan_table);
-                pa = uint64_t(pt[2 * pi]) | (uint64_t(pt[2 * pi + 1]) << 32);
+            uint64_t blk;
+            const uint8_t* plan = a.plan;
+            if (a.nseg) {
+                blk = seg_block(a, j, &plan);
+            } else {
+                blk = a.blk_list ? uint64_t(as_const<cu32>(a.blk_list)[j]) : a.blk_first + j * a.blk_stride;
+                if (multi) {   // plan_table[blk_plan[j]] through scalar loads
+                    const uint32_t pi = plan_u16(a.blk_plan, uint32_t(j));
+                    const cu32* pt = as_const<cu32>(a.plan_table);
+                    plan = reinterpret_cast<const uint8_t*>(uint64_t(pt[2 * pi]) | (uint64_t(pt[2 * pi + 1]) << 32));
+                }
             }
-            const uint8_t* plan = reinterpret_cast<const uint8_t*>(pa);
             const uint8_t* ib = a.in_base + blk * a.in_bpitch;
             uint8_t* ob = a.out_base + blk * a.out_bpitch;
             const uint64_t col = a.col_base + cc * tb;
@@ -599,8 +616,8 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
         }
         return;
     }
-    // Shard-pointer launches restage per tile (the offsets depend on the block).
-    const bool restage = multi || a.shard_ptrs != nullptr;
+    // Multi-plan, segment and shard-pointer launches restage per tile.
+    const bool restage = multi || a.nseg != 0 || a.shard_ptrs != nullptr;
     Ctx c{};
     if (!restage) {
         if constexpr (kLds) {
@@ -616,9 +633,15 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
     for (uint64_t tile = first_tile(a); tile < a.ntiles; tile += gridDim.x) {
         const TileRef tr = tile_ref<F>(a, tile);
         const uint64_t j = tr.j, cc = tr.cc;
-        const uint64_t blk = a.blk_list ? uint64_t(a.blk_list[j]) : a.blk_first + j * a.blk_stride;
+        const uint8_t* plan = a.plan;
+        uint64_t blk;
+        if (a.nseg) {
+            blk = seg_block(a, j, &plan);
+        } else {
+            blk = a.blk_list ? uint64_t(a.blk_list[j]) : a.blk_first + j * a.blk_stride;
+            if (multi) plan = a.plan_table[a.blk_plan[j]];
+        }
         if (restage) {
-            const uint8_t* plan = multi ? a.plan_table[a.blk_plan[j]] : a.plan;
             if constexpr (kLds) {
                 __syncthreads();   // previous tile's LDS reads are done
                 stage_plan<R, TH>(a, plan, smem, c, blk);

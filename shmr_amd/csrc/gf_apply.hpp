@@ -14,6 +14,18 @@ constexpr int kThreads = 256;                          // lanes per workgroup (4
 inline uint64_t tile_bytes(int u, int threads = kThreads) { return uint64_t(threads) * 16 * uint64_t(u); }
 constexpr unsigned kMaxRowsPerLaunch = 4;
 
+// Multi-plan launches described in the kernel arguments (no table upload):
+// launch blocks j in [start, start + count) of a segment are blocks
+// first + (j - start) * stride, all using `plan` (a device plan image).
+constexpr unsigned kMaxSegs = 32;
+struct Seg {
+    uint32_t start;
+    uint32_t first;
+    uint32_t stride;
+    uint32_t pad_;
+    const uint8_t* plan;
+};
+
 // Shard t of block b lives at in_base + b * in_bpitch + in_idx[t] * in_spitch,
 // output r of block b at out_base + b * out_bpitch + (out_idx[row0 + r] - out_bias) * out_spitch.
 // Blocks of a launch: blk_list[j] if blk_list, else blk_first + j * blk_stride.
@@ -59,6 +71,10 @@ struct ApplyArgs {
     // run bounds-checked; tile lead_tails + t is full tile t.  Leading, so the
     // latency-bound partial tiles start first and finish under the full ones.
     uint64_t lead_tails;
+    // Segment launches (nseg > 0; plan / plan_table / blk_list unused): block
+    // j of the launch is found in segs[0 .. nseg) (ascending start, segs[0].start = 0).
+    uint32_t nseg;
+    Seg segs[kMaxSegs];
 };
 
 // Compiled-in kernel variant for full tiles (see gf_apply.hip dispatch_full).

@@ -258,12 +258,14 @@ def test_encode_batch_dev_unaligned_reference_layout(gpu):
             assert np.array_equal(hp[b, r * S:(r + 1) * S], ref[r])
 
 
-@pytest.mark.parametrize("k,p,erasures", [(8, 3, 1), (10, 4, 2), (8, 3, 3)])
-def test_reconstruct_batch_dev_mixed_patterns(gpu, k, p, erasures):
+@pytest.mark.parametrize("k,p,erasures,B", [(8, 3, 1, 24), (10, 4, 2, 24), (8, 3, 3, 24),
+                                             (10, 4, 2, 90)])   # > 32 runs: uploaded block/plan tables
+def test_reconstruct_batch_dev_mixed_patterns(gpu, k, p, erasures, B):
+    """Mixed erasure patterns in one batch: few runs travel in the kernel
+    arguments (segment launch), many take the uploaded-table launch."""
     import torch
     S = 65536 + 12
     pitch = (S + 255) // 256 * 256
-    B = 24
     rng = np.random.default_rng(k + erasures)
     host = rng.integers(0, 256, (B, k + p, pitch), dtype=np.uint8)
     for b in range(B):
@@ -424,3 +426,30 @@ def test_blocks_host_device_list_round_robin(gpu, mapped):
     for b in range(B):
         for i in range(k + p):
             assert np.array_equal(blocks[b][i], full[b][i]), (b, i)
+
+
+def test_reconstruct_segments_irregular_runs(gpu):
+    """Two patterns whose blocks are not one arithmetic progression each (some
+    blocks lose nothing): split into several runs, still one segment launch."""
+    import torch
+    k, p, S, B = 8, 3, 8192 + 16, 40
+    pitch = S + 240
+    rng = np.random.default_rng(23)
+    host = rng.integers(0, 256, (B, k + p, pitch), dtype=np.uint8)
+    for b in range(B):
+        par = oracle_parity(k, p, [host[b, i, :S].copy() for i in range(k)])
+        for r in range(p):
+            host[b, k + r, :S] = par[r]
+    present = np.ones((B, k + p), np.uint8)
+    for b in range(B):
+        if b % 7 == 3:
+            continue                       # untouched blocks break the progressions
+        present[b, 2 if b % 2 else 9] = 0
+    dev = torch.from_numpy(host.copy()).to(gpu)
+    for b in range(B):
+        for i in range(k + p):
+            if not present[b, i]:
+                dev[b, i, :S] = 0xEE
+    shmr_amd.ReedSolomon(k, p).reconstruct_batch_dev(dev, present, shard_len=S)
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy()[:, :, :S], host[:, :, :S])
