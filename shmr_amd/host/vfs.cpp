@@ -690,28 +690,29 @@ std::vector<size_t> VirtualFile::blocks_for_range(uint64_t pos, size_t len) cons
     return out;
 }
 
-// mod.rs:137-180.  Chunks map to (block, block_pos) from chunk_idx * chunk_size,
-// ignoring pos % chunk_size, exactly as the reference does.
-Status VirtualFile::read(uint64_t pos, uint8_t* buf, size_t len, size_t* nread) {
-    *nread = 0;
-    if (!cfg_) return fs_error(EINVAL);
-    if (len == 0 || size == 0) return std::nullopt;
-    if (pos > size) return ShmrError{ShmrError::EndOfFile};
-    if (auto e = load_blocks(blocks_for_range(pos, len))) return e;
+namespace {
+
+// A run of consecutive chunks inside one block, copied as one memcpy.
+struct ReadRun {
+    size_t blk;
+    uint64_t block_pos;
+    size_t off, len;
+};
+
+}  // namespace
+
+// Plan of VirtualFile::read: runs of consecutive chunks inside one block.
+// When the block holds every byte of a run (buffered(blk) >= block_pos + n),
+// the reference's per-chunk copies are one contiguous copy (same bytes, same
+// count) at a known offset; planning stops at the first run that could come
+// up short, and *c / *done say where the reference's chunk loop takes over.
+template <class Buffered>
+static std::vector<ReadRun> plan_read_runs(const std::vector<VirtualBlock>& blocks, uint64_t chunk_size,
+                                           uint64_t block_size, uint64_t pos, size_t len, Buffered buffered,
+                                           uint64_t* c_out, size_t* done_out) {
     const uint64_t start_chunk = pos / chunk_size;
     const uint64_t end_chunk = len / chunk_size + start_chunk;
-    // Plan: runs of consecutive chunks inside one block.  When the block holds
-    // every byte of a run, the reference's per-chunk copies are one contiguous
-    // copy (same bytes, same count) at a known offset, and such runs are
-    // copied in parallel; the first run that could come up short (or fail)
-    // and everything after it is done chunk by chunk, in order, as the
-    // reference does.
-    struct Run {
-        size_t blk;
-        uint64_t block_pos;
-        size_t off, len;
-    };
-    std::vector<Run> runs;
+    std::vector<ReadRun> runs;
     uint64_t c = start_chunk;
     size_t done = 0;
     for (; c <= end_chunk;) {
@@ -720,11 +721,75 @@ Status VirtualFile::read(uint64_t pos, uint8_t* buf, size_t len, size_t* nread) 
         if (block_idx >= blocks.size()) break;
         const uint64_t run = std::min<uint64_t>(end_chunk - c + 1, (block_size - block_pos + chunk_size - 1) / chunk_size);
         const size_t want = size_t(std::min<uint64_t>(uint64_t(done) + run * chunk_size, len)) - done;
-        if (want > 0 && blocks[block_idx].buffered_len() < block_pos + want) break;
+        if (want > 0 && buffered(size_t(block_idx)) < block_pos + want) break;
         if (want > 0) runs.push_back({size_t(block_idx), block_pos, done, want});
         done += want;
         c += run;
     }
+    *c_out = c;
+    *done_out = done;
+    return runs;
+}
+
+// mod.rs:137-180.  Chunks map to (block, block_pos) from chunk_idx * chunk_size,
+// ignoring pos % chunk_size, exactly as the reference does.
+Status VirtualFile::read(uint64_t pos, uint8_t* buf, size_t len, size_t* nread) {
+    *nread = 0;
+    if (!cfg_) return fs_error(EINVAL);
+    if (len == 0 || size == 0) return std::nullopt;
+    if (pos > size) return ShmrError{ShmrError::EndOfFile};
+    // Copy-out overlapped with the load: the runs of blocks that the batched
+    // load is about to bring in (an Erasure v1 block always ends with its full
+    // `size` buffered) are planned up front and copied as soon as their batch
+    // is loaded, while later batches are still reading / reconstructing.
+    uint64_t c_early = 0;
+    size_t done_early = 0;
+    const std::vector<ReadRun> early = plan_read_runs(
+        blocks, chunk_size, block_size, pos, len,
+        [&](size_t bi) -> uint64_t {
+            const VirtualBlock& b = blocks[bi];
+            if (b.buffer_loaded()) return b.buffered_len();
+            const bool erasure1 = b.topology.kind == BlockTopology::Erasure && b.topology.version == 1;
+            return erasure1 ? b.size : 0;
+        },
+        &c_early, &done_early);
+    std::map<size_t, std::vector<size_t>> early_of;   // block -> early run indices
+    for (size_t i = 0; i < early.size(); ++i) early_of[early[i].blk].push_back(i);
+    std::vector<uint8_t> copied(early.size(), 0);
+    auto on_batch = [&](const std::vector<size_t>& loaded) {
+        std::vector<size_t> todo;
+        for (size_t bi : loaded) {
+            auto it = early_of.find(bi);
+            if (it != early_of.end()) todo.insert(todo.end(), it->second.begin(), it->second.end());
+        }
+        // load_blocks holds these blocks' locks until this returns; read their
+        // buffers directly (VirtualBlock::read would take the lock again)
+        parallel_for(todo.size(), todo.size() > 4 ? 8 : 1, [&](size_t q) {
+            const ReadRun& r = early[todo[q]];
+            const auto& data = blocks[r.blk].st_->buffer;
+            if (data.size() < r.block_pos + r.len) return;   // not as planned: the plan below copies it
+            std::memcpy(buf + r.off, data.data() + r.block_pos, r.len);
+            copied[todo[q]] = 1;
+        });
+    };
+    if (auto e = load_blocks(blocks_for_range(pos, len), on_batch)) return e;
+    uint64_t c = 0;
+    size_t done = 0;
+    std::vector<ReadRun> runs = plan_read_runs(blocks, chunk_size, block_size, pos, len,
+                                               [&](size_t bi) -> uint64_t { return blocks[bi].buffered_len(); },
+                                               &c, &done);
+    {   // runs already copied during the load (same run, same bytes) are skipped
+        std::vector<ReadRun> rest;
+        size_t e = 0;
+        for (const ReadRun& r : runs) {
+            while (e < early.size() && early[e].off < r.off) ++e;
+            const bool same = e < early.size() && copied[e] && early[e].blk == r.blk &&
+                              early[e].block_pos == r.block_pos && early[e].off == r.off && early[e].len == r.len;
+            if (!same) rest.push_back(r);
+        }
+        runs.swap(rest);
+    }
+    const uint64_t end_chunk = len / chunk_size + pos / chunk_size;
     std::vector<Status> res(runs.size());
     parallel_for(runs.size(), runs.size() > 4 ? 8 : 1, [&](size_t i) {
         size_t n = 0;
@@ -939,7 +1004,8 @@ Status VirtualFile::sync_data(bool force) {
 
 // Batched load_block (block.rs:496-584) over several blocks: the same rules
 // per block, one reconstruct call per (k, p, S) for the blocks with erasures.
-Status VirtualFile::load_blocks(const std::vector<size_t>& block_indices) {
+Status VirtualFile::load_blocks(const std::vector<size_t>& block_indices,
+                                const std::function<void(const std::vector<size_t>&)>& on_batch) {
     last_load = IoStats{};
     const double t0 = now_s();
     std::vector<Status> results(blocks.size());
@@ -1069,6 +1135,7 @@ Status VirtualFile::load_blocks(const std::vector<size_t>& block_indices) {
             io_busy += now_s() - tr;
         });
     };
+    std::vector<std::future<void>> handed;   // on_batch calls in flight
     if (!batches.empty()) start_read(0);
     for (size_t bi = 0; bi < batches.size(); ++bi) {
         reader.get();
@@ -1076,9 +1143,18 @@ Status VirtualFile::load_blocks(const std::vector<size_t>& block_indices) {
         const double tc = now_s();
         reconstruct_batch(batches[bi]);
         last_load.codec_s += now_s() - tc;
+        if (on_batch) {
+            std::vector<size_t> loaded;
+            for (size_t j = batches[bi].b; j < batches[bi].e; ++j) {
+                const size_t i = batches[bi].g->members[j];
+                if (!results[i]) loaded.push_back(i);
+            }
+            handed.push_back(std::async(std::launch::async, [&on_batch, loaded] { on_batch(loaded); }));
+        }
     }
     last_load.io_s = io_busy;
     last_load.total_s = now_s() - t1;
+    for (auto& f : handed) f.get();   // before the blocks' locks are released
     locks.held.clear();
     parallel_for(others.size(), 16, [&](size_t j) { results[others[j]] = blocks[others[j]].load_block(); });
     for (auto& r : results)

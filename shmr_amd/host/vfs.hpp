@@ -18,6 +18,7 @@
 
 #include <cstdint>
 #include <filesystem>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -193,15 +194,16 @@ public:
     IoStats last_sync, last_load;     // instrumentation of the last batched flush / load
     // Data bytes per pipelined batch of a flush / load (the codec call of one
     // batch overlaps the shard-file I/O of the previous one); 0 = one batch.
-    // Auto (the default): flushes with pinned Block-Cache buffers pipeline in
-    // 128 MiB batches (1.15x); loads, and anything with pageable buffers, run
-    // as one batch -- there the codec's copies and the file I/O compete for
-    // host memory bandwidth and pipelining measured slower.
+    // Auto (the default): with mapped Block-Cache buffers flushes pipeline in
+    // 128 MiB batches and loads in 64 MiB batches; pageable buffers run as one
+    // batch -- there the codec's copies and the file I/O compete for host
+    // memory bandwidth and pipelining measured slower.
     static constexpr size_t kAutoBatch = ~size_t(0);
     size_t pipeline_batch_bytes = kAutoBatch;
 
-    // read (mod.rs:137-180): the blocks the range touches are first loaded as
-    // one batch (load_blocks), then copied out chunk by chunk as the reference.
+    // read (mod.rs:137-180): the blocks the range touches are loaded in one
+    // batched call (load_blocks) and copied out as the reference's chunk loop
+    // would; runs of Erasure blocks are copied while later batches still load.
     Status read(uint64_t pos, uint8_t* buf, size_t len, size_t* nread);
     Status write(uint64_t pos, const uint8_t* buf, size_t len, size_t* nwritten);
     // sync_data (mod.rs:91-103): every block is flushed, errors reported after
@@ -210,7 +212,12 @@ public:
     Status sync_data(bool force);
     // Loads every listed block that is not buffered; Erasure blocks with
     // erasures are reconstructed in one batched GPU call per (k, p, S).
-    Status load_blocks(const std::vector<size_t>& block_indices);
+    // on_batch, if set, is called on a helper thread with the Erasure blocks of
+    // each pipeline batch as soon as they are loaded (while later batches load);
+    // it may read those blocks' buffers without locking -- load_blocks holds
+    // their locks until every on_batch call has returned.
+    Status load_blocks(const std::vector<size_t>& block_indices,
+                       const std::function<void(const std::vector<size_t>&)>& on_batch = {});
     Status drop_buffers() const;
     Status drop_handles() const;
     Status replace_block(size_t block_idx, VirtualBlock new_block);
