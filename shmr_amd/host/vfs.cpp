@@ -10,10 +10,14 @@
 #include <atomic>
 #include <cerrno>
 #include <chrono>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <future>
 #include <map>
+#include <memory>
 #include <new>
 #include <thread>
 #include <tuple>
@@ -40,18 +44,84 @@ Status write_path(int fd, const uint8_t* buf, size_t len, bool sync = true) {
     return std::nullopt;
 }
 
+// Persistent worker pool behind parallel_for: the host path fans out hundreds
+// of small file and memcpy tasks per flush / load batch, and spawning threads
+// per call cost milliseconds per batch.  A caller always works on its own job
+// and, once its indices are exhausted, withdraws helper slots no worker has
+// picked up yet, so nested parallel_for calls cannot deadlock.
+class WorkPool {
+public:
+    static WorkPool& get() {
+        static WorkPool* p = new WorkPool(32);   // leaked: outlives static teardown
+        return *p;
+    }
+    void run(size_t n, size_t threads, const std::function<void(size_t)>& fn) {
+        auto job = std::make_shared<Job>();
+        job->n = n;
+        job->fn = &fn;
+        const size_t helpers = std::min(threads, n) - 1;
+        {
+            std::lock_guard<std::mutex> lock(mu_);
+            for (size_t h = 0; h < helpers; ++h) queue_.push_back(job);
+            job->pending = helpers;
+        }
+        if (helpers == 1) cv_.notify_one();
+        else if (helpers > 1) cv_.notify_all();
+        work(*job);
+        std::unique_lock<std::mutex> lock(mu_);
+        for (auto it = queue_.begin(); it != queue_.end();) {   // withdraw unstarted helper slots
+            if (*it == job) {
+                it = queue_.erase(it);
+                --job->pending;
+            } else {
+                ++it;
+            }
+        }
+        done_cv_.wait(lock, [&] { return job->pending == 0; });
+    }
+
+private:
+    struct Job {
+        std::atomic<size_t> next{0};
+        size_t n = 0;
+        const std::function<void(size_t)>* fn = nullptr;
+        size_t pending = 0;   // helper slots queued or running (under mu_)
+    };
+    explicit WorkPool(size_t workers) {
+        for (size_t i = 0; i < workers; ++i) std::thread([this] { loop(); }).detach();
+    }
+    static void work(Job& j) {
+        for (size_t i = j.next++; i < j.n; i = j.next++) (*j.fn)(i);
+    }
+    void loop() {
+        for (;;) {
+            std::shared_ptr<Job> job;
+            {
+                std::unique_lock<std::mutex> lock(mu_);
+                cv_.wait(lock, [&] { return !queue_.empty(); });
+                job = queue_.front();
+                queue_.pop_front();
+            }
+            work(*job);
+            std::lock_guard<std::mutex> lock(mu_);
+            if (--job->pending == 0) done_cv_.notify_all();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    std::deque<std::shared_ptr<Job>> queue_;
+};
+
 // Runs fn(i) for i < n on up to `threads` threads (the reference's rayon fan-out).
 template <class F>
 void parallel_for(size_t n, size_t threads, F fn) {
     threads = std::max<size_t>(1, std::min(threads, n));
-    std::atomic<size_t> next{0};
-    auto work = [&] {
-        for (size_t i = next++; i < n; i = next++) fn(i);
-    };
-    std::vector<std::thread> th;
-    for (size_t t = 1; t < threads; ++t) th.emplace_back(work);
-    work();
-    for (auto& t : th) t.join();
+    if (threads == 1) {
+        for (size_t i = 0; i < n; ++i) fn(i);
+        return;
+    }
+    const std::function<void(size_t)> f = std::ref(fn);
+    WorkPool::get().run(n, threads, f);
 }
 
 }  // namespace
