@@ -561,7 +561,7 @@ Status VirtualBlock::write(uint64_t pos, const uint8_t* buf, size_t len, size_t*
 }
 
 // block.rs:373-452
-Status VirtualBlock::sync_data(bool force) const {
+Status VirtualBlock::sync_data(bool force, int device) const {
     if (!force && !st_->should_flush.load()) return std::nullopt;
     if (!st_->shard_loaded.load()) {
         if (auto e = open_handles()) return e;
@@ -576,6 +576,10 @@ Status VirtualBlock::sync_data(bool force) const {
         EcStatus es;
         auto r = ReedSolomon::create(topology.data, topology.parity, &es);   // block.rs:405
         if (!r) return ec_error(es.code);
+        if (device != 0) {
+            const int rc = shmr_ec_set_device(r->handle(), device);
+            if (rc != SHMR_EC_OK) return ec_error(rc);
+        }
         const size_t S = shard_size();                                      // block.rs:406
         if (auto e = prepare_erasure(buffer, topology, S)) return e;
         const size_t n = size_t(topology.data) + topology.parity;
@@ -956,6 +960,22 @@ Status VirtualFile::sync_data(bool force) {
     last_sync = IoStats{};
     const double t0 = now_s();
     std::vector<Status> results(blocks.size());
+    if (opt_.pinned_buffers && pipeline_batch_bytes == kAutoBatch) {
+        // one flush task per block (mod.rs:93-96's par_iter), blocks round-robin over the GPUs
+        const size_t nd = std::max<size_t>(1, devices.size());
+        std::atomic<size_t> coded{0};
+        parallel_for(blocks.size(), 16, [&](size_t i) {
+            const VirtualBlock& b = blocks[i];
+            const bool dirty = force || b.st_->should_flush.load();
+            results[i] = b.sync_data(force, devices.empty() ? 0 : devices[i % nd]);
+            if (!results[i] && dirty && b.topology.kind == BlockTopology::Erasure) ++coded;
+        });
+        last_sync.blocks = coded.load();
+        last_sync.total_s = now_s() - t0;
+        for (auto& r : results)
+            if (r) return r;
+        return std::nullopt;
+    }
     std::map<std::tuple<unsigned, unsigned, size_t>, Group> groups;
     std::vector<size_t> others;
     for (size_t i = 0; i < blocks.size(); ++i) {

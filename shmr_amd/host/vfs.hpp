@@ -151,7 +151,8 @@ public:
 
     Status read(uint64_t pos, uint8_t* buf, size_t len, size_t* nread) const;
     Status write(uint64_t pos, const uint8_t* buf, size_t len, size_t* nwritten) const;
-    Status sync_data(bool force) const;
+    Status sync_data(bool force) const { return sync_data(force, 0); }
+    Status sync_data(bool force, int device) const;   // Erasure encode on that GPU
     Status drop_buffer() const;
     Status drop_handles() const;
 
@@ -207,8 +208,12 @@ public:
     Status read(uint64_t pos, uint8_t* buf, size_t len, size_t* nread);
     Status write(uint64_t pos, const uint8_t* buf, size_t len, size_t* nwritten);
     // sync_data (mod.rs:91-103): every block is flushed, errors reported after
-    // all were attempted.  Erasure blocks with the same (k, p, S) are encoded in
-    // one batched GPU call, their k+p shard files written in parallel.
+    // all were attempted.  Mapped Block-Cache buffers (auto batching): one
+    // flush task per block on the worker pool, as the reference's rayon
+    // fan-out, each a zero-copy encode on GPU devices[i % n] plus its shard
+    // writes -- fine-grained overlap of encodes and writes (40 vs 34 GiB/s
+    // batched).  Otherwise Erasure blocks with the same (k, p, S) are encoded
+    // in pipelined batched GPU calls, their k+p shard files written in parallel.
     Status sync_data(bool force);
     // Loads every listed block that is not buffered; Erasure blocks with
     // erasures are reconstructed in one batched GPU call per (k, p, S).

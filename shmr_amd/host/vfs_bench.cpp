@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <random>
+#include <string>
 #include <thread>
 
 #include "vfs.hpp"
@@ -160,20 +161,30 @@ int main(int argc, char** argv) {
             best.per_block_sync_s = std::min(best.per_block_sync_s, r.per_block_sync_s);
         }
         shmr_ec_path_stats(&zc1, &st1);
+        // GiB/s of file data for a phase time, "null" for phases a mode does not have
+        auto rate = [&](double sec) {
+            if (!(sec > 0)) return std::string("null");
+            char t[32];
+            std::snprintf(t, sizeof t, "%.2f", bytes / sec / GiB);
+            return std::string(t);
+        };
+        const std::string batch_name =
+            bm == VirtualFile::kAutoBatch ? "auto" : bm == 0 ? "one batch" : std::to_string(bm) + " MiB";
         std::printf(
-            "{\"buffers\": \"%s\", \"codec_blocks_zero_copy\": %llu, \"codec_blocks_staged\": %llu, \"batch\": \"%s\", \"file_MiB\": %llu, \"block_MiB\": %llu, \"topology\": \"Erasure(1, 8, 3)\", "
+            "{\"buffers\": \"%s\", \"codec_blocks_zero_copy\": %llu, \"codec_blocks_staged\": %llu, \"batch\": \"%s\", "
+            "\"file_MiB\": %llu, \"block_MiB\": %llu, \"topology\": \"Erasure(1, 8, 3)\", "
             "\"fsync\": %d, \"reps\": %d, \"unit\": \"GiB/s of file data (best rep)\", "
-            "\"write_GiBps\": %.2f, \"sync_GiBps\": %.2f, \"sync_encode_GiBps\": %.2f, \"sync_shard_io_GiBps\": %.2f, "
-            "\"sync_pipeline_GiBps\": %.2f, \"per_block_sync_GiBps\": %.2f, \"read_with_erasure_GiBps\": %.2f, "
-            "\"read_reconstruct_GiBps\": %.2f, \"read_shard_io_GiBps\": %.2f, \"read_pipeline_GiBps\": %.2f, "
+            "\"write_GiBps\": %s, \"sync_GiBps\": %s, \"sync_encode_GiBps\": %s, \"sync_shard_io_GiBps\": %s, "
+            "\"sync_pipeline_GiBps\": %s, \"per_block_sync_GiBps\": %s, \"read_with_erasure_GiBps\": %s, "
+            "\"read_reconstruct_GiBps\": %s, \"read_shard_io_GiBps\": %s, \"read_pipeline_GiBps\": %s, "
             "\"reconstructed_blocks\": %zu, \"sync_prepare_ms\": %.2f, \"read_prepare_ms\": %.2f, \"verified\": true}\n",
             pinned ? "mapped Block Cache (shmr_ec_host_alloc)" : "pageable", (unsigned long long)(zc1 - zc0),
-            (unsigned long long)(st1 - st0), bm == VirtualFile::kAutoBatch ? "auto" : bm == 0 ? "one batch" : (std::to_string(bm) + " MiB").c_str(),
-            (unsigned long long)file_mib, (unsigned long long)block_mib, int(do_fsync),
-            reps, bytes / best.write_s / GiB, bytes / best.sync_s / GiB, bytes / best.sync.codec_s / GiB,
-            bytes / best.sync.io_s / GiB, bytes / best.sync.total_s / GiB, bytes / best.per_block_sync_s / GiB,
-            bytes / best.read_s / GiB, bytes / best.load.codec_s / GiB, bytes / best.load.io_s / GiB,
-            bytes / best.load.total_s / GiB, best.load.blocks, best.sync.prepare_s * 1e3, best.load.prepare_s * 1e3);
+            (unsigned long long)(st1 - st0), batch_name.c_str(), (unsigned long long)file_mib,
+            (unsigned long long)block_mib, int(do_fsync), reps, rate(best.write_s).c_str(), rate(best.sync_s).c_str(),
+            rate(best.sync.codec_s).c_str(), rate(best.sync.io_s).c_str(), rate(best.sync.total_s).c_str(),
+            rate(best.per_block_sync_s).c_str(), rate(best.read_s).c_str(), rate(best.load.codec_s).c_str(),
+            rate(best.load.io_s).c_str(), rate(best.load.total_s).c_str(), best.load.blocks, best.sync.prepare_s * 1e3,
+            best.load.prepare_s * 1e3);
         std::fflush(stdout);
     }
     return 0;

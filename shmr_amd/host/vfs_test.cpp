@@ -526,6 +526,53 @@ void test_virtual_file_batched_reconstruct() {
               fsize(shard_file(*cfg, vf.blocks[i], i % 11)) == calculate_shard_size(bs, 8));
 }
 
+// Mapped Block Cache with auto batching: sync_data flushes block by block on
+// the worker pool (zero-copy encodes, blocks round-robin over a device list),
+// then a pipelined load rebuilds a lost shard of every block.
+void test_virtual_file_mapped_per_block_flush() {
+    auto cfg = test_config();
+    auto in = read_input();
+    const uint64_t bs = 1024 * 1024;
+    const size_t nblk = in.size() / bs;
+    CHECK(nblk * bs == in.size() && nblk > 0);
+    VirtualFile vf = VirtualFile::new_with(17, 0);
+    vf.populate(cfg);
+    VfsOptions o;
+    o.missing_shard_is_erasure = true;
+    o.pread_from_start = true;
+    o.pinned_buffers = true;
+    for (size_t i = 0; i < nblk; ++i) {
+        VirtualBlock b;
+        CHECK_OK(VirtualBlock::create(17, i + 1, cfg, bs, BlockTopology::erasure(1, 8, 3), &b));
+        vf.blocks.push_back(b);
+    }
+    vf.set_options(o);
+    vf.devices = {0, 0};   // round-robin over a device list (one GPU on the test box)
+    uint64_t zc0 = 0, st0 = 0, zc1 = 0, st1 = 0;
+    shmr_ec_path_stats(&zc0, &st0);
+    size_t n = 0;
+    CHECK_OK(vf.write(0, in.data(), in.size(), &n));
+    CHECK(vf.blocks[0].buffer_pinned());
+    CHECK_OK(vf.sync_data(true));
+    CHECK(vf.last_sync.blocks == nblk);
+    shmr_ec_path_stats(&zc1, &st1);
+    CHECK(zc1 - zc0 == nblk && st1 == st0);   // every block encoded zero-copy
+    for (size_t i = 0; i < nblk; ++i) print_shards(*cfg, i, vf.blocks[i]);
+    CHECK_OK(vf.drop_buffers());
+    CHECK_OK(vf.drop_handles());
+    for (size_t i = 0; i < nblk; ++i) fs::remove(shard_file(*cfg, vf.blocks[i], (i * 5) % 11));
+    std::vector<uint8_t> rb(in.size());
+    CHECK_OK(vf.read(0, rb.data(), rb.size(), &n));
+    CHECK(n == in.size());
+    CHECK(vf.last_load.blocks == nblk);
+    CHECK(rb == in);
+    // a clean flush writes nothing; a forced one rewrites every shard
+    CHECK_OK(vf.sync_data(false));
+    CHECK_OK(vf.sync_data(true));
+    for (size_t i = 0; i < nblk; ++i)
+        CHECK(fsize(shard_file(*cfg, vf.blocks[i], (i * 5) % 11)) == calculate_shard_size(bs, 8));
+}
+
 // rewrite_erasure: Single blocks -> Erasure(1, 4, 2), batched.
 void test_rewrite_erasure() {
     auto cfg = test_config();
@@ -579,6 +626,7 @@ int main(int argc, char** argv) {
         {"replace_block_erasure", test_replace_block_erasure},
         {"virtual_file_batched_reconstruct", test_virtual_file_batched_reconstruct},
         {"rewrite_erasure", test_rewrite_erasure},
+        {"virtual_file_mapped_per_block_flush", test_virtual_file_mapped_per_block_flush},
     };
     auto it = cases.find(name);
     if (it == cases.end()) {

@@ -152,3 +152,18 @@ def test_rewrite_erasure(tmp_path, gpu):
         assert len(files) == 6
         for i, f in enumerate(files):
             assert np.array_equal(read(f), want[i]), f"block {b} shard {i}"
+
+
+@pytest.mark.gpu
+def test_virtual_file_mapped_per_block_flush(tmp_path, gpu):
+    """Mapped Block Cache, auto batching: per-block zero-copy flushes on the
+    worker pool (devices round-robin), then a pipelined load with one lost
+    shard per block -- shard files equal the oracle's sync_data Erasure arm."""
+    nblk, k, p = 10, 8, 3
+    data = np.concatenate([O.seeded_block(O.BENCH_SEED, 600 + i, MiB) for i in range(nblk)])
+    shards = run_case("virtual_file_mapped_per_block_flush", tmp_path, data)
+    assert sorted(shards) == list(range(nblk))
+    for b in range(nblk):
+        want = O.sync_data_erasure(data[b * MiB:(b + 1) * MiB].tobytes(), MiB, k, p)
+        for i, f in enumerate(shards[b]):
+            assert np.array_equal(read(f), want[i]), f"block {b} shard {i}"
