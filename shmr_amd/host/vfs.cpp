@@ -625,7 +625,8 @@ Status VirtualBlock::open_handles() const {
 }
 
 // block.rs:496-584
-Status VirtualBlock::load_block() const {
+Status VirtualBlock::load_block(bool* reconstructed, int device) const {
+    if (reconstructed) *reconstructed = false;
     if (!st_->shard_loaded.load()) {
         if (auto e = open_handles()) return e;
     }
@@ -645,6 +646,10 @@ Status VirtualBlock::load_block() const {
         EcStatus es;
         auto r = ReedSolomon::create(topology.data, topology.parity, &es);
         if (!r) return ec_error(es.code);
+        if (device != 0) {
+            const int rc = shmr_ec_set_device(r->handle(), device);
+            if (rc != SHMR_EC_OK) return ec_error(rc);
+        }
         const size_t S = shard_size();
         const size_t n = st_->handles.size();
         buffer.reserve(std::max<size_t>(size, n * S));
@@ -665,6 +670,7 @@ Status VirtualBlock::load_block() const {
         if (missing) {
             es = r->reconstruct_in_place(ptrs.data(), present.data(), n, S, false);   // block.rs:560 (unwrap)
             if (!es.ok()) return ec_error(es.code);
+            if (reconstructed) *reconstructed = true;
         }
         buffer.resize(size);   // ec_data[..size] (block.rs:576); the bytes are already in place
     }
@@ -1099,6 +1105,32 @@ Status VirtualFile::load_blocks(const std::vector<size_t>& block_indices,
     last_load = IoStats{};
     const double t0 = now_s();
     std::vector<Status> results(blocks.size());
+    if (opt_.pinned_buffers && pipeline_batch_bytes == kAutoBatch) {
+        // one load task per block (block.rs:496-584 each), blocks round-robin over the GPUs
+        std::vector<size_t> todo;
+        for (size_t i : block_indices) {
+            if (i >= blocks.size()) return ShmrError{ShmrError::BlockIndexOutOfBounds};
+            if (!blocks[i].st_->buffer_loaded.load()) todo.push_back(i);
+        }
+        const size_t nd = std::max<size_t>(1, devices.size());
+        std::atomic<size_t> rebuilt{0};
+        parallel_for(todo.size(), 16, [&](size_t q) {
+            const size_t i = todo[q];
+            const VirtualBlock& b = blocks[i];
+            bool rec = false;
+            results[i] = b.load_block(&rec, devices.empty() ? 0 : devices[i % nd]);
+            if (rec) ++rebuilt;
+            if (!results[i] && on_batch && b.topology.kind == BlockTopology::Erasure) {
+                std::lock_guard<std::mutex> lock(b.st_->buf_mu);   // on_batch reads the buffer unlocked
+                on_batch(std::vector<size_t>{i});
+            }
+        });
+        last_load.blocks = rebuilt.load();
+        last_load.total_s = now_s() - t0;
+        for (auto& r : results)
+            if (r) return r;
+        return std::nullopt;
+    }
     std::map<std::tuple<unsigned, unsigned, size_t>, Group> groups;
     std::vector<size_t> others;
     for (size_t i : block_indices) {

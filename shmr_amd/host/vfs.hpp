@@ -166,7 +166,9 @@ private:
     friend class VirtualFile;
     struct State;
     Status open_handles() const;
-    Status load_block() const;
+    Status load_block() const { return load_block(nullptr, 0); }
+    // *reconstructed (if set): an Erasure block needed a reconstruct (on `device`)
+    Status load_block(bool* reconstructed, int device) const;
     size_t shard_size() const;   // S of an Erasure block (mod.rs:16-18)
     std::shared_ptr<State> st_;
     std::shared_ptr<const ShmrFsConfig> cfg_;
@@ -215,8 +217,11 @@ public:
     // batched).  Otherwise Erasure blocks with the same (k, p, S) are encoded
     // in pipelined batched GPU calls, their k+p shard files written in parallel.
     Status sync_data(bool force);
-    // Loads every listed block that is not buffered; Erasure blocks with
-    // erasures are reconstructed in one batched GPU call per (k, p, S).
+    // Loads every listed block that is not buffered.  Mapped Block-Cache
+    // buffers (auto batching): one load task per block on the worker pool
+    // (shard reads, then a zero-copy reconstruct on devices[i % n] if needed).
+    // Otherwise Erasure blocks with erasures are reconstructed in batched GPU
+    // calls per (k, p, S), pipelined against the shard-file reads.
     // on_batch, if set, is called on a helper thread with the Erasure blocks of
     // each pipeline batch as soon as they are loaded (while later batches load);
     // it may read those blocks' buffers without locking -- load_blocks holds
