@@ -9,11 +9,12 @@
 // file into its slot and reconstructs in place.  With VfsOptions::pinned_buffers
 // the allocation is mapped host memory (shmr_ec_host_alloc) that the GPU kernels
 // read and write in place across PCIe (zero-copy, no staging).
-// VirtualFile::sync_data / read batch every Erasure block of the operation into
-// one pipelined multi-GPU call (shmr_ec_encode_blocks_host /
-// shmr_ec_reconstruct_blocks_host) and fan the shard-file I/O out over a
-// thread pool (parallel pwrite+fsync, row 3).  Deviations from the reference
-// are opt-in (VfsOptions).
+// VirtualFile::sync_data / read fan the work out over a persistent worker pool:
+// with mapped buffers one task per block (zero-copy encode / reconstruct on
+// GPU devices[i % n] plus its shard-file I/O); with pageable buffers the Erasure
+// blocks go into pipelined multi-GPU batch calls (shmr_ec_encode_blocks_host /
+// shmr_ec_reconstruct_blocks_host) against parallel pwrite+fsync / reads
+// (row 3).  Deviations from the reference are opt-in (VfsOptions).
 #pragma once
 
 #include <cstdint>
