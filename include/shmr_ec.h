@@ -183,14 +183,12 @@ int shmr_ec_set_device(shmr_ec_t* rs, int device);
  * register budget for that many waves per SIMD), "early" (0/1: issue the
  * first data loads before the plan's LDS staging completes), "spre" (0/1:
  * coefficient tables and shard offsets by scalar loads one shard ahead, no
- * LDS), "xcd" (0/1: XCD-grouped tile order -- workgroup w takes tile
- * (w % 8) * (ntiles / 8) + w / 8, so each XCD streams one contiguous eighth of
- * the batch), "fuse_tail" (0/1: a shard length that is not a multiple of the
+ * LDS), "fuse_tail" (0/1: a shard length that is not a multiple of the
  * tile runs the partial last tile of every block at the head of the full-tile
  * launch instead of in a second launch), "diag" (0/1:
  * XOR-only diagnostic kernel, WRONG results, for ceiling measurements).
  * Prefix "encode." or "decode." to set one operation class only.
- * "chunks", "nt_load", "nt_store", "depth", "occ", "early", "spre", "xcd" and "fuse_tail" default to -2 (auto): a per-shape policy
+ * "chunks", "nt_load", "nt_store", "depth", "occ", "early", "spre" and "fuse_tail" default to -2 (auto): a per-shape policy
  * of the fastest variants measured on MI355X; any other value pins the knob,
  * and setting -2 returns it to the policy. */
 int shmr_ec_set_tuning(const char* key, int value);

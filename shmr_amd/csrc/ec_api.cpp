@@ -131,9 +131,9 @@ int shmr_ec_describe_variant(int decode, uint32_t data_shards, uint32_t rows, ch
     const bool compiled = shmr::kern::variant_compiled(lean) && (!v.fuse_tail || shmr::kern::variant_compiled(v));
     std::snprintf(buf, len,
                   "chunks=%d nt_load=%d nt_store=%d scalar_tabs=%d occ8=%d threads=%d grid=%d diag=%d depth=%d "
-                  "wgs_per_cu=%d occ=%d early=%d spre=%d xcd=%d fuse_tail=%d compiled=%d",
+                  "wgs_per_cu=%d occ=%d early=%d spre=%d fuse_tail=%d compiled=%d",
                   v.u, int(v.nt_load), int(v.nt_store), int(v.scalar_tabs), int(v.occ8), v.threads,
-                  core::grid_mode(op), int(v.diag), v.depth, v.wgs_per_cu, v.occ, int(v.early), int(v.spre), int(v.xcd), int(v.fuse_tail),
+                  core::grid_mode(op), int(v.diag), v.depth, v.wgs_per_cu, v.occ, int(v.early), int(v.spre), int(v.fuse_tail),
                   int(compiled));
     return SHMR_EC_OK;
 }

@@ -29,7 +29,6 @@ struct Tuning {
     std::atomic<int> occ{kAuto};
     std::atomic<int> early{kAuto};
     std::atomic<int> spre{kAuto};
-    std::atomic<int> xcd{kAuto};
     std::atomic<int> fuse_tail{kAuto};
 };
 Tuning g_tune[2];   // [kEncode], [kDecode]
@@ -44,8 +43,9 @@ Tuning g_tune[2];   // [kEncode], [kDecode]
 // (short-lived workgroups) issue their first data loads ahead of the plan
 // staging ("early": RS(4,2) 83 % vs 80 %; neutral at k = 8, -2 % on decode).
 // Scalar-loaded tables ("spre", 7-8 waves/SIMD) lose 3-6 % everywhere.
-// XCD-grouped tile order ("xcd") is within +-2 % (RS(8,3) +0.5 %, RS(4,2)
-// -2 %): off.  Shard lengths that are not a multiple of the tile (RS(10,4):
+// An XCD-grouped tile order (workgroup w -> tile (w % 8) * n/8 + w / 8, each
+// XCD streaming one contiguous eighth) measured within +-2 % and was dropped.
+// Shard lengths that are not a multiple of the tile (RS(10,4):
 // S = 1,677,722) run each block's partial last tile at the HEAD of the
 // full-tile grid ("fuse_tail"): 5.5-5.8 % less time than a second launch of
 // 64 latency-bound workgroups after the full tiles.  Placed at each block's
@@ -125,8 +125,6 @@ int set_tuning(const char* key, int value) {
             T.early = value == kAuto ? kAuto : (value != 0);
         } else if (k == "spre") {
             T.spre = value == kAuto ? kAuto : (value != 0);
-        } else if (k == "xcd") {
-            T.xcd = value == kAuto ? kAuto : (value != 0);
         } else if (k == "fuse_tail") {
             T.fuse_tail = value == kAuto ? kAuto : (value != 0);
         } else {
@@ -154,7 +152,6 @@ int get_tuning(const char* key) {
     if (k == "occ") return T.occ;
     if (k == "early") return T.early;
     if (k == "spre") return T.spre;
-    if (k == "xcd") return T.xcd;
     if (k == "fuse_tail") return T.fuse_tail;
     return SHMR_EC_INVALID_ARGUMENT;
 }
@@ -174,12 +171,37 @@ kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_m
     if (T.occ.load() != kAuto) v.occ = T.occ.load();
     if (T.early.load() != kAuto) v.early = T.early.load() != 0;
     if (T.spre.load() != kAuto) v.spre = T.spre.load() != 0;
-    if (T.xcd.load() != kAuto) v.xcd = T.xcd.load() != 0;
     if (T.fuse_tail.load() != kAuto) v.fuse_tail = T.fuse_tail.load() != 0;
     return v;
 }
 
 int grid_mode(OpClass op) { return g_tune[op].grid.load(); }
+
+kern::Variant launch_variant(OpClass op, unsigned k, unsigned rows, bool host_mapped, bool ptrs, bool segs) {
+    kern::Variant v = resolve_variant(op, k, rows, host_mapped);
+    v.ptrs = ptrs;
+    v.segs = segs;
+    if (ptrs) {
+        v.early = v.spre = v.scalar_tabs = false;   // only the plain LDS-staged tile reads pointer tables
+        kern::Variant lean = v;
+        lean.fuse_tail = false;
+        if (!kern::variant_compiled(lean)) {   // tuned knobs without a pointer-table build: the mapped policy
+            v = variant_policy(op, k, rows, true);
+            v.ptrs = true;
+            v.segs = segs;
+        }
+    }
+    return v;
+}
+
+bool segs_supported(OpClass op, unsigned k, bool host_mapped, bool ptrs) {
+    for (unsigned rows : {1u, kern::kMaxRowsPerLaunch}) {
+        kern::Variant v = launch_variant(op, k, rows, host_mapped, ptrs, true);
+        v.fuse_tail = false;
+        if (!kern::variant_compiled(v)) return false;
+    }
+    return true;
+}
 
 // ===========================================================================
 // Devices and plans
@@ -248,12 +270,7 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
                                     aligned16(L.out_spitch);
     for (uint32_t row0 = 0; row0 < plan.m; row0 += kern::kMaxRowsPerLaunch) {
         const uint32_t rows = std::min<uint32_t>(kern::kMaxRowsPerLaunch, plan.m - row0);
-        kern::Variant var = resolve_variant(op, plan.k, rows, L.host_mapped);
-        if (ptrs) {   // only the plain LDS-staged tile reads a shard-pointer table
-            var.early = false;
-            var.spre = false;
-            var.scalar_tabs = false;
-        }
+        kern::Variant var = launch_variant(op, plan.k, rows, L.host_mapped, ptrs, bs.segs != nullptr);
         const uint64_t tb = kern::tile_bytes(var.u, var.threads);
         kern::ApplyArgs a{};
         a.in_base = L.in_base;
@@ -399,7 +416,7 @@ int reconstruct_on_device(Codec& c, int dev, const Layout& L, const uint8_t* pre
         // no dependent table loads in the kernel prologue.
         {
             std::vector<kern::Seg> segs;
-            bool fits = true;
+            bool fits = segs_supported(kDecode, c.k(), L.host_mapped, L.d_ptrs != nullptr);
             for (size_t i = 0; i < grp.blocks.size() && fits;) {
                 size_t e = i + 1;
                 const uint32_t st = e < grp.blocks.size() ? grp.blocks[e] - grp.blocks[i] : 1;

@@ -37,6 +37,11 @@ constexpr int kAuto = -2;
 int set_tuning(const char* key, int value);
 int get_tuning(const char* key);
 kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_mapped = false);
+// The full-tile variant a launch uses: resolve_variant plus the launch form
+// (shard-pointer tables, segment table), which selects its own instantiation.
+kern::Variant launch_variant(OpClass op, unsigned k, unsigned rows, bool host_mapped, bool ptrs, bool segs);
+// Whether segment launches are compiled for this op's current tuning.
+bool segs_supported(OpClass op, unsigned k, bool host_mapped, bool ptrs);
 int grid_mode(OpClass op);
 
 // ---- devices --------------------------------------------------------------

@@ -51,6 +51,21 @@ constexpr int kEarly = 1 << 16;  // first data loads issued before the plan's LD
 constexpr int kSPre = 1 << 17;   // tables + offsets by scalar loads one shard ahead, no LDS
 constexpr int kFuse = 1 << 18;   // leading partial tiles (ApplyArgs::lead_tails) in a MODE 0 launch; a
                                  // separate instantiation: the bounds-checked path costs 4-7 VGPRs
+// Launch forms a full-tile (MODE 0) kernel supports only when compiled with
+// the flag, so the lean encode kernel carries none of their code (measured:
+// the runtime checks alone cost the RS(8,3) encode 1.3 %).  The tail and
+// byte-granular kernels (MODE 1, 2) always support both.
+constexpr int kPtrs = 1 << 19;   // shard-pointer tables (ApplyArgs::shard_ptrs)
+constexpr int kSegs = 1 << 20;   // segment launches (ApplyArgs::segs)
+
+template <int MODE, int F>
+constexpr bool has_ptrs() {
+    return MODE != 0 || (F & kPtrs) != 0;
+}
+template <int MODE, int F>
+constexpr bool has_segs() {
+    return MODE != 0 || (F & kSegs) != 0;
+}
 // Bits 12-15: occupancy target in waves per SIMD (0 = compiler's choice);
 // the register allocator must then fit 512 / target VGPRs.
 constexpr int kOccShift = 12;
@@ -289,7 +304,7 @@ __device__ __forceinline__ void do_tile(const ApplyArgs& a, const Ctx& c, const 
 
 // Stages rows [row0, row0 + R) of a plan image into LDS:
 // [tables k*R*32 B][in_off k*8 B][out_off R*8 B].
-template <int R, int TH>
+template <int R, int TH, bool PTRS>
 __device__ __forceinline__ void stage_plan(const ApplyArgs& a, const uint8_t* plan, uint8_t* smem, Ctx& c,
                                            uint64_t blk) {
     const uint32_t k = a.k;
@@ -306,7 +321,7 @@ __device__ __forceinline__ void stage_plan(const ApplyArgs& a, const uint8_t* pl
         const uint32_t t = e / R, r = e - t * R;
         s_tab[i] = ptab[(size_t(t) * a.m + a.row0 + r) * 2 + half];
     }
-    if (a.shard_ptrs) {   // absolute shard addresses (in/out bases are 0)
+    if (PTRS && a.shard_ptrs) {   // absolute shard addresses (in/out bases are 0)
         const uint64_t* bp = a.shard_ptrs + blk * a.total;
         for (uint32_t t = threadIdx.x; t < k; t += TH) s_in_off[t] = bp[c.g_in_idx[t]];
         for (uint32_t r = threadIdx.x; r < uint32_t(R); r += TH) s_out_off[r] = bp[c.g_out_idx[a.row0 + r]];
@@ -533,12 +548,6 @@ __device__ __forceinline__ void spre_tile(const ApplyArgs& a, const uint8_t* pla
     }
 }
 
-__device__ __forceinline__ uint64_t first_tile(const ApplyArgs& a) {
-    const uint64_t w = blockIdx.x;
-    if (a.xcd_q != 0 && w < 8 * a.xcd_q) return (w & 7) * a.xcd_q + (w >> 3);
-    return w;
-}
-
 // Block index and plan of launch block j of a segment launch: binary search
 // over the (kernel-argument, wave-uniform) segment table -- scalar loads.
 __device__ __forceinline__ uint64_t seg_block(const ApplyArgs& a, uint64_t j, const uint8_t** plan) {
@@ -580,12 +589,12 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
     if constexpr ((F & (kEarly | kSPre)) != 0) {
         const uint64_t tb = uint64_t(TH) * 16 * U;
         bool first = true;
-        for (uint64_t tile = first_tile(a); tile < a.ntiles; tile += gridDim.x) {
+        for (uint64_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
             const TileRef tr = tile_ref<F>(a, tile);
             const uint64_t j = tr.j, cc = tr.cc;
             uint64_t blk;
             const uint8_t* plan = a.plan;
-            if (a.nseg) {
+            if (has_segs<MODE, F>() && a.nseg) {
                 blk = seg_block(a, j, &plan);
             } else {
                 blk = a.blk_list ? uint64_t(as_const<cu32>(a.blk_list)[j]) : a.blk_first + j * a.blk_stride;
@@ -617,11 +626,12 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
         return;
     }
     // Multi-plan, segment and shard-pointer launches restage per tile.
-    const bool restage = multi || a.nseg != 0 || a.shard_ptrs != nullptr;
+    constexpr bool PTRS = has_ptrs<MODE, F>(), SEGS = has_segs<MODE, F>();
+    const bool restage = multi || (SEGS && a.nseg != 0) || (PTRS && a.shard_ptrs != nullptr);
     Ctx c{};
     if (!restage) {
         if constexpr (kLds) {
-            stage_plan<R, TH>(a, a.plan, smem, c, 0);
+            stage_plan<R, TH, PTRS>(a, a.plan, smem, c, 0);
             __syncthreads();
         } else {
             c.g_in_idx = reinterpret_cast<const uint16_t*>(a.plan + 8);
@@ -630,12 +640,12 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
         }
     }
     const uint64_t tb = uint64_t(TH) * 16 * U;
-    for (uint64_t tile = first_tile(a); tile < a.ntiles; tile += gridDim.x) {
+    for (uint64_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
         const TileRef tr = tile_ref<F>(a, tile);
         const uint64_t j = tr.j, cc = tr.cc;
         const uint8_t* plan = a.plan;
         uint64_t blk;
-        if (a.nseg) {
+        if (SEGS && a.nseg) {
             blk = seg_block(a, j, &plan);
         } else {
             blk = a.blk_list ? uint64_t(a.blk_list[j]) : a.blk_first + j * a.blk_stride;
@@ -644,7 +654,7 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
         if (restage) {
             if constexpr (kLds) {
                 __syncthreads();   // previous tile's LDS reads are done
-                stage_plan<R, TH>(a, plan, smem, c, blk);
+                stage_plan<R, TH, PTRS>(a, plan, smem, c, blk);
                 __syncthreads();
             } else {
                 c.g_in_idx = reinterpret_cast<const uint16_t*>(plan + 8);
@@ -697,9 +707,7 @@ hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStr
     }
     if (grid > a.ntiles) grid = a.ntiles;
     if (grid == 0) return hipSuccess;
-    ApplyArgs la = a;
-    la.xcd_q = (v.xcd && grid == a.ntiles) ? a.ntiles / 8 : 0;
-    hipLaunchKernelGGL(kern, dim3(uint32_t(grid)), dim3(threads_of<F>()), lds, stream, la);
+    hipLaunchKernelGGL(kern, dim3(uint32_t(grid)), dim3(threads_of<F>()), lds, stream, a);
     return hipGetLastError();
 }
 
@@ -751,15 +759,24 @@ hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStr
     X(2, kNtLoad | kNtStore | kDepth2 | kFuse) \
     X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse) \
     X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse) \
-    X(1, kNtStore | kDepth2 | kFuse) \
-    X(2, kNtStore | kDepth2 | kFuse)
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse) \
+    X(1, kNtStore | kDepth2 | kPtrs) \
+    X(2, kNtStore | kDepth2 | kPtrs) \
+    X(1, kNtStore | kDepth2 | kPtrs | kFuse) \
+    X(2, kNtStore | kDepth2 | kPtrs | kFuse) \
+    X(1, kNtStore | kDepth2 | kPtrs | kSegs) \
+    X(1, kNtStore | kDepth2 | kPtrs | kSegs | kFuse) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kPtrs) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kPtrs)
 
 int variant_flags(const Variant& v) {
     return (v.nt_load ? kNtLoad : 0) | (v.nt_store ? kNtStore : 0) | (v.scalar_tabs ? kScalarTabs : 0) |
            (v.occ8 ? kOcc8 : 0) | (v.diag ? kDiagXor : 0) | (v.threads == 128 ? kTh128 : 0) |
            (v.threads == 512 ? kTh512 : 0) | (v.depth == 5 ? kDepth5 : 0) | (v.depth == 9 ? kDepth9 : 0) |
            (v.depth == 2 ? kDepth2 : 0) | (v.depth == 1 ? kDepth1 : 0) | ((v.occ & 15) << kOccShift) |
-           (v.early ? kEarly : 0) | (v.spre ? kSPre : 0) | (v.fuse_tail ? kFuse : 0);
+           (v.early ? kEarly : 0) | (v.spre ? kSPre : 0) | (v.fuse_tail ? kFuse : 0) | (v.ptrs ? kPtrs : 0) |
+           (v.segs ? kSegs : 0);
 }
 
 template <int R>

@@ -17,7 +17,10 @@ constexpr unsigned kMaxRowsPerLaunch = 4;
 // Multi-plan launches described in the kernel arguments (no table upload):
 // launch blocks j in [start, start + count) of a segment are blocks
 // first + (j - start) * stride, all using `plan` (a device plan image).
-constexpr unsigned kMaxSegs = 32;
+#ifndef SHMR_MAX_SEGS
+#define SHMR_MAX_SEGS 32
+#endif
+constexpr unsigned kMaxSegs = SHMR_MAX_SEGS;
 struct Seg {
     uint32_t start;
     uint32_t first;
@@ -59,12 +62,6 @@ struct ApplyArgs {
     // plain LDS-staged tile supports it (no early / spre / scalar_tabs).
     const uint64_t* shard_ptrs;
     uint32_t total;
-    // XCD-grouped tile order (one-workgroup-per-tile launches only): the
-    // dispatcher deals workgroup IDs round-robin over the 8 XCDs, so with
-    // xcd_q = ntiles / 8 > 0 workgroup w takes tile (w % 8) * xcd_q + w / 8 and
-    // every XCD streams one contiguous eighth of the batch (tiles >= 8 * xcd_q
-    // keep their own index).  0 = tile w.
-    uint64_t xcd_q;
     // Fused tails (kernels compiled with the fused-tail flag): the first
     // lead_tails tiles of the grid are the partial last tiles of blocks
     // j = 0 .. lead_tails-1 (column col_base + tiles_per_block * tile bytes),
@@ -91,8 +88,9 @@ struct Variant {
     int occ = 0;             // > 0: register budget for this many waves per SIMD (6, 7)
     bool early = false;      // first data loads before the plan's LDS staging completes
     bool spre = false;       // tables/offsets by scalar loads one shard ahead (no LDS)
-    bool xcd = false;        // XCD-grouped tile order (ApplyArgs::xcd_q)
     bool fuse_tail = false;  // partial last tiles inside the full-tile launch (ApplyArgs::lead_tails)
+    bool ptrs = false;       // full-tile kernel that reads shard-pointer tables (set by launch_set)
+    bool segs = false;       // full-tile kernel that takes segment launches (set by launch_set)
 };
 
 // rows in [1, kMaxRowsPerLaunch].  mode 0: full tiles, every shard base
