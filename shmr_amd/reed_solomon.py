@@ -261,8 +261,13 @@ class PinnedBuffer:
 def host_register(arr: np.ndarray) -> None:
     """Page-lock and map an existing C-contiguous host array for zero-copy
     use by the host-buffer entry points (shmr_ec_host_register)."""
-    a = _writable_u8(arr.reshape(-1).view(np.uint8))
-    _check(lib().shmr_ec_host_register(ctypes.c_void_p(a.ctypes.data), a.nbytes))
+    # Register the array's own memory: a reshape of a non-contiguous array would
+    # be a temporary copy, whose registration would outlive it.
+    if not isinstance(arr, np.ndarray) or not arr.flags["C_CONTIGUOUS"] or not arr.flags["WRITEABLE"]:
+        raise TypeError("host_register needs a writable C-contiguous numpy array")
+    if arr.nbytes == 0:
+        raise ValueError("host_register needs a non-empty array")
+    _check(lib().shmr_ec_host_register(ctypes.c_void_p(arr.ctypes.data), arr.nbytes))
 
 
 def host_unregister(arr: np.ndarray) -> None:

@@ -226,3 +226,22 @@ def test_native_library_is_required():
     finally:
         _native.LIB_PATH = saved
         _native._lib = keep
+
+
+def test_host_register_rejects_non_contiguous():
+    """A non-contiguous array would be registered through a temporary copy;
+    the shim refuses it before any device call (no GPU needed)."""
+    a = np.zeros((8, 8), np.uint8)[:, ::2]
+    with pytest.raises(TypeError):
+        shmr_amd.host_register(a)
+    ro = np.zeros(16, np.uint8)
+    ro.flags.writeable = False
+    with pytest.raises(TypeError):
+        shmr_amd.host_register(ro)
+    with pytest.raises(ValueError):
+        shmr_amd.host_register(np.zeros(0, np.uint8))
+
+
+def test_path_stats_api():
+    z, s = shmr_amd.path_stats()
+    assert z >= 0 and s >= 0
