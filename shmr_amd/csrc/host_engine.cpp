@@ -191,6 +191,9 @@ struct MappedRange {
     size_t bytes;
     uintptr_t dev;
 };
+// Zero-copy takes a range only when its device address equals its host
+// address (unified addressing: then it is the same on every GPU of the node);
+// otherwise the range stays registered (pinned, DMA'd) but is staged.
 std::mutex g_mapped_mu;
 std::map<uintptr_t, MappedRange>& mapped_ranges() {
     static auto* m = new std::map<uintptr_t, MappedRange>;   // leaked: outlives static teardown
@@ -237,6 +240,7 @@ bool translate_locked(const void* p, size_t len, uint64_t* dev, std::map<uintptr
         if (!inside(it)) return false;
         *hint = it;
     }
+    if ((*hint)->second.dev != (*hint)->first) return false;
     *dev = uint64_t((*hint)->second.dev + (a - (*hint)->first));
     return true;
 }
