@@ -451,3 +451,38 @@ def test_reconstruct_segments_irregular_runs(gpu):
     shmr_amd.ReedSolomon(k, p).reconstruct_batch_dev(dev, present, shard_len=S)
     torch.cuda.synchronize()
     assert np.array_equal(dev.cpu().numpy()[:, :, :S], host[:, :, :S])
+
+
+def test_roundtrip_full_size_104(gpu):
+    """BASELINE config 4 at its full per-GPU size (64 x 16 MiB RS(10,4) blocks,
+    S = 1,677,722, pitched): encode -> erase {b mod 10, (b+3) mod 10} (the bench
+    pattern) plus every parity shard of every 7th block (4 erasures, the most the
+    code allows) -> reconstruct == original; one block's parity vs the oracle."""
+    import torch
+    k, p, B = 10, 4, 64
+    S = shmr_amd.calculate_shard_size(16 << 20, k)
+    pitch = (S + 255) // 256 * 256
+    g = torch.Generator(device=gpu)
+    g.manual_seed(104)
+    shards = torch.zeros((B, k + p, pitch), dtype=torch.uint8, device=gpu)
+    shards[:, :k, :S] = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=gpu, generator=g)
+    rs = shmr_amd.ReedSolomon(k, p)
+    rs.encode_batch_dev(shards[:, :k], shards[:, k:], shard_len=S, data_shard_pitch=pitch, parity_shard_pitch=pitch)
+    ref = shards.clone()
+    present = np.ones((B, k + p), np.uint8)
+    b = np.arange(B)
+    present[b, b % 10] = 0
+    present[b, (b + 3) % 10] = 0
+    present[::7] = 1
+    present[::7, k:] = 0
+    for i in range(B):
+        for s in range(k + p):
+            if not present[i, s]:
+                shards[i, s, :S] = 0xEE
+    rs.reconstruct_batch_dev(shards, present, shard_len=S)
+    torch.cuda.synchronize()
+    assert torch.equal(shards[:, :, :S], ref[:, :, :S])
+    hd = ref[5].cpu().numpy()
+    par = oracle_parity(k, p, [hd[i, :S].copy() for i in range(k)])
+    for r in range(p):
+        assert np.array_equal(hd[k + r, :S], par[r])
