@@ -212,6 +212,21 @@ class ReedSolomon:
 
     def _host_ptrs(self, blocks):
         t = self.total_shard_count()
+        if isinstance(blocks, np.ndarray):
+            # [B, total, S] array (e.g. a Block Cache slab): shard pointers computed
+            # in one vectorised step instead of B * total Python views
+            if blocks.ndim != 3 or blocks.dtype != np.uint8 or blocks.strides[2] != 1:
+                raise TypeError("blocks array must be uint8 [nblocks, total, shard_len], shard bytes contiguous")
+            if not blocks.flags["WRITEABLE"]:
+                raise TypeError("blocks array must be writable")
+            if blocks.shape[1] != t:
+                raise Error(-1 if blocks.shape[1] < t else -2)
+            B, _, L = blocks.shape
+            base = blocks.ctypes.data
+            ptrs = (np.uint64(base) + np.arange(B, dtype=np.uint64)[:, None] * np.uint64(blocks.strides[0])
+                    + np.arange(t, dtype=np.uint64)[None, :] * np.uint64(blocks.strides[1])).reshape(-1)
+            ptrs = np.ascontiguousarray(ptrs)
+            return (blocks, ptrs), L, ptrs.ctypes.data_as(ctypes.POINTER(_u8p))
         arrs = [[(None if s is None else _writable_u8(s)) for s in blk] for blk in blocks]
         for blk in arrs:
             if len(blk) != t:
@@ -221,22 +236,28 @@ class ReedSolomon:
         ptrs = (_u8p * max(len(flat), 1))(*[(_ptr(a) if a is not None else _u8p()) for a in flat])
         return arrs, L, ptrs
 
-    def encode_blocks_host(self, blocks: Sequence[Sequence[np.ndarray]], devices: Sequence[int] = (0,)) -> None:
-        """Encode many host-resident blocks (each a list of total shards; parity
-        overwritten), whole blocks round-robin over devices, pipelined."""
-        arrs, L, ptrs = self._host_ptrs(blocks)
+    def encode_blocks_host(self, blocks, devices: Sequence[int] = (0,)) -> None:
+        """Encode many host-resident blocks, whole blocks round-robin over
+        devices.  blocks: a list of per-block shard lists, or one uint8 array
+        [nblocks, total, shard_len] (parity rows overwritten)."""
+        keep, L, ptrs = self._host_ptrs(blocks)
+        n = len(blocks)
         devs = (ctypes.c_int * len(devices))(*devices)
-        _check(lib().shmr_ec_encode_blocks_host(self._h, ptrs, len(arrs), L, devs, len(devices)))
+        _check(lib().shmr_ec_encode_blocks_host(self._h, ptrs, n, L, devs, len(devices)))
+        del keep
 
-    def reconstruct_blocks_host(self, blocks: Sequence[Sequence[np.ndarray]], present, data_only: bool = False,
+    def reconstruct_blocks_host(self, blocks, present, data_only: bool = False,
                                 devices: Sequence[int] = (0,)) -> None:
-        """Rebuild absent shards of many host-resident blocks in place.
-        present: [nblocks][total] flags; absent shards need (writable) buffers."""
-        arrs, L, ptrs = self._host_ptrs(blocks)
-        pr = np.ascontiguousarray(present, dtype=np.uint8).reshape(len(arrs), self.total_shard_count())
+        """Rebuild absent shards of many host-resident blocks in place (blocks as
+        for encode_blocks_host).  present: [nblocks][total] flags; absent shards
+        need (writable) buffers."""
+        keep, L, ptrs = self._host_ptrs(blocks)
+        n = len(blocks)
+        pr = np.ascontiguousarray(present, dtype=np.uint8).reshape(n, self.total_shard_count())
         devs = (ctypes.c_int * len(devices))(*devices)
-        _check(lib().shmr_ec_reconstruct_blocks_host(self._h, ptrs, _ptr(pr), len(arrs), L, int(data_only), devs,
+        _check(lib().shmr_ec_reconstruct_blocks_host(self._h, ptrs, _ptr(pr), n, L, int(data_only), devs,
                                                      len(devices)))
+        del keep
 
 
 class PinnedBuffer:

@@ -75,3 +75,37 @@ def test_reconstruct_blocks_host_validates_first(gpu):
     with pytest.raises(shmr_amd.Error) as e:
         shmr_amd.ReedSolomon(k, p).reconstruct_blocks_host(blocks, present, devices=[0])
     assert e.value.name == "TooFewShardsPresent"
+
+
+@pytest.mark.parametrize("mapped", [False, True])
+def test_blocks_host_array_form(gpu, mapped):
+    """encode/reconstruct_blocks_host on one [B, total, S] array (vectorised
+    pointer marshalling), pageable and mapped, bit-exact vs the oracle."""
+    k, p, S, B = 8, 3, 65536 + 4, 7
+    rng = np.random.default_rng(31)
+    keep = None
+    if mapped:
+        keep = shmr_amd.PinnedBuffer(B * (k + p) * S)
+        arr = keep.array.reshape(B, k + p, S)
+    else:
+        arr = np.zeros((B, k + p, S), np.uint8)
+    arr[:, :k] = rng.integers(0, 256, (B, k, S), dtype=np.uint8)
+    rs = shmr_amd.ReedSolomon(k, p)
+    z0, s0 = shmr_amd.path_stats()
+    rs.encode_blocks_host(arr)
+    z1, s1 = shmr_amd.path_stats()
+    assert (z1 - z0, s1 - s0) == ((B, 0) if mapped else (0, B))
+    for b in range(B):
+        want = oracle_parity(k, p, [arr[b, i].copy() for i in range(k)])
+        for r in range(p):
+            assert np.array_equal(arr[b, k + r], want[r])
+    full = arr.copy()
+    present = np.ones((B, k + p), np.uint8)
+    for b in range(B):
+        present[b, [b % k, k + (b % p)]] = 0
+        arr[b, b % k] = 0
+        arr[b, k + b % p] = 0
+    rs.reconstruct_blocks_host(arr, present)
+    assert np.array_equal(arr, full)
+    with pytest.raises(TypeError):
+        rs.encode_blocks_host(arr[:, :, ::2])     # shard bytes not contiguous
