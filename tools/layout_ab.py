@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=512)
     ap.add_argument("--rounds", type=int, default=11)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--decode", type=int, default=0, help="erasures per block: time reconstruct instead")
     a = ap.parse_args()
     k, p, B = a.k, a.p, a.blocks
     S = shmr_amd.calculate_shard_size(a.block_mib << 20, k)
@@ -46,11 +47,26 @@ def main():
     Q = P + 4096 + 256   # padded pitch: breaks the power-of-two shard stride
     pad = torch.empty((B, k + p, Q), dtype=torch.uint8, device=dev)
     pad[:, :k, :P] = sep_d
-    runs = {
+    if a.decode:
+        present = np.ones((B, k + p), np.uint8)
+        b = np.arange(B)
+        for e in range(a.decode):
+            present[b, (b + 3 * e) % k] = 0
+        rs.encode_batch_dev(blk[:, :k], blk[:, k:], shard_len=S)
+        rs.encode_batch_dev(pad[:, :k], pad[:, k:], shard_len=S)
+        runs = {f"decode_pitch_{P}": lambda: rs.reconstruct_batch_dev(blk, present, shard_len=S),
+                f"decode_pitch_{Q}": lambda: rs.reconstruct_batch_dev(pad, present, shard_len=S)}
+        for d in (4096, 8192 + 256, 65536 + 256):
+            t = torch.empty((B, k + p, P + d), dtype=torch.uint8, device=dev)
+            t[:, :, :P] = blk
+            runs[f"decode_pitch_{P + d}"] = (lambda t=t: rs.reconstruct_batch_dev(t, present, shard_len=S))
+    else:
+        runs = {}
+    runs.update({} if a.decode else {
         "separate": lambda: rs.encode_batch_dev(sep_d, sep_p, shard_len=S),
         "block_buffer": lambda: rs.encode_batch_dev(blk[:, :k], blk[:, k:], shard_len=S),
         "block_buffer_padded": lambda: rs.encode_batch_dev(pad[:, :k], pad[:, k:], shard_len=S),
-    }
+    })
     st = torch.cuda.current_stream()
     for r in runs.values():
         for _ in range(50):
@@ -66,8 +82,9 @@ def main():
             e1.record(st)
             torch.cuda.synchronize()
             times[n].append(e0.elapsed_time(e1) / a.iters)
-    assert torch.equal(blk[:, k:, :S], sep_p[:, :, :S]) and torch.equal(pad[:, k:, :S], sep_p[:, :, :S])
-    algo = B * (k + p) * S
+    if not a.decode:
+        assert torch.equal(blk[:, k:, :S], sep_p[:, :, :S]) and torch.equal(pad[:, k:, :S], sep_p[:, :, :S])
+    algo = B * ((k + a.decode) if a.decode else (k + p)) * S
     for n, ts in times.items():
         med = float(np.median(ts))
         print(json.dumps({"layout": n, "k": k, "p": p, "S": S, "median_ms": round(med, 4),
