@@ -501,18 +501,23 @@ UploadRing* UploadRing::for_device(int dev, int* rc, Kind kind) {
     auto& r = (*rings)[{dev, int(kind)}];
     if (!r) {
         auto* ring = new UploadRing;
+        // on failure nothing is kept: the next call retries from scratch
+        auto give_up = [&](int code) -> UploadRing* {
+            for (int i = 0; i < kSlots; ++i)
+                if (ring->ev_[i]) (void)hipEventDestroy(ring->ev_[i]);
+            if (ring->dev_) (void)hipFree(ring->dev_);
+            if (ring->host_) (void)hipHostFree(ring->host_);
+            delete ring;
+            *rc = code;
+            return nullptr;
+        };
         if (hipHostMalloc(reinterpret_cast<void**>(&ring->host_), kSlots * kSlotBytes, hipHostMallocDefault) !=
                 hipSuccess ||
-            hipMalloc(reinterpret_cast<void**>(&ring->dev_), kSlots * kSlotBytes) != hipSuccess) {
-            *rc = SHMR_EC_OUT_OF_MEMORY;
-            return nullptr;
-        }
-        for (int i = 0; i < kSlots; ++i) {
-            if (hipEventCreateWithFlags(&ring->ev_[i], hipEventDisableTiming) != hipSuccess) {
-                *rc = SHMR_EC_DEVICE_ERROR;
-                return nullptr;
-            }
-        }
+            hipMalloc(reinterpret_cast<void**>(&ring->dev_), kSlots * kSlotBytes) != hipSuccess)
+            return give_up(SHMR_EC_OUT_OF_MEMORY);
+        for (int i = 0; i < kSlots; ++i)
+            if (hipEventCreateWithFlags(&ring->ev_[i], hipEventDisableTiming) != hipSuccess)
+                return give_up(SHMR_EC_DEVICE_ERROR);
         r = ring;
     }
     *rc = SHMR_EC_OK;
