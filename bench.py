@@ -210,8 +210,11 @@ def main():
         },
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu and erasures is None:
-        out["cpu_baseline"] = cpu_baseline(k, p, S, data, parity, args.cpu_seconds)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        if erasures is None:
+            out["cpu_baseline"] = cpu_baseline(k, p, S, block_bytes, data, parity, args.cpu_seconds)
+        else:
+            out["cpu_baseline"] = cpu_baseline_decode(k, p, S, shards, present, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -242,7 +245,7 @@ def cpu_model() -> str:
     return platform.processor() or platform.machine()
 
 
-def cpu_baseline(k, p, S, data_t, parity_t, budget_s):
+def cpu_baseline(k, p, S, block_bytes, data_t, parity_t, budget_s):
     """CPU restatement of the crate's simd_c AVX2 loop (oracle/, "port"),
     one block per thread as rayon does over VirtualFile blocks; bounded sample
     of the same workload; also checks the GPU parity of the sampled blocks."""
@@ -259,6 +262,19 @@ def cpu_baseline(k, p, S, data_t, parity_t, budget_s):
     ok = bool(np.array_equal(gpu_par, host_par))
     gib = nb * k * S * reps / secs / 2 ** 30
     single = c_oracle.encode_batch(k, p, host_data[: k * S], host_par[: p * S], 1, S, 1, variant=1)
+    # the whole VirtualBlock::sync_data Erasure arm minus disk I/O (block.rs:406-430):
+    # chunks(S).to_vec() copies, zero pad, zero shards, encode, per block
+    ns = min(nb, max(1, (256 << 20) // block_bytes))
+    src = np.zeros(ns * block_bytes, np.uint8)
+    for b in range(ns):
+        n = min(k * S, block_bytes)
+        src[b * block_bytes:b * block_bytes + n] = host_data[b * k * S:b * k * S + n]
+    sync_par = np.zeros(ns * p * S, np.uint8)
+    sreps, ssecs = 0, 0.0
+    while ssecs < budget_s / 3 or sreps == 0:
+        ssecs += c_oracle.sync_data_batch(k, p, src, block_bytes, S, sync_par, ns, cores)
+        sreps += 1
+    sync_ok = bool(np.array_equal(sync_par, host_par[:ns * p * S])) if block_bytes >= k * S else None
     return {
         "value": round(gib, 3),
         "unit": "GiB/s",
@@ -269,8 +285,45 @@ def cpu_baseline(k, p, S, data_t, parity_t, budget_s):
                   f"(one block per thread, AVX2 nibble-pshufb loop restating reed-solomon-erasure "
                   f"6.0.0 simd_c); encode only (erasure_encode_duration scope, block.rs:425-430)",
         "single_core_GiBps": round(k * S / single / 2 ** 30, 3),
+        "sync_data_GiBps": round(ns * block_bytes * sreps / ssecs / 2 ** 30, 3),
+        "sync_data_sample": f"{ns} blocks x {sreps} reps: chunk to_vec copies + zero pad/shards + encode "
+                            f"per block (block.rs:406-430), {cores} threads",
+        "sync_data_parity_matches": sync_ok,
         "cpu_model": cpu_model(),
         "gpu_parity_bit_exact_on_sample": ok,
+    }
+
+
+def cpu_baseline_decode(k, p, S, shards_t, present, budget_s):
+    """CPU restatement of the crate's reconstruct (first k present shards,
+    inverted sub-matrix, SIMD mul_slice loop; oracle/, "port"), one block per
+    thread; bounded sample of the same decode workload.  The GPU's rebuilt
+    shards of the sampled blocks are checked bit-for-bit against it."""
+    from oracle import c_oracle   # cpu_baseline leg: oracle allowed here only
+    cores = min(16, os.cpu_count() or 1)
+    t = k + p
+    nb = min(shards_t.shape[0], max(1, (1 << 30) // (t * S)))
+    gpu = np.ascontiguousarray(shards_t[:nb, :, :S].cpu().numpy())
+    pr = np.ascontiguousarray(present[:nb], dtype=np.uint8)
+    work = gpu.copy()
+    work[pr == 0] = 0
+    reps, secs = 0, 0.0
+    while secs < budget_s or reps == 0:
+        secs += c_oracle.reconstruct_batch(k, p, work, pr, S, cores)
+        reps += 1
+    ok = bool(np.array_equal(work, gpu))
+    single = c_oracle.reconstruct_batch(k, p, work[:1], pr[:1], S, 1)
+    return {
+        "value": round(nb * k * S * reps / secs / 2 ** 30, 3),
+        "unit": "GiB/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": f"{nb} blocks x {reps} reps of the same decode workload ({secs:.1f} s wall, "
+                  f"~{secs * cores:.0f} core-seconds), {cores} threads (one block per thread; crate reconstruct "
+                  f"restated: inv(M[first k present]) + AVX2 nibble-pshufb mul_slice)",
+        "single_core_GiBps": round(k * S / single / 2 ** 30, 3),
+        "cpu_model": cpu_model(),
+        "gpu_rebuilt_bit_exact_on_sample": ok,
     }
 
 

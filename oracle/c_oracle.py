@@ -52,6 +52,14 @@ def lib():
                                           ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
                                           ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
                                           ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int]
+        L.oracle_reconstruct_batch.restype = ctypes.c_double
+        L.oracle_reconstruct_batch.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                               ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+                                               ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
+        L.oracle_sync_data_batch.restype = ctypes.c_double
+        L.oracle_sync_data_batch.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                             ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+                                             ctypes.c_int]
         L.oracle_has_avx2.restype = ctypes.c_int
         _lib = L
     return _lib
@@ -113,3 +121,30 @@ def encode_batch(k: int, p: int, data: np.ndarray, parity: np.ndarray, nblocks: 
     assert data.size >= nblocks * k * length and parity.size >= nblocks * p * length
     return lib().oracle_encode_batch(variant, k, p, data.ctypes.data, length, k * length,
                                      parity.ctypes.data, length, p * length, nblocks, length, nthreads)
+
+
+def reconstruct_batch(k: int, p: int, shards: np.ndarray, present: np.ndarray, length: int, nthreads: int,
+                      variant: int = 1, data_only: bool = False) -> float:
+    """shards: uint8 [nblocks][k+p][pitch] (absent shards overwritten in place);
+    present: [nblocks][k+p].  Returns seconds (one block per thread task)."""
+    assert shards.ndim == 3 and shards.dtype == np.uint8 and shards.flags["C_CONTIGUOUS"]
+    pr = np.ascontiguousarray(present, dtype=np.uint8)
+    B = shards.shape[0]
+    secs = lib().oracle_reconstruct_batch(variant, k, p, shards.ctypes.data, shards.strides[1], shards.strides[0],
+                                          pr.ctypes.data, B, length, int(data_only), nthreads)
+    if secs < 0:
+        raise ValueError("reconstruct failed")
+    return secs
+
+
+def sync_data_batch(k: int, p: int, src: np.ndarray, size: int, shard: int, parity: np.ndarray, nblocks: int,
+                    nthreads: int, variant: int = 1) -> float:
+    """VirtualBlock::sync_data minus disk (block.rs:406-430) for nblocks
+    size-byte buffers at src + b * size: chunk to_vec copies, zero pad, zero
+    shards, encode.  parity: [nblocks][p][shard] out.  Returns seconds."""
+    assert src.size >= nblocks * size and parity.size >= nblocks * p * shard
+    secs = lib().oracle_sync_data_batch(variant, k, p, src.ctypes.data, size, shard, parity.ctypes.data, nblocks,
+                                        nthreads)
+    if secs < 0:
+        raise ValueError("sync_data batch failed")
+    return secs

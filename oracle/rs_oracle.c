@@ -222,9 +222,21 @@ int oracle_encode(int variant, uint32_t k, uint32_t p, uint8_t* const* shards, s
 /* ReedSolomon::reconstruct{,_data}.  present[i] != 0 marks present shards.
  * Absent shards must point at len-byte buffers; they are filled (absent
  * parity only when !data_only).  returns 0 / -10 (TooFewShardsPresent). */
+static int reconstruct_impl(int variant, uint32_t k, uint32_t p, uint8_t* const* shards, const uint8_t* present,
+                            size_t len, int data_only);
+
 int oracle_reconstruct(uint32_t k, uint32_t p, uint8_t* const* shards, const uint8_t* present,
                        size_t len, int data_only) {
     tables();
+    return reconstruct_impl(0, k, p, shards, present, len, data_only);
+}
+
+/* The crate's reconstruct (galois_8 ReedSolomon::reconstruct_internal): the
+ * first k present shards in index order, decode matrix = inv(M[valid]),
+ * absent data rows rebuilt with the SIMD mul_slice loop, absent parity
+ * re-encoded from the rebuilt data unless data_only. */
+static int reconstruct_impl(int variant, uint32_t k, uint32_t p, uint8_t* const* shards, const uint8_t* present,
+                            size_t len, int data_only) {
     uint32_t t = k + p, npresent = 0;
     for (uint32_t i = 0; i < t; ++i) npresent += present[i] ? 1 : 0;
     if (npresent == t) return 0;
@@ -248,13 +260,13 @@ int oracle_reconstruct(uint32_t k, uint32_t p, uint8_t* const* shards, const uin
         for (uint32_t i = 0; i < k; ++i) in[i] = shards[valid[i]];
         for (uint32_t j = 0; j < ninval; ++j)
             if (inval[j] < k) { memcpy(rows + (size_t)nr * k, dec + (size_t)inval[j] * k, k); out[nr++] = shards[inval[j]]; }
-        if (nr) code_some_slices(0, rows, nr, k, in, out, len);
+        if (nr) code_some_slices(variant, rows, nr, k, in, out, len);
         if (!data_only) {
             nr = 0;
             for (uint32_t j = 0; j < ninval; ++j)
                 if (inval[j] >= k) { memcpy(rows + (size_t)nr * k, m + (size_t)inval[j] * k, k); out[nr++] = shards[inval[j]]; }
             for (uint32_t i = 0; i < k; ++i) in[i] = shards[i];   /* full data after rebuild */
-            if (nr) code_some_slices(0, rows, nr, k, in, out, len);
+            if (nr) code_some_slices(variant, rows, nr, k, in, out, len);
         }
     }
     free(sub); free(dec); free(m);
@@ -307,6 +319,114 @@ double oracle_encode_batch(int variant, uint32_t k, uint32_t p,
     clock_gettime(CLOCK_MONOTONIC, &t0);
     for (int i = 1; i < nthreads; ++i) pthread_create(&th[i], NULL, batch_worker, &j);
     batch_worker(&j);
+    for (int i = 1; i < nthreads; ++i) pthread_join(th[i], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    free(m);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
+/* ---- threaded batch reconstruct (CPU baseline of the decode configs):
+ * block b's shard i at base + b * block_pitch + i * shard_pitch, presence
+ * flags present[b * (k + p) + i]; one block per task. ---------------------- */
+typedef struct {
+    int variant; uint32_t k, p;
+    uint8_t* base; size_t shard_pitch, block_pitch;
+    const uint8_t* present; size_t len; int data_only;
+    size_t nblocks; size_t next; int rc; pthread_mutex_t mu;
+} rbatch_job;
+
+static void* rbatch_worker(void* arg) {
+    rbatch_job* j = (rbatch_job*)arg;
+    uint8_t* sh[256];
+    const uint32_t t = j->k + j->p;
+    for (;;) {
+        pthread_mutex_lock(&j->mu);
+        size_t b = j->next++;
+        pthread_mutex_unlock(&j->mu);
+        if (b >= j->nblocks) break;
+        for (uint32_t i = 0; i < t; ++i) sh[i] = j->base + b * j->block_pitch + i * j->shard_pitch;
+        int rc = reconstruct_impl(j->variant, j->k, j->p, sh, j->present + b * t, j->len, j->data_only);
+        if (rc) { pthread_mutex_lock(&j->mu); j->rc = rc; pthread_mutex_unlock(&j->mu); }
+    }
+    return NULL;
+}
+
+double oracle_reconstruct_batch(int variant, uint32_t k, uint32_t p, uint8_t* base, size_t shard_pitch,
+                                size_t block_pitch, const uint8_t* present, size_t nblocks, size_t len,
+                                int data_only, int nthreads) {
+    tables();
+    if (variant == 1 && !have_avx2()) variant = 0;
+    rbatch_job j = {variant, k, p, base, shard_pitch, block_pitch, present, len, data_only, nblocks, 0, 0,
+                    PTHREAD_MUTEX_INITIALIZER};
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int i = 1; i < nthreads; ++i) pthread_create(&th[i], NULL, rbatch_worker, &j);
+    rbatch_worker(&j);
+    for (int i = 1; i < nthreads; ++i) pthread_join(th[i], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    if (j.rc) return -1.0;
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
+/* ---- threaded VirtualBlock::sync_data Erasure arm minus disk I/O
+ * (block.rs:406-430): per block, chunks(S).to_vec() of the size-byte buffer,
+ * the last chunk resized to S, p + (k - nchunks) zero shards appended, then
+ * encode; the Vec allocations are part of the timed work, as in the
+ * reference.  Parity is written to parity + b * p * S for checking. -------- */
+typedef struct {
+    int variant; uint32_t k, p;
+    const uint8_t* src; size_t size, S;
+    uint8_t* parity; const uint8_t* prow;
+    size_t nblocks; size_t next; pthread_mutex_t mu;
+} sbatch_job;
+
+static void* sbatch_worker(void* arg) {
+    sbatch_job* j = (sbatch_job*)arg;
+    uint8_t* sh[256];
+    for (;;) {
+        pthread_mutex_lock(&j->mu);
+        size_t b = j->next++;
+        pthread_mutex_unlock(&j->mu);
+        if (b >= j->nblocks) break;
+        const uint8_t* buf = j->src + b * j->size;
+        const size_t nchunks = (j->size + j->S - 1) / j->S;
+        const uint32_t t = j->k + j->p;
+        for (uint32_t i = 0; i < t; ++i) {
+            sh[i] = (uint8_t*)malloc(j->S);
+            if (i < nchunks) {
+                const size_t off = (size_t)i * j->S;
+                const size_t n = off + j->S <= j->size ? j->S : j->size - off;
+                memcpy(sh[i], buf + off, n);
+                if (n < j->S) memset(sh[i] + n, 0, j->S - n);
+            } else {
+                memset(sh[i], 0, j->S);
+            }
+        }
+        code_some_slices(j->variant, j->prow, j->p, j->k, (const uint8_t* const*)sh, sh + j->k, j->S);
+        for (uint32_t r = 0; r < j->p; ++r) memcpy(j->parity + (b * j->p + r) * j->S, sh[j->k + r], j->S);
+        for (uint32_t i = 0; i < t; ++i) free(sh[i]);
+    }
+    return NULL;
+}
+
+double oracle_sync_data_batch(int variant, uint32_t k, uint32_t p, const uint8_t* src, size_t size, size_t S,
+                              uint8_t* parity, size_t nblocks, int nthreads) {
+    tables();
+    if (variant == 1 && !have_avx2()) variant = 0;
+    if (S == 0 || (size + S - 1) / S > k) return -1.0;
+    uint8_t* m = (uint8_t*)malloc((size_t)(k + p) * k);
+    if (oracle_build_matrix(k, p, m) != 0) { free(m); return -1.0; }
+    sbatch_job j = {variant, k, p, src, size, S, parity, m + (size_t)k * k, nblocks, 0, PTHREAD_MUTEX_INITIALIZER};
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int i = 1; i < nthreads; ++i) pthread_create(&th[i], NULL, sbatch_worker, &j);
+    sbatch_worker(&j);
     for (int i = 1; i < nthreads; ++i) pthread_join(th[i], NULL);
     clock_gettime(CLOCK_MONOTONIC, &t1);
     free(m);

@@ -271,3 +271,46 @@ def test_load_block_quirks():
     s2[2] = s2[2][:100]
     got = O.load_block_erasure(s2, size, k, p)
     assert sha(got) == case["truncated_data2"] != case["original"]   # zero padding survives (block.rs:548-551)
+
+
+def test_reconstruct_batch_matches_single_block():
+    """Threaded AVX2 batch reconstruct (the decode CPU baseline) == the
+    single-block oracle (scalar), mixed patterns incl. data_only."""
+    k, p, S, B = 8, 3, 4096 + 7, 9
+    rng = np.random.default_rng(77)
+    data = rng.integers(0, 256, (B, k + p, S), dtype=np.uint8)
+    for b in range(B):
+        sh = [data[b, i].copy() for i in range(k)] + [np.zeros(S, np.uint8) for _ in range(p)]
+        c_oracle.encode(k, p, sh)
+        data[b, k:] = np.stack(sh[k:])
+    full = data.copy()
+    present = np.ones((B, k + p), np.uint8)
+    for b in range(B):
+        present[b, rng.choice(k + p, size=int(rng.integers(0, p + 1)), replace=False)] = 0
+    for data_only in (False, True):
+        work = full.copy()
+        work[present == 0] = 0
+        assert c_oracle.reconstruct_batch(k, p, work, present, S, 4, data_only=data_only) >= 0
+        for b in range(B):
+            for i in range(k + p):
+                if data_only and i >= k and not present[b, i]:
+                    assert not work[b, i].any()
+                else:
+                    assert np.array_equal(work[b, i], full[b, i]), (b, i, data_only)
+
+
+@pytest.mark.parametrize("size", [1 << 20, 700_001, 8 * 4096 - 100])
+def test_sync_data_batch_matches_restatement(size):
+    """Threaded sync_data-minus-disk baseline (block.rs:406-430) == the
+    numpy restatement of the Erasure arm, parity for parity."""
+    k, p, B = 4, 2, 5
+    S = O.calculate_shard_size(1 << 20, k) if size == 700_001 else O.calculate_shard_size(size, k)
+    rng = np.random.default_rng(size)
+    src = rng.integers(0, 256, B * size, dtype=np.uint8)
+    par = np.zeros(B * p * S, np.uint8)
+    c_oracle.sync_data_batch(k, p, src, size, S, par, B, 3)
+    block = 1 << 20 if size == 700_001 else size
+    for b in range(B):
+        want = O.sync_data_erasure(src[b * size:(b + 1) * size].tobytes(), block, k, p)
+        for r in range(p):
+            assert np.array_equal(par[(b * p + r) * S:(b * p + r + 1) * S], want[k + r])
