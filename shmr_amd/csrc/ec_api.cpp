@@ -223,6 +223,10 @@ int shmr_ec_encode(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_le
         rc = core::run_mapped_job(job, &dev, 1, &handled);
         if (handled || rc) return rc;
     }
+    if (uint64_t(t) * len <= core::bounce_limit()) {   // pageable, small: one bounce, one launch
+        const core::HostJob job{c, core::kEncode, false, shards, nullptr, 1, len, 0, 1};
+        return core::run_bounced_job(job, dev);
+    }
     core::count_blocks(false, 1);
     core::DeviceScope scope(dev);
     if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
@@ -280,6 +284,10 @@ int shmr_ec_reconstruct(shmr_ec_t* rs, uint8_t* const* shards, const size_t* sha
         bool handled = false;
         rc = core::run_mapped_job(job, &dev, 1, &handled);
         if (handled || rc) return rc;
+    }
+    if (uint64_t(t) * len <= core::bounce_limit()) {   // pageable, small: one bounce, one launch
+        const core::HostJob job{c, core::kDecode, data_only != 0, shards, present, 1, len, 0, 1};
+        return core::run_bounced_job(job, dev);
     }
     core::count_blocks(false, 1);
     core::DeviceScope scope(dev);

@@ -15,6 +15,8 @@ namespace core {
 // ===========================================================================
 namespace {
 
+constexpr int kBounceKibDefault = 8192;   // measured: see bounce_limit()
+
 struct Tuning {
     std::atomic<int> u{kAuto};
     std::atomic<int> nt_load{kAuto};
@@ -32,6 +34,7 @@ struct Tuning {
     std::atomic<int> fuse_tail{kAuto};
 };
 Tuning g_tune[2];   // [kEncode], [kDecode]
+std::atomic<int> g_bounce_kib{kBounceKibDefault};
 
 // Measured (tools/tune.py, interleaved A/B in one process): a register ring
 // of depth 2 (one shard of loads in flight per wave) beats depth 3 on every
@@ -91,6 +94,11 @@ int set_tuning(const char* key, int value) {
     std::string k;
     int first = 0, last = 1;
     if (!split_key(key, &k, &first, &last)) return SHMR_EC_INVALID_ARGUMENT;
+    if (k == "bounce_kib") {   // not per op class
+        if (value < 0 && value != kAuto) return SHMR_EC_INVALID_ARGUMENT;
+        g_bounce_kib = value == kAuto ? kBounceKibDefault : value;
+        return SHMR_EC_OK;
+    }
     for (int i = first; i <= last; ++i) {
         Tuning& T = g_tune[i];
         if (k == "chunks") {
@@ -139,6 +147,7 @@ int get_tuning(const char* key) {
     int first = 0, last = 1;
     if (!split_key(key, &k, &first, &last)) return SHMR_EC_INVALID_ARGUMENT;
     const Tuning& T = g_tune[first];
+    if (k == "bounce_kib") return g_bounce_kib;
     if (k == "chunks") return T.u;
     if (k == "nt_load") return T.nt_load;
     if (k == "nt_store") return T.nt_store;
@@ -176,6 +185,8 @@ kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_m
 }
 
 int grid_mode(OpClass op) { return g_tune[op].grid.load(); }
+
+uint64_t bounce_limit() { return uint64_t(g_bounce_kib.load()) << 10; }
 
 kern::Variant launch_variant(OpClass op, unsigned k, unsigned rows, bool host_mapped, bool ptrs, bool segs) {
     kern::Variant v = resolve_variant(op, k, rows, host_mapped);

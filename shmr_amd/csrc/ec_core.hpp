@@ -43,6 +43,9 @@ kern::Variant launch_variant(OpClass op, unsigned k, unsigned rows, bool host_ma
 // Whether segment launches are compiled for this op's current tuning.
 bool segs_supported(OpClass op, unsigned k, bool host_mapped, bool ptrs);
 int grid_mode(OpClass op);
+// Largest block ((k+p) * shard bytes) a pageable single-block call bounces
+// through a mapped buffer instead of per-shard DMA copies (knob "bounce_kib").
+uint64_t bounce_limit();
 
 // ---- devices --------------------------------------------------------------
 int device_count();

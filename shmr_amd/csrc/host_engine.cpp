@@ -371,7 +371,85 @@ bool mapped_translate(const void* p, size_t len, uint64_t* dev) {
     return translate_locked(p, len, dev, &hint);
 }
 
-int run_mapped_job(const HostJob& job, const int* devices, int ndev, bool* handled) {
+namespace {
+
+// Pool of mapped (pinned, device-visible) bounce buffers for run_bounced_job.
+class BouncePool {
+public:
+    static BouncePool& get() {
+        static BouncePool* p = new BouncePool;   // leaked: outlives static teardown
+        return *p;
+    }
+    uint8_t* acquire(size_t bytes) {
+        {
+            std::lock_guard<std::mutex> lock(mu_);
+            for (size_t i = 0; i < free_.size(); ++i)
+                if (free_[i].second >= bytes) {
+                    uint8_t* p = free_[i].first;
+                    free_.erase(free_.begin() + long(i));
+                    return p;
+                }
+        }
+        void* p = nullptr;
+        if (hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        void* dev = nullptr;
+        if (hipHostGetDevicePointer(&dev, p, 0) != hipSuccess || dev != p) {   // zero-copy needs unified addresses
+            (void)hipGetLastError();
+            (void)hipHostFree(p);
+            return nullptr;
+        }
+        mapped_add(p, bytes, dev);
+        std::lock_guard<std::mutex> lock(mu_);
+        size_[static_cast<uint8_t*>(p)] = bytes;
+        return static_cast<uint8_t*>(p);
+    }
+    void release(uint8_t* p) {
+        std::lock_guard<std::mutex> lock(mu_);
+        if (free_.size() >= kKeep) {   // keep a bounded pool
+            mapped_remove(p);
+            (void)hipHostFree(p);
+            size_.erase(p);
+            return;
+        }
+        free_.emplace_back(p, size_[p]);
+    }
+
+private:
+    static constexpr size_t kKeep = 32;
+    std::mutex mu_;
+    std::vector<std::pair<uint8_t*, size_t>> free_;
+    std::map<uint8_t*, size_t> size_;
+};
+
+}  // namespace
+
+int run_bounced_job(const HostJob& job, int device) {
+    const unsigned t = job.codec.k() + job.codec.p();
+    const size_t len = job.len;
+    std::vector<unsigned> in, out;
+    job_io(job, 0, in, out);
+    if (out.empty()) return SHMR_EC_OK;
+    uint8_t* bounce = BouncePool::get().acquire(size_t(t) * len);
+    if (!bounce) return SHMR_EC_OUT_OF_MEMORY;
+    std::vector<uint8_t*> ptrs(t);
+    for (unsigned i = 0; i < t; ++i) ptrs[i] = bounce + size_t(i) * len;
+    for (unsigned i : in) std::memcpy(ptrs[i], job.host_shards[i], len);
+    HostJob bj = job;
+    bj.host_shards = ptrs.data();
+    bool handled = false;
+    int rc = run_mapped_job(bj, &device, 1, &handled, false);
+    count_blocks(false, 1);
+    if (rc == SHMR_EC_OK && !handled) rc = SHMR_EC_DEVICE_ERROR;
+    if (rc == SHMR_EC_OK)
+        for (unsigned i : out) std::memcpy(job.host_shards[i], ptrs[i], len);
+    BouncePool::get().release(bounce);
+    return rc;
+}
+
+int run_mapped_job(const HostJob& job, const int* devices, int ndev, bool* handled, bool count) {
     *handled = false;
     if (job.op == kDecode) {
         const int rc = validate_presence(job.codec, job.present, job.nblocks);
@@ -381,7 +459,7 @@ int run_mapped_job(const HostJob& job, const int* devices, int ndev, bool* handl
     bool aligned = true;
     if (!map_job(job, &dptrs, &aligned)) return SHMR_EC_OK;
     *handled = true;
-    count_blocks(true, job.nblocks);
+    if (count) count_blocks(true, job.nblocks);
     return run_mapped(job, dptrs, aligned, devices, ndev);
 }
 

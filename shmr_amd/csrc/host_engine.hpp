@@ -31,7 +31,12 @@ int run_host_job(const HostJob& job, const int* devices, int ndev);
 
 // Zero-copy only: *handled = false (and nothing runs) unless every shard the
 // job touches is mapped.  Used by the single-block entry points.
-int run_mapped_job(const HostJob& job, const int* devices, int ndev, bool* handled);
+int run_mapped_job(const HostJob& job, const int* devices, int ndev, bool* handled, bool count = true);
+
+// Pageable single-block job through a pooled mapped bounce buffer: the input
+// shards are memcpy'd in, the kernel runs zero-copy on the bounce buffer, the
+// outputs are memcpy'd back -- one launch instead of one DMA per shard.
+int run_bounced_job(const HostJob& job, int device);
 
 // Registry of mapped (page-locked, device-visible) host memory: allocations of
 // shmr_ec_host_alloc and ranges given to shmr_ec_host_register.

@@ -201,6 +201,16 @@ def test_tuning_api():
     assert "early=0" in shmr_amd.describe_variant(True, 4, 2)
     assert "fuse_tail=1" in shmr_amd.describe_variant(False, 10, 4)
     assert "fuse_tail=1" in shmr_amd.describe_variant(True, 10, 2)
+    saved = shmr_amd.get_tuning("bounce_kib")
+    try:
+        shmr_amd.set_tuning(bounce_kib=0)
+        assert shmr_amd.get_tuning("bounce_kib") == 0
+        shmr_amd.set_tuning(bounce_kib=-2)
+        assert shmr_amd.get_tuning("bounce_kib") == 8192       # auto: 8 MiB blocks bounce (measured crossover)
+        with pytest.raises(shmr_amd.Error):
+            shmr_amd.set_tuning(bounce_kib=-5)
+    finally:
+        shmr_amd.set_tuning(bounce_kib=saved)
 
 
 def test_auto_policy_variants_are_compiled():

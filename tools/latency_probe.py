@@ -27,8 +27,11 @@ from shmr_amd._native import _u8p, lib  # noqa: E402
 def main():
     k, p = 8, 3
     out = []
+    cases = [(True, None), (False, 0), (False, 65536)]   # mapped; pageable staged; pageable bounced
     for S in (4096, 524288):
-        for mapped in (True, False):
+        for mapped, bounce in cases:
+            if bounce is not None:
+                shmr_amd.set_tuning(bounce_kib=bounce)
             if mapped:
                 keep = shmr_amd.PinnedBuffer((k + p) * S)
                 arr = keep.array.reshape(k + p, S)
@@ -51,11 +54,31 @@ def main():
                     t0 = time.perf_counter()
                     call()
                     ts.append(time.perf_counter() - t0)
-                rec = {"call": name, "shard_bytes": S, "buffers": "mapped" if mapped else "pageable",
+                rec = {"call": name, "shard_bytes": S,
+                       "buffers": "mapped" if mapped else ("pageable, bounced" if bounce else "pageable, staged DMA"),
                        "median_us": round(float(np.median(ts)) * 1e6, 1), "p10_us": round(float(np.percentile(ts, 10)) * 1e6, 1)}
                 out.append(rec)
                 print(json.dumps(rec), flush=True)
             del keep
+    shmr_amd.set_tuning(bounce_kib=-2)
+    # the reference's shape: per-block encode calls from 8 threads, pageable 4 MiB blocks
+    from concurrent.futures import ThreadPoolExecutor
+    S = 524288
+    rng = np.random.default_rng(2)
+    blocks = [[rng.integers(0, 256, S, dtype=np.uint8) if i < k else np.zeros(S, np.uint8) for i in range(k + p)]
+              for _ in range(64)]
+    rs = shmr_amd.ReedSolomon(k, p)
+    pool = ThreadPoolExecutor(8)
+    for bounce in (0, 65536):
+        shmr_amd.set_tuning(bounce_kib=bounce)
+        list(pool.map(rs.encode, blocks))
+        t0 = time.perf_counter()
+        for _ in range(3):
+            list(pool.map(rs.encode, blocks))
+        dt = (time.perf_counter() - t0) / 3
+        print(json.dumps({"call": "encode x64 blocks, 8 threads", "buffers": "pageable, bounced" if bounce else
+                          "pageable, staged DMA", "data_GiBps": round(64 * k * S / dt / 2 ** 30, 2)}), flush=True)
+    shmr_amd.set_tuning(bounce_kib=-2)
 
 
 if __name__ == "__main__":
