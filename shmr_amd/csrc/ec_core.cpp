@@ -54,7 +54,10 @@ std::atomic<int> g_bounce_kib{kBounceKibDefault};
 // 64 latency-bound workgroups after the full tiles.  Placed at each block's
 // end instead, the slow partial tiles finished last and the fused launch lost
 // 5 %; a concurrent side-stream tail launch lost 3 %; uploading multi-plan
-// tables on a side stream was neutral.
+// tables on a side stream was neutral.  Computing an encode's shard offsets
+// arithmetically (identity plan) instead of reading them from LDS before each
+// look-ahead load measured neutral (-0.2 to -1 %): the LDS round trip hides
+// under the other waves.
 //
 // Zero-copy launches over mapped host memory (the kernel's loads and stores
 // cross PCIe) are bound by the link, not HBM: there plain (temporal) loads
