@@ -191,7 +191,9 @@ int shmr_ec_set_device(shmr_ec_t* rs, int device);
  * "bounce_kib" (both op classes): pageable single-block calls whose (k+p) x
  * shard bytes fit in this many KiB go through one mapped bounce buffer and a
  * single zero-copy launch instead of per-shard DMA copies (default 8192; 0
- * disables).
+ * disables).  "mirror_zc" (0/1, default 1): pageable host batches are
+ * gathered into a pinned mirror that the kernel codes in place across PCIe
+ * (zero-copy) instead of DMA-ing it to device staging.
  * "chunks", "nt_load", "nt_store", "depth", "occ", "early", "spre" and "fuse_tail" default to -2 (auto): a per-shape policy
  * of the fastest variants measured on MI355X; any other value pins the knob,
  * and setting -2 returns it to the policy. */

@@ -35,6 +35,7 @@ struct Tuning {
 };
 Tuning g_tune[2];   // [kEncode], [kDecode]
 std::atomic<int> g_bounce_kib{kBounceKibDefault};
+std::atomic<int> g_mirror_zc{1};
 
 // Measured (tools/tune.py, interleaved A/B in one process): a register ring
 // of depth 2 (one shard of loads in flight per wave) beats depth 3 on every
@@ -102,6 +103,10 @@ int set_tuning(const char* key, int value) {
         g_bounce_kib = value == kAuto ? kBounceKibDefault : value;
         return SHMR_EC_OK;
     }
+    if (k == "mirror_zc") {
+        g_mirror_zc = value == kAuto ? 1 : (value != 0);
+        return SHMR_EC_OK;
+    }
     for (int i = first; i <= last; ++i) {
         Tuning& T = g_tune[i];
         if (k == "chunks") {
@@ -151,6 +156,7 @@ int get_tuning(const char* key) {
     if (!split_key(key, &k, &first, &last)) return SHMR_EC_INVALID_ARGUMENT;
     const Tuning& T = g_tune[first];
     if (k == "bounce_kib") return g_bounce_kib;
+    if (k == "mirror_zc") return g_mirror_zc;
     if (k == "chunks") return T.u;
     if (k == "nt_load") return T.nt_load;
     if (k == "nt_store") return T.nt_store;
@@ -190,6 +196,8 @@ kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_m
 int grid_mode(OpClass op) { return g_tune[op].grid.load(); }
 
 uint64_t bounce_limit() { return uint64_t(g_bounce_kib.load()) << 10; }
+
+bool mirror_zero_copy() { return g_mirror_zc.load() != 0; }
 
 kern::Variant launch_variant(OpClass op, unsigned k, unsigned rows, bool host_mapped, bool ptrs, bool segs) {
     kern::Variant v = resolve_variant(op, k, rows, host_mapped);

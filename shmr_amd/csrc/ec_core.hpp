@@ -46,6 +46,9 @@ int grid_mode(OpClass op);
 // Largest block ((k+p) * shard bytes) a pageable single-block call bounces
 // through a mapped buffer instead of per-shard DMA copies (knob "bounce_kib").
 uint64_t bounce_limit();
+// Pageable host batches: code the pinned mirror in place (zero-copy) instead
+// of DMA-ing it to device staging (knob "mirror_zc").
+bool mirror_zero_copy();
 
 // ---- devices --------------------------------------------------------------
 int device_count();

@@ -113,7 +113,8 @@ bool is_pinned(const void* p) {
 
 struct StageSet {
     uint8_t* dbuf = nullptr;   // [C][t][pitch] device
-    uint8_t* hbuf = nullptr;   // pinned mirror (pageable mode)
+    uint8_t* hbuf = nullptr;   // pinned mirror (pageable mode), mapped
+    bool hbuf_unified = false; // hbuf's device address is hbuf: kernels can run on it in place
     size_t dcap = 0, hcap = 0;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
@@ -145,9 +146,14 @@ struct DevicePipe {
                 if (s.hbuf) (void)hipHostFree(s.hbuf);
                 s.hbuf = nullptr;
                 s.hcap = 0;
-                if (hipHostMalloc(reinterpret_cast<void**>(&s.hbuf), hbytes, hipHostMallocDefault) != hipSuccess)
+                s.hbuf_unified = false;
+                if (hipHostMalloc(reinterpret_cast<void**>(&s.hbuf), hbytes,
+                                  hipHostMallocMapped | hipHostMallocPortable) != hipSuccess)
                     return SHMR_EC_OUT_OF_MEMORY;
                 s.hcap = hbytes;
+                void* d = nullptr;
+                s.hbuf_unified = hipHostGetDevicePointer(&d, s.hbuf, 0) == hipSuccess && d == s.hbuf;
+                if (!s.hbuf_unified) (void)hipGetLastError();
             }
             s.pending = false;
             s.blocks.clear();
@@ -559,7 +565,10 @@ int run_host_job(const HostJob& job, const int* devices, int ndev) {
                 }
                 crew.run(tasks);
             }
-            for (size_t j = 0; j < n && rc == SHMR_EC_OK; ++j) {
+            // Pageable mode with a unified mirror: the kernel codes the mirror in
+            // place across PCIe (zero-copy) -- no H2D / D2H copies.
+            const bool zc = !pinned && s.hbuf_unified && mirror_zero_copy();
+            for (size_t j = 0; j < n && rc == SHMR_EC_OK && !zc; ++j) {
                 io(s.blocks[j], in, out);
                 if (job.op == kEncode && !pinned) {   // k data shards are contiguous in the mirror
                     if (hipMemcpyAsync(s.dbuf + j * block_bytes, s.hbuf + j * block_bytes, (k - 1) * pitch + len,
@@ -580,19 +589,20 @@ int run_host_job(const HostJob& job, const int* devices, int ndev) {
             }
             // compute
             if (rc == SHMR_EC_OK) {
+                uint8_t* base = zc ? s.hbuf : s.dbuf;
+                Layout L{base, base, block_bytes, pitch, block_bytes, pitch, 0};
+                L.host_mapped = zc;
                 if (job.op == kEncode) {
-                    const Layout L{s.dbuf, s.dbuf, block_bytes, pitch, block_bytes, pitch, 0};
                     rc = encode_on_device(c, dev, L, n, len, s.stream);
                 } else {
                     present.assign(n * t, 1);
                     for (size_t j = 0; j < n; ++j)
                         std::memcpy(present.data() + j * t, job.present + s.blocks[j] * t, t);
-                    rc = reconstruct_on_device(c, dev, s.dbuf, pitch, block_bytes, present.data(), n, len,
-                                               job.data_only, s.stream);
+                    rc = reconstruct_on_device(c, dev, L, present.data(), n, len, job.data_only, s.stream);
                 }
             }
             // outputs
-            for (size_t j = 0; j < n && rc == SHMR_EC_OK; ++j) {
+            for (size_t j = 0; j < n && rc == SHMR_EC_OK && !zc; ++j) {
                 io(s.blocks[j], in, out);
                 if (job.op == kEncode && !pinned) {   // p parity shards are contiguous too
                     if (hipMemcpyAsync(s.hbuf + (j * t + k) * pitch, s.dbuf + (j * t + k) * pitch,

@@ -109,3 +109,31 @@ def test_blocks_host_array_form(gpu, mapped):
     assert np.array_equal(arr, full)
     with pytest.raises(TypeError):
         rs.encode_blocks_host(arr[:, :, ::2])     # shard bytes not contiguous
+
+
+@pytest.mark.parametrize("mirror_zc", [0, 1])
+def test_pageable_batch_mirror_modes(gpu, mirror_zc):
+    """Pageable host batches: the pinned mirror coded in place (zero-copy) or
+    DMA'd to device staging -- identical, oracle-exact results."""
+    saved = shmr_amd.get_tuning("mirror_zc")
+    shmr_amd.set_tuning(mirror_zc=mirror_zc)
+    try:
+        k, p, S, B = 10, 4, 1677722, 5
+        rng = np.random.default_rng([mirror_zc, 5])
+        arr = np.zeros((B, k + p, S), np.uint8)
+        arr[:, :k] = rng.integers(0, 256, (B, k, S), dtype=np.uint8)
+        rs = shmr_amd.ReedSolomon(k, p)
+        rs.encode_blocks_host(arr)
+        for b in range(B):
+            want = oracle_parity(k, p, [arr[b, i].copy() for i in range(k)])
+            for r in range(p):
+                assert np.array_equal(arr[b, k + r], want[r])
+        full = arr.copy()
+        present = np.ones((B, k + p), np.uint8)
+        for b in range(B):
+            present[b, [b % k, (b + 3) % k, k + b % p]] = 0
+            arr[b, [b % k, (b + 3) % k, k + b % p]] = 0
+        rs.reconstruct_blocks_host(arr, present)
+        assert np.array_equal(arr, full)
+    finally:
+        shmr_amd.set_tuning(mirror_zc=saved)
