@@ -11,7 +11,8 @@
 // across PCIe through a device table of shard pointers (zero-copy; measured
 // 1.5x the staged DMA pipeline, tools/pcie_probe.py).  Other pinned buffers
 // are DMA'd directly; pageable buffers (plain Vec<u8>/malloc) are first
-// gathered into a pinned mirror by a crew of copy threads.
+// gathered into a mapped pinned mirror by a crew of copy threads, which the
+// kernels then code in place (zero-copy; DMA staging if "mirror_zc" is off).
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
