@@ -45,7 +45,11 @@ std::atomic<int> g_mirror_zc{1};
 // occupancy caps lose.  With depth 2, NT loads + NT stores win everywhere;
 // encodes with 4 rows per launch (RS(10,4)) use U = 2.  Encodes with k < 8
 // (short-lived workgroups) issue their first data loads ahead of the plan
-// staging ("early": RS(4,2) 83 % vs 80 %; neutral at k = 8, -2 % on decode).
+// staging ("early": RS(4,2) 83 % vs 80 %; neutral at k = 8, -2 % on decode,
+// re-measured with segment launches: RS(8,3) 71.1 vs 72.6 %, RS(10,4) 75.1 vs
+// 76.6 %).  Decodes with temporal stores lose 5-8 points (RS(8,3) 64.8 vs
+// 73.3 %, RS(10,4) 70.7 vs 75.9 %), although a copy-only 8-in/1-out probe
+// preferred them (tools/membench.hip).
 // Scalar-loaded tables ("spre", 7-8 waves/SIMD) lose 3-6 % everywhere.
 // An XCD-grouped tile order (workgroup w -> tile (w % 8) * n/8 + w / 8, each
 // XCD streaming one contiguous eighth) measured within +-2 % and was dropped.
