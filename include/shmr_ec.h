@@ -18,7 +18,8 @@
  * compute entry point returns SHMR_EC_NO_DEVICE / SHMR_EC_DEVICE_ERROR.
  *
  * Conventions: plain pointers and sizes, 0 on success, negative status on
- * failure, never aborts, never frees caller memory.  Thread-safe: contexts
+ * failure, never aborts (an internal allocation failure returns
+ * SHMR_EC_OUT_OF_MEMORY), never frees caller memory.  Thread-safe: contexts
  * may be shared across threads or created per call (the reference creates a
  * ReedSolomon per block from rayon workers, src/vfs/mod.rs:93-96).
  */

@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <new>
 #include <vector>
 
 #include "ec_core.hpp"
@@ -20,6 +21,21 @@
 using shmr::core::Codec;
 using shmr::core::Plan;
 namespace core = shmr::core;
+
+namespace {
+// No C++ exception (allocation failure, thread or stream creation) crosses the
+// C ABI: it becomes a status code, so a Rust/C caller never sees an abort.
+template <class F>
+int guarded(F&& f) noexcept {
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        return SHMR_EC_OUT_OF_MEMORY;
+    } catch (...) {
+        return SHMR_EC_DEVICE_ERROR;
+    }
+}
+}  // namespace
 
 extern "C" {
 
@@ -92,25 +108,27 @@ int shmr_ec_matrix(const shmr_ec_t* rs, uint8_t* out, size_t out_len) {
 int shmr_ec_reconstruct_plan(shmr_ec_t* rs, const uint8_t* present, size_t nshards, int data_only,
                              uint16_t* in_idx, uint16_t* out_idx, uint8_t* out_rows, size_t out_rows_len,
                              uint32_t* n_out) {
-    if (!rs || !present || !in_idx || !out_idx || !out_rows || !n_out) return SHMR_EC_INVALID_ARGUMENT;
-    const unsigned k = rs->codec->k(), t = k + rs->codec->p();
-    if (nshards < t) return SHMR_EC_TOO_FEW_SHARDS;
-    if (nshards > t) return SHMR_EC_TOO_MANY_SHARDS;
-    unsigned np = 0;
-    for (unsigned i = 0; i < t; ++i) np += present[i] ? 1 : 0;
-    if (np == t) {
-        *n_out = 0;
+    return guarded([&]() -> int {
+        if (!rs || !present || !in_idx || !out_idx || !out_rows || !n_out) return SHMR_EC_INVALID_ARGUMENT;
+        const unsigned k = rs->codec->k(), t = k + rs->codec->p();
+        if (nshards < t) return SHMR_EC_TOO_FEW_SHARDS;
+        if (nshards > t) return SHMR_EC_TOO_MANY_SHARDS;
+        unsigned np = 0;
+        for (unsigned i = 0; i < t; ++i) np += present[i] ? 1 : 0;
+        if (np == t) {
+            *n_out = 0;
+            return SHMR_EC_OK;
+        }
+        if (np < k) return SHMR_EC_TOO_FEW_SHARDS_PRESENT;
+        std::vector<uint8_t> pr(present, present + t);
+        auto plan = rs->codec->reconstruct_plan(pr, data_only != 0);
+        if (out_rows_len < size_t(plan->m) * k) return SHMR_EC_INVALID_ARGUMENT;
+        std::memcpy(in_idx, plan->in_idx.data(), 2 * size_t(k));
+        std::memcpy(out_idx, plan->out_idx.data(), 2 * size_t(plan->m));
+        std::memcpy(out_rows, plan->rows.d.data(), size_t(plan->m) * k);
+        *n_out = plan->m;
         return SHMR_EC_OK;
-    }
-    if (np < k) return SHMR_EC_TOO_FEW_SHARDS_PRESENT;
-    std::vector<uint8_t> pr(present, present + t);
-    auto plan = rs->codec->reconstruct_plan(pr, data_only != 0);
-    if (out_rows_len < size_t(plan->m) * k) return SHMR_EC_INVALID_ARGUMENT;
-    std::memcpy(in_idx, plan->in_idx.data(), 2 * size_t(k));
-    std::memcpy(out_idx, plan->out_idx.data(), 2 * size_t(plan->m));
-    std::memcpy(out_rows, plan->rows.d.data(), size_t(plan->m) * k);
-    *n_out = plan->m;
-    return SHMR_EC_OK;
+    });
 }
 
 int shmr_ec_set_device(shmr_ec_t* rs, int device) {
@@ -119,8 +137,12 @@ int shmr_ec_set_device(shmr_ec_t* rs, int device) {
     return SHMR_EC_OK;
 }
 
-int shmr_ec_set_tuning(const char* key, int value) { return core::set_tuning(key, value); }
-int shmr_ec_get_tuning(const char* key) { return core::get_tuning(key); }
+int shmr_ec_set_tuning(const char* key, int value) {
+    return guarded([&] { return core::set_tuning(key, value); });
+}
+int shmr_ec_get_tuning(const char* key) {
+    return guarded([&] { return core::get_tuning(key); });
+}
 
 int shmr_ec_describe_variant(int decode, uint32_t data_shards, uint32_t rows, char* buf, size_t len) {
     if (!buf || len == 0 || rows == 0) return SHMR_EC_INVALID_ARGUMENT;
@@ -156,19 +178,30 @@ int shmr_ec_path_stats(uint64_t* zero_copy_blocks, uint64_t* staged_blocks) {
 // Mapped + portable: every GPU of the node can address it, so the host-buffer
 // entry points run their kernels on it in place (zero-copy).
 int shmr_ec_host_alloc(size_t bytes, void** out) {
-    if (!out) return SHMR_EC_INVALID_ARGUMENT;
-    *out = nullptr;
-    int rc = core::check_device(0);
-    if (rc) return rc;
-    const size_t n = bytes ? bytes : 1;
-    if (hipHostMalloc(out, n, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) {
+    return guarded([&]() -> int {
+        if (!out) return SHMR_EC_INVALID_ARGUMENT;
         *out = nullptr;
-        return SHMR_EC_OUT_OF_MEMORY;
-    }
-    void* dev = nullptr;
-    if (hipHostGetDevicePointer(&dev, *out, 0) == hipSuccess && dev) core::mapped_add(*out, n, dev);
-    else (void)hipGetLastError();   // still pinned: the staged DMA path takes it
-    return SHMR_EC_OK;
+        int rc = core::check_device(0);
+        if (rc) return rc;
+        const size_t n = bytes ? bytes : 1;
+        if (hipHostMalloc(out, n, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) {
+            *out = nullptr;
+            return SHMR_EC_OUT_OF_MEMORY;
+        }
+        void* dev = nullptr;
+        if (hipHostGetDevicePointer(&dev, *out, 0) == hipSuccess && dev) {
+            try {
+                core::mapped_add(*out, n, dev);
+            } catch (...) {   // registry allocation failed: hand nothing out
+                (void)hipHostFree(*out);
+                *out = nullptr;
+                throw;
+            }
+        } else {
+            (void)hipGetLastError();   // still pinned: the staged DMA path takes it
+        }
+        return SHMR_EC_OK;
+    });
 }
 
 void shmr_ec_host_free(void* p) {
@@ -178,198 +211,217 @@ void shmr_ec_host_free(void* p) {
 }
 
 int shmr_ec_host_register(void* p, size_t bytes) {
-    if (!p || bytes == 0) return SHMR_EC_INVALID_ARGUMENT;
-    int rc = core::check_device(0);
-    if (rc) return rc;
-    if (hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable) != hipSuccess) {
-        (void)hipGetLastError();
-        return SHMR_EC_DEVICE_ERROR;
-    }
-    void* dev = nullptr;
-    if (hipHostGetDevicePointer(&dev, p, 0) != hipSuccess || !dev) {
-        (void)hipGetLastError();
-        (void)hipHostUnregister(p);
-        return SHMR_EC_DEVICE_ERROR;
-    }
-    core::mapped_add(p, bytes, dev);
-    return SHMR_EC_OK;
+    return guarded([&]() -> int {
+        if (!p || bytes == 0) return SHMR_EC_INVALID_ARGUMENT;
+        int rc = core::check_device(0);
+        if (rc) return rc;
+        if (hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable) != hipSuccess) {
+            (void)hipGetLastError();
+            return SHMR_EC_DEVICE_ERROR;
+        }
+        void* dev = nullptr;
+        if (hipHostGetDevicePointer(&dev, p, 0) != hipSuccess || !dev) {
+            (void)hipGetLastError();
+            (void)hipHostUnregister(p);
+            return SHMR_EC_DEVICE_ERROR;
+        }
+        try {
+            core::mapped_add(p, bytes, dev);
+        } catch (...) {
+            (void)hipHostUnregister(p);
+            throw;
+        }
+        return SHMR_EC_OK;
+    });
 }
 
 int shmr_ec_host_unregister(void* p) {
-    if (!p || !core::mapped_remove(p)) return SHMR_EC_INVALID_ARGUMENT;
-    return hipHostUnregister(p) == hipSuccess ? SHMR_EC_OK : SHMR_EC_DEVICE_ERROR;
+    return guarded([&]() -> int {
+        if (!p || !core::mapped_remove(p)) return SHMR_EC_INVALID_ARGUMENT;
+        return hipHostUnregister(p) == hipSuccess ? SHMR_EC_OK : SHMR_EC_DEVICE_ERROR;
+    });
 }
 
 // ---- host-buffer encode (ReedSolomon::encode) --------------------------------------
 int shmr_ec_encode(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_lens, size_t nshards) {
-    if (!rs || !shards || !shard_lens) return SHMR_EC_INVALID_ARGUMENT;
-    Codec& c = *rs->codec;
-    const unsigned k = c.k(), p = c.p(), t = k + p;
-    // crate check_piece_count!(all) then check_slices!(multi)
-    if (nshards < t) return SHMR_EC_TOO_FEW_SHARDS;
-    if (nshards > t) return SHMR_EC_TOO_MANY_SHARDS;
-    const size_t len = shard_lens[0];
-    if (len == 0) return SHMR_EC_EMPTY_SHARD;
-    for (unsigned i = 0; i < t; ++i)
-        if (shard_lens[i] != len) return SHMR_EC_INCORRECT_SHARD_SIZE;
-    for (unsigned i = 0; i < t; ++i)
-        if (!shards[i]) return SHMR_EC_INVALID_ARGUMENT;
-    const int dev = rs->device;
-    int rc = core::check_device(dev);
-    if (rc) return rc;
-    {   // shards in mapped memory: the kernel encodes them in place (zero-copy)
-        const core::HostJob job{c, core::kEncode, false, shards, nullptr, 1, len, 0, 1};
-        bool handled = false;
-        rc = core::run_mapped_job(job, &dev, 1, &handled);
-        if (handled || rc) return rc;
-    }
-    if (uint64_t(t) * len <= core::bounce_limit()) {   // pageable, small: one bounce, one launch
-        const core::HostJob job{c, core::kEncode, false, shards, nullptr, 1, len, 0, 1};
-        return core::run_bounced_job(job, dev);
-    }
-    core::count_blocks(false, 1);
-    core::DeviceScope scope(dev);
-    if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
-    const uint64_t pitch = core::round_up(len, 256);
-    core::StagingLease lease;
-    lease.s = core::StagingPool::get().acquire(dev, pitch * t, &rc);
-    if (!lease.s) return rc;
-    core::Staging& s = *lease.s;
-    for (unsigned i = 0; i < k; ++i)
-        SHMR_HIP_TRY(hipMemcpyAsync(s.dbuf + i * pitch, shards[i], len, hipMemcpyHostToDevice, s.stream));
-    const core::Layout L{s.dbuf, s.dbuf, 0, pitch, 0, pitch, 0};
-    rc = core::encode_on_device(c, dev, L, 1, len, s.stream);
-    if (rc) return rc;
-    for (unsigned r = 0; r < p; ++r)
-        SHMR_HIP_TRY(hipMemcpyAsync(shards[k + r], s.dbuf + (k + r) * pitch, len, hipMemcpyDeviceToHost, s.stream));
-    SHMR_HIP_TRY(hipStreamSynchronize(s.stream));
-    return SHMR_EC_OK;
+    return guarded([&]() -> int {
+        if (!rs || !shards || !shard_lens) return SHMR_EC_INVALID_ARGUMENT;
+        Codec& c = *rs->codec;
+        const unsigned k = c.k(), p = c.p(), t = k + p;
+        // crate check_piece_count!(all) then check_slices!(multi)
+        if (nshards < t) return SHMR_EC_TOO_FEW_SHARDS;
+        if (nshards > t) return SHMR_EC_TOO_MANY_SHARDS;
+        const size_t len = shard_lens[0];
+        if (len == 0) return SHMR_EC_EMPTY_SHARD;
+        for (unsigned i = 0; i < t; ++i)
+            if (shard_lens[i] != len) return SHMR_EC_INCORRECT_SHARD_SIZE;
+        for (unsigned i = 0; i < t; ++i)
+            if (!shards[i]) return SHMR_EC_INVALID_ARGUMENT;
+        const int dev = rs->device;
+        int rc = core::check_device(dev);
+        if (rc) return rc;
+        {   // shards in mapped memory: the kernel encodes them in place (zero-copy)
+            const core::HostJob job{c, core::kEncode, false, shards, nullptr, 1, len, 0, 1};
+            bool handled = false;
+            rc = core::run_mapped_job(job, &dev, 1, &handled);
+            if (handled || rc) return rc;
+        }
+        if (uint64_t(t) * len <= core::bounce_limit()) {   // pageable, small: one bounce, one launch
+            const core::HostJob job{c, core::kEncode, false, shards, nullptr, 1, len, 0, 1};
+            return core::run_bounced_job(job, dev);
+        }
+        core::count_blocks(false, 1);
+        core::DeviceScope scope(dev);
+        if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
+        const uint64_t pitch = core::round_up(len, 256);
+        core::StagingLease lease;
+        lease.s = core::StagingPool::get().acquire(dev, pitch * t, &rc);
+        if (!lease.s) return rc;
+        core::Staging& s = *lease.s;
+        for (unsigned i = 0; i < k; ++i)
+            SHMR_HIP_TRY(hipMemcpyAsync(s.dbuf + i * pitch, shards[i], len, hipMemcpyHostToDevice, s.stream));
+        const core::Layout L{s.dbuf, s.dbuf, 0, pitch, 0, pitch, 0};
+        rc = core::encode_on_device(c, dev, L, 1, len, s.stream);
+        if (rc) return rc;
+        for (unsigned r = 0; r < p; ++r)
+            SHMR_HIP_TRY(hipMemcpyAsync(shards[k + r], s.dbuf + (k + r) * pitch, len, hipMemcpyDeviceToHost, s.stream));
+        SHMR_HIP_TRY(hipStreamSynchronize(s.stream));
+        return SHMR_EC_OK;
+    });
 }
 
 // ---- host-buffer reconstruct (ReedSolomon::reconstruct{,_data}) ---------------------
 int shmr_ec_reconstruct(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_lens, const uint8_t* present,
                         size_t nshards, int data_only) {
-    if (!rs || !shards || !shard_lens || !present) return SHMR_EC_INVALID_ARGUMENT;
-    Codec& c = *rs->codec;
-    const unsigned k = c.k(), p = c.p(), t = k + p;
-    if (nshards < t) return SHMR_EC_TOO_FEW_SHARDS;
-    if (nshards > t) return SHMR_EC_TOO_MANY_SHARDS;
-    // crate reconstruct_internal: per present shard, len 0 -> EmptyShard,
-    // mismatch -> IncorrectShardSize, in index order.
-    unsigned np = 0;
-    size_t len = 0;
-    bool have_len = false;
-    for (unsigned i = 0; i < t; ++i) {
-        if (!present[i]) continue;
-        if (shard_lens[i] == 0) return SHMR_EC_EMPTY_SHARD;
-        ++np;
-        if (have_len && shard_lens[i] != len) return SHMR_EC_INCORRECT_SHARD_SIZE;
-        len = shard_lens[i];
-        have_len = true;
-    }
-    if (np == t) return SHMR_EC_OK;
-    if (np < k) return SHMR_EC_TOO_FEW_SHARDS_PRESENT;
-    std::vector<uint8_t> pr(present, present + t);
-    auto plan = c.reconstruct_plan(pr, data_only != 0);
-    for (unsigned m = 0; m < plan->m; ++m)
-        if (!shards[plan->out_idx[m]]) return SHMR_EC_INVALID_ARGUMENT;
-    for (unsigned i = 0; i < k; ++i)
-        if (!shards[plan->in_idx[i]]) return SHMR_EC_INVALID_ARGUMENT;
-    if (plan->m == 0) return SHMR_EC_OK;
-    const int dev = rs->device;
-    int rc = core::check_device(dev);
-    if (rc) return rc;
-    {   // shards in mapped memory: rebuilt in place by the kernel (zero-copy)
-        const core::HostJob job{c, core::kDecode, data_only != 0, shards, present, 1, len, 0, 1};
-        bool handled = false;
-        rc = core::run_mapped_job(job, &dev, 1, &handled);
-        if (handled || rc) return rc;
-    }
-    if (uint64_t(t) * len <= core::bounce_limit()) {   // pageable, small: one bounce, one launch
-        const core::HostJob job{c, core::kDecode, data_only != 0, shards, present, 1, len, 0, 1};
-        return core::run_bounced_job(job, dev);
-    }
-    core::count_blocks(false, 1);
-    core::DeviceScope scope(dev);
-    if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
-    const uint64_t pitch = core::round_up(len, 256);
-    core::StagingLease lease;
-    lease.s = core::StagingPool::get().acquire(dev, pitch * t, &rc);
-    if (!lease.s) return rc;
-    core::Staging& s = *lease.s;
-    for (unsigned i = 0; i < k; ++i) {
-        const unsigned idx = plan->in_idx[i];
-        SHMR_HIP_TRY(hipMemcpyAsync(s.dbuf + idx * pitch, shards[idx], len, hipMemcpyHostToDevice, s.stream));
-    }
-    rc = core::reconstruct_on_device(c, dev, s.dbuf, pitch, pitch * t, present, 1, len, data_only != 0, s.stream);
-    if (rc) return rc;
-    for (unsigned m = 0; m < plan->m; ++m) {
-        const unsigned idx = plan->out_idx[m];
-        SHMR_HIP_TRY(hipMemcpyAsync(shards[idx], s.dbuf + idx * pitch, len, hipMemcpyDeviceToHost, s.stream));
-    }
-    SHMR_HIP_TRY(hipStreamSynchronize(s.stream));
-    return SHMR_EC_OK;
+    return guarded([&]() -> int {
+        if (!rs || !shards || !shard_lens || !present) return SHMR_EC_INVALID_ARGUMENT;
+        Codec& c = *rs->codec;
+        const unsigned k = c.k(), p = c.p(), t = k + p;
+        if (nshards < t) return SHMR_EC_TOO_FEW_SHARDS;
+        if (nshards > t) return SHMR_EC_TOO_MANY_SHARDS;
+        // crate reconstruct_internal: per present shard, len 0 -> EmptyShard,
+        // mismatch -> IncorrectShardSize, in index order.
+        unsigned np = 0;
+        size_t len = 0;
+        bool have_len = false;
+        for (unsigned i = 0; i < t; ++i) {
+            if (!present[i]) continue;
+            if (shard_lens[i] == 0) return SHMR_EC_EMPTY_SHARD;
+            ++np;
+            if (have_len && shard_lens[i] != len) return SHMR_EC_INCORRECT_SHARD_SIZE;
+            len = shard_lens[i];
+            have_len = true;
+        }
+        if (np == t) return SHMR_EC_OK;
+        if (np < k) return SHMR_EC_TOO_FEW_SHARDS_PRESENT;
+        std::vector<uint8_t> pr(present, present + t);
+        auto plan = c.reconstruct_plan(pr, data_only != 0);
+        for (unsigned m = 0; m < plan->m; ++m)
+            if (!shards[plan->out_idx[m]]) return SHMR_EC_INVALID_ARGUMENT;
+        for (unsigned i = 0; i < k; ++i)
+            if (!shards[plan->in_idx[i]]) return SHMR_EC_INVALID_ARGUMENT;
+        if (plan->m == 0) return SHMR_EC_OK;
+        const int dev = rs->device;
+        int rc = core::check_device(dev);
+        if (rc) return rc;
+        {   // shards in mapped memory: rebuilt in place by the kernel (zero-copy)
+            const core::HostJob job{c, core::kDecode, data_only != 0, shards, present, 1, len, 0, 1};
+            bool handled = false;
+            rc = core::run_mapped_job(job, &dev, 1, &handled);
+            if (handled || rc) return rc;
+        }
+        if (uint64_t(t) * len <= core::bounce_limit()) {   // pageable, small: one bounce, one launch
+            const core::HostJob job{c, core::kDecode, data_only != 0, shards, present, 1, len, 0, 1};
+            return core::run_bounced_job(job, dev);
+        }
+        core::count_blocks(false, 1);
+        core::DeviceScope scope(dev);
+        if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
+        const uint64_t pitch = core::round_up(len, 256);
+        core::StagingLease lease;
+        lease.s = core::StagingPool::get().acquire(dev, pitch * t, &rc);
+        if (!lease.s) return rc;
+        core::Staging& s = *lease.s;
+        for (unsigned i = 0; i < k; ++i) {
+            const unsigned idx = plan->in_idx[i];
+            SHMR_HIP_TRY(hipMemcpyAsync(s.dbuf + idx * pitch, shards[idx], len, hipMemcpyHostToDevice, s.stream));
+        }
+        rc = core::reconstruct_on_device(c, dev, s.dbuf, pitch, pitch * t, present, 1, len, data_only != 0, s.stream);
+        if (rc) return rc;
+        for (unsigned m = 0; m < plan->m; ++m) {
+            const unsigned idx = plan->out_idx[m];
+            SHMR_HIP_TRY(hipMemcpyAsync(shards[idx], s.dbuf + idx * pitch, len, hipMemcpyDeviceToHost, s.stream));
+        }
+        SHMR_HIP_TRY(hipStreamSynchronize(s.stream));
+        return SHMR_EC_OK;
+    });
 }
 
 // ---- device-resident batches --------------------------------------------------------
 int shmr_ec_encode_batch_dev(shmr_ec_t* rs, const uint8_t* d_data, size_t data_shard_pitch, size_t data_block_pitch,
                              uint8_t* d_parity, size_t parity_shard_pitch, size_t parity_block_pitch, size_t nblocks,
                              size_t shard_len, int device, void* stream) {
-    if (!rs) return SHMR_EC_INVALID_ARGUMENT;
-    if (nblocks == 0) return SHMR_EC_OK;
-    if (shard_len == 0) return SHMR_EC_EMPTY_SHARD;
-    if (!d_data || !d_parity) return SHMR_EC_INVALID_ARGUMENT;
-    int rc = core::check_device(device);
-    if (rc) return rc;
-    core::DeviceScope scope(device);
-    if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
-    Codec& c = *rs->codec;
-    const core::Layout L{d_data, d_parity, data_block_pitch, data_shard_pitch, parity_block_pitch, parity_shard_pitch,
-                         c.k()};
-    return core::encode_on_device(c, device, L, nblocks, shard_len, static_cast<hipStream_t>(stream));
+    return guarded([&]() -> int {
+        if (!rs) return SHMR_EC_INVALID_ARGUMENT;
+        if (nblocks == 0) return SHMR_EC_OK;
+        if (shard_len == 0) return SHMR_EC_EMPTY_SHARD;
+        if (!d_data || !d_parity) return SHMR_EC_INVALID_ARGUMENT;
+        int rc = core::check_device(device);
+        if (rc) return rc;
+        core::DeviceScope scope(device);
+        if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
+        Codec& c = *rs->codec;
+        const core::Layout L{d_data, d_parity, data_block_pitch, data_shard_pitch, parity_block_pitch, parity_shard_pitch,
+                             c.k()};
+        return core::encode_on_device(c, device, L, nblocks, shard_len, static_cast<hipStream_t>(stream));
+    });
 }
 
 int shmr_ec_reconstruct_batch_dev(shmr_ec_t* rs, uint8_t* d_shards, size_t shard_pitch, size_t block_pitch,
                                   const uint8_t* present, size_t nblocks, size_t shard_len, int data_only, int device,
                                   void* stream) {
-    if (!rs || !present) return SHMR_EC_INVALID_ARGUMENT;
-    if (nblocks == 0) return SHMR_EC_OK;
-    if (shard_len == 0) return SHMR_EC_EMPTY_SHARD;
-    if (!d_shards) return SHMR_EC_INVALID_ARGUMENT;
-    Codec& c = *rs->codec;
-    int rc = core::validate_presence(c, present, nblocks);   // no launch on a bad batch
-    if (rc) return rc;
-    rc = core::check_device(device);
-    if (rc) return rc;
-    core::DeviceScope scope(device);
-    if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
-    return core::reconstruct_on_device(c, device, d_shards, shard_pitch, block_pitch, present, nblocks, shard_len,
-                                       data_only != 0, static_cast<hipStream_t>(stream));
+    return guarded([&]() -> int {
+        if (!rs || !present) return SHMR_EC_INVALID_ARGUMENT;
+        if (nblocks == 0) return SHMR_EC_OK;
+        if (shard_len == 0) return SHMR_EC_EMPTY_SHARD;
+        if (!d_shards) return SHMR_EC_INVALID_ARGUMENT;
+        Codec& c = *rs->codec;
+        int rc = core::validate_presence(c, present, nblocks);   // no launch on a bad batch
+        if (rc) return rc;
+        rc = core::check_device(device);
+        if (rc) return rc;
+        core::DeviceScope scope(device);
+        if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
+        return core::reconstruct_on_device(c, device, d_shards, shard_pitch, block_pitch, present, nblocks, shard_len,
+                                           data_only != 0, static_cast<hipStream_t>(stream));
+    });
 }
 
 // ---- host-buffer batches over one or more GPUs -------------------------------------
 static int host_batch(shmr_ec_t* rs, uint8_t* const* host_shards, const uint8_t* present, size_t nblocks,
                       size_t shard_len, int data_only, const int* devices, int ndev, core::OpClass op) {
-    if (!rs || !host_shards || !devices || ndev <= 0) return SHMR_EC_INVALID_ARGUMENT;
-    if (op == core::kDecode && !present) return SHMR_EC_INVALID_ARGUMENT;
-    if (nblocks == 0) return SHMR_EC_OK;
-    if (shard_len == 0) return SHMR_EC_EMPTY_SHARD;
-    Codec& c = *rs->codec;
-    const unsigned t = c.k() + c.p();
-    for (size_t b = 0; b < nblocks; ++b)
-        for (unsigned i = 0; i < t; ++i) {
-            // absent shards of a decode still need an output buffer (unless
-            // they are parity under data_only)
-            const bool needed = op == core::kEncode || present[b * t + i] || i < c.k() || !data_only;
-            if (needed && !host_shards[b * t + i]) return SHMR_EC_INVALID_ARGUMENT;
+    return guarded([&]() -> int {
+        if (!rs || !host_shards || !devices || ndev <= 0) return SHMR_EC_INVALID_ARGUMENT;
+        if (op == core::kDecode && !present) return SHMR_EC_INVALID_ARGUMENT;
+        if (nblocks == 0) return SHMR_EC_OK;
+        if (shard_len == 0) return SHMR_EC_EMPTY_SHARD;
+        Codec& c = *rs->codec;
+        const unsigned t = c.k() + c.p();
+        for (size_t b = 0; b < nblocks; ++b)
+            for (unsigned i = 0; i < t; ++i) {
+                // absent shards of a decode still need an output buffer (unless
+                // they are parity under data_only)
+                const bool needed = op == core::kEncode || present[b * t + i] || i < c.k() || !data_only;
+                if (needed && !host_shards[b * t + i]) return SHMR_EC_INVALID_ARGUMENT;
+            }
+        for (int d = 0; d < ndev; ++d) {
+            int rc = core::check_device(devices[d]);
+            if (rc) return rc;
         }
-    for (int d = 0; d < ndev; ++d) {
-        int rc = core::check_device(devices[d]);
-        if (rc) return rc;
-    }
-    core::HostJob job{c, op, data_only != 0, host_shards, present, nblocks, shard_len, 64ull << 20,
-                      core::copy_threads_default()};
-    return core::run_host_job(job, devices, ndev);
+        core::HostJob job{c, op, data_only != 0, host_shards, present, nblocks, shard_len, 64ull << 20,
+                          core::copy_threads_default()};
+        return core::run_host_job(job, devices, ndev);
+    });
 }
 
 int shmr_ec_encode_blocks_host(shmr_ec_t* rs, uint8_t* const* host_shards, size_t nblocks, size_t shard_len,
