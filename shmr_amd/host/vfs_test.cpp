@@ -26,9 +26,33 @@ struct Failure {
     std::string msg;
 };
 
+static std::string diff_report(const std::vector<uint8_t>& a, const std::vector<uint8_t>& b, size_t bs, size_t S) {
+    std::string r;
+    if (a.size() != b.size()) return ": sizes " + std::to_string(a.size()) + " vs " + std::to_string(b.size());
+    for (size_t blk = 0; blk * bs < a.size(); ++blk) {
+        size_t nd = 0, first = SIZE_MAX;
+        for (size_t o = blk * bs; o < std::min(a.size(), (blk + 1) * bs); ++o)
+            if (a[o] != b[o]) {
+                ++nd;
+                if (first == SIZE_MAX) first = o - blk * bs;
+            }
+        if (nd)
+            r += "\n  block " + std::to_string(blk) + ": " + std::to_string(nd) + " bytes differ, first at " +
+                 std::to_string(first) + " (shard " + std::to_string(first / S) + " + " + std::to_string(first % S) + ")";
+    }
+    return r;
+}
+
 #define CHECK(cond)                                                                     \
     do {                                                                                \
         if (!(cond)) throw Failure{std::string(#cond) + " (line " + std::to_string(__LINE__) + ")"}; \
+    } while (0)
+// Equality with a diagnostic: per block of bs bytes, the number of differing
+// bytes and the first differing offset (and its shard of size S).
+#define CHECK_SAME(a, b, bs, S)                                                          \
+    do {                                                                                \
+        if ((a) != (b)) throw Failure{std::string(#a " == " #b) + " (line " + std::to_string(__LINE__) + ")" + \
+                                      diff_report(a, b, bs, S)};                       \
     } while (0)
 #define CHECK_OK(st)                                                                    \
     do {                                                                                \
@@ -518,7 +542,7 @@ void test_virtual_file_batched_reconstruct() {
     CHECK_OK(vf.read(0, rb.data(), rb.size(), &n));
     CHECK(n == in.size());
     CHECK(vf.last_load.blocks == nblk);   // every block needed a reconstruct, one batch
-    CHECK(rb == in);
+    CHECK_SAME(rb, in, bs, calculate_shard_size(bs, 8));
     // the flush after the repair rewrites the lost shard files
     CHECK_OK(vf.drop_buffers());
     for (size_t i = 0; i < nblk; ++i)
