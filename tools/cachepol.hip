@@ -25,7 +25,8 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // LA / SA: load / store aux bits for buffer ops; -1 = global nontemporal builtin.
 // T > 0: the reconstruct layout -- one [B][T][S] shard array, block j reads
-// shards 0..K of it except e = j % K and writes shard e (R = 1).
+// shards 0..K of it except e = j % K and writes shard e (R = 1).  T < 0: the
+// same reads, shard e written to the same place of a second [B][-T][S] array.
 template <int K, int R, int LA, int SA, int T = 0>
 __global__ __launch_bounds__(256) void probe(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, uint64_t S,
                                              uint64_t tiles_per_block) {
@@ -33,8 +34,9 @@ __global__ __launch_bounds__(256) void probe(const uint8_t* __restrict__ in, uin
     const uint64_t j = tile / tiles_per_block;
     const uint32_t col = uint32_t((tile - j * tiles_per_block) * 4096ull + threadIdx.x * 16);
     const uint32_t e = uint32_t(j % K);
-    const uint8_t* ib = T ? out + j * T * S : in + j * K * S;
-    uint8_t* ob = T ? out + j * T * S + e * S : out + j * R * S;
+    constexpr int AT = T < 0 ? -T : T;
+    const uint8_t* ib = T ? out + j * AT * S : in + j * K * S;
+    uint8_t* ob = T > 0 ? out + j * T * S + e * S : T < 0 ? const_cast<uint8_t*>(in) + j * AT * S + e * S : out + j * R * S;
     __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc((void*)ib, 0, 0x7fffffff, 0x00020000);
     __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc((void*)ob, 0, 0x7fffffff, 0x00020000);
     u32x4 acc[R];
@@ -81,7 +83,7 @@ void run(const uint8_t* in, uint8_t* out, uint64_t S, uint64_t B, int iters) {
     const double tbps = double(B) * (K + R) * S / (ms * 1e-3) / 1e12;
     std::printf("{\"pattern\": \"%din%dout%s\", \"load_aux\": %d, \"store_aux\": %d, \"ms\": %.4f, \"TBps\": %.3f, "
                 "\"frac\": %.4f}\n",
-                K, R, T ? "_in_place" : "", LA, SA, ms, tbps, tbps / 8.0);
+                K, R, T > 0 ? "_in_place" : T < 0 ? "_sparse_out" : "", LA, SA, ms, tbps, tbps / 8.0);
     std::fflush(stdout);
     CK(hipEventDestroy(e0));
     CK(hipEventDestroy(e1));
@@ -115,9 +117,9 @@ int main(int argc, char** argv) {
         return 2;
     }
     uint8_t *in, *out;
-    CK(hipMalloc(&in, B * 8 * S));
+    CK(hipMalloc(&in, B * 11 * S));
     CK(hipMalloc(&out, B * 11 * S));
-    CK(hipMemset(in, 0x5a, B * 8 * S));
+    CK(hipMemset(in, 0x5a, B * 11 * S));
     CK(hipMemset(out, 0x33, B * 11 * S));
     for (int i = 0; i < 300; ++i) probe<8, 3, -1, -1><<<uint32_t(S / 4096 * B), 256>>>(in, out, S, S / 4096);   // clock ramp
     CK(hipDeviceSynchronize());
@@ -125,6 +127,7 @@ int main(int argc, char** argv) {
         pattern<8, 3>(in, out, S, B, iters);
         pattern<8, 1>(in, out, S, B, iters);
         pattern<8, 1, 11>(in, out, S, B, iters);
+        pattern<8, 1, -11>(in, out, S, B, iters);
     }
     CK(hipFree(in));
     CK(hipFree(out));
