@@ -180,6 +180,40 @@ class ReedSolomon:
 
     # -- device-resident batches (torch tensors on the GPU) ------------------------
     @staticmethod
+    def _check_batch_tensor(t, rows: int, shard_pitch: int, shard_len: int) -> None:
+        """Bounds of one [B, rows, pitch] / [B, rows*pitch] batch tensor, checked
+        before the launch: the C ABI takes raw pointers and pitches and cannot
+        see the allocation, so a short tensor would be an out-of-bounds kernel
+        access.  Order: dtype, shard count, shard size, then memory kind."""
+        import torch
+        if not isinstance(t, torch.Tensor) or t.dtype != torch.uint8:
+            raise TypeError("batch tensors must be torch.uint8")
+        if t.dim() == 3:
+            if t.shape[1] != rows:
+                raise Error(-1 if t.shape[1] < rows else -2)     # TooFewShards / TooManyShards
+            if t.stride(2) != 1:
+                raise TypeError("shard bytes must be contiguous (stride 1 in the last dimension)")
+            extent = (t.shape[1] - 1) * t.stride(1) + t.shape[2]
+        elif t.dim() == 2:
+            if t.stride(1) != 1:
+                raise TypeError("block bytes must be contiguous (stride 1 in the last dimension)")
+            extent = t.shape[1]
+        else:
+            raise TypeError("batch tensors are [blocks, shards, bytes] or [blocks, shards * bytes]")
+        if shard_len <= 0 and t.shape[0] > 0:
+            raise Error(-11)                                     # EmptyShard
+        if shard_pitch < 0 or (rows - 1) * shard_pitch + shard_len > extent:
+            raise Error(-9)                                      # IncorrectShardSize
+
+    @staticmethod
+    def _check_addressable(*tensors) -> None:
+        """After the shape checks of every operand: the GPU must be able to
+        address them (device memory, or pinned host memory for zero-copy)."""
+        for t in tensors:
+            if not (t.is_cuda or t.is_pinned()):
+                raise TypeError("batch tensors must be on the GPU or in pinned host memory")
+
+    @staticmethod
     def _stream_and_device(t):
         import torch
         dev = t.device.index if t.device.index is not None else torch.cuda.current_device()
@@ -196,6 +230,11 @@ class ReedSolomon:
         dsp = data_shard_pitch if data_shard_pitch is not None else (data.stride(1) if data.dim() == 3 else dbp // self.data_shard_count())
         psp = parity_shard_pitch if parity_shard_pitch is not None else (parity.stride(1) if parity.dim() == 3 else pbp // self.parity_shard_count())
         L = shard_len if shard_len is not None else dsp
+        if parity.shape[0] != B:
+            raise ValueError(f"data has {B} blocks, parity {parity.shape[0]}")
+        self._check_batch_tensor(data, self.data_shard_count(), dsp, L)
+        self._check_batch_tensor(parity, self.parity_shard_count(), psp, L)
+        self._check_addressable(data, parity)
         dev, stream = self._stream_and_device(data)
         _check(lib().shmr_ec_encode_batch_dev(self._h, ctypes.c_void_p(data.data_ptr()), dsp, dbp,
                                               ctypes.c_void_p(parity.data_ptr()), psp, pbp, B, L, dev, stream))
@@ -203,9 +242,16 @@ class ReedSolomon:
     def reconstruct_batch_dev(self, shards, present: np.ndarray, shard_len: Optional[int] = None,
                               data_only: bool = False) -> None:
         """shards: uint8 [B, total, pitch] on the GPU; present: host bool/uint8 [B, total]."""
-        B, t = shards.shape[0], shards.shape[1]
-        pr = np.ascontiguousarray(present, dtype=np.uint8).reshape(B, t)
+        if shards.dim() != 3:
+            raise TypeError("shards must be a [blocks, total, bytes] tensor")
+        B, t = shards.shape[0], self.total_shard_count()
         L = shard_len if shard_len is not None else shards.stride(1)
+        self._check_batch_tensor(shards, t, shards.stride(1), L)
+        pr = np.ascontiguousarray(present, dtype=np.uint8)
+        if pr.size != B * t:
+            raise ValueError(f"present must hold {B} x {t} flags")
+        pr = pr.reshape(B, t)
+        self._check_addressable(shards)
         dev, stream = self._stream_and_device(shards)
         _check(lib().shmr_ec_reconstruct_batch_dev(self._h, ctypes.c_void_p(shards.data_ptr()), shards.stride(1),
                                                    shards.stride(0), _ptr(pr), B, L, int(data_only), dev, stream))

@@ -252,6 +252,47 @@ def test_host_register_rejects_non_contiguous():
         shmr_amd.host_register(np.zeros(0, np.uint8))
 
 
+def test_batch_tensor_bounds_checked_before_launch():
+    """The device-batch shim checks dtype, shard count and shard size against the
+    tensors before the raw-pointer ABI call (a short tensor would be an
+    out-of-bounds kernel access), then refuses memory the GPU cannot address."""
+    import torch
+    rs = shmr_amd.ReedSolomon(4, 2)
+    data = torch.zeros((3, 4, 1024), dtype=torch.uint8)
+    parity = torch.zeros((3, 2, 1024), dtype=torch.uint8)
+    with pytest.raises(TypeError):
+        rs.encode_batch_dev(data.float(), parity)
+    with pytest.raises(shmr_amd.Error) as e:
+        rs.encode_batch_dev(data[:, :3], parity)
+    assert e.value.name == "TooFewShards"
+    with pytest.raises(shmr_amd.Error) as e:
+        rs.encode_batch_dev(data, torch.zeros((3, 3, 1024), dtype=torch.uint8))
+    assert e.value.name == "TooManyShards"
+    with pytest.raises(shmr_amd.Error) as e:
+        rs.encode_batch_dev(data, parity, shard_len=1025)
+    assert e.value.name == "IncorrectShardSize"
+    with pytest.raises(shmr_amd.Error) as e:                     # 2-D block rows too short for the pitch
+        rs.encode_batch_dev(torch.zeros((3, 4000), dtype=torch.uint8), parity, shard_len=1000,
+                            data_shard_pitch=1024)
+    assert e.value.name == "IncorrectShardSize"
+    with pytest.raises(ValueError):
+        rs.encode_batch_dev(data, parity[:2])
+    with pytest.raises(TypeError):                               # well formed, but pageable host memory
+        rs.encode_batch_dev(data, parity, shard_len=1000)
+    shards = torch.zeros((3, 6, 1024), dtype=torch.uint8)
+    present = np.ones((3, 6), np.uint8)
+    with pytest.raises(shmr_amd.Error) as e:
+        rs.reconstruct_batch_dev(shards[:, :5], present[:, :5])
+    assert e.value.name == "TooFewShards"
+    with pytest.raises(shmr_amd.Error) as e:
+        rs.reconstruct_batch_dev(shards, present, shard_len=2048)
+    assert e.value.name == "IncorrectShardSize"
+    with pytest.raises(ValueError):
+        rs.reconstruct_batch_dev(shards, present[:2])
+    with pytest.raises(TypeError):
+        rs.reconstruct_batch_dev(shards, present)
+
+
 def test_path_stats_api():
     z, s = shmr_amd.path_stats()
     assert z >= 0 and s >= 0
