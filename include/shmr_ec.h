@@ -194,7 +194,10 @@ int shmr_ec_set_device(shmr_ec_t* rs, int device);
  * single zero-copy launch instead of per-shard DMA copies (default 8192; 0
  * disables).  "mirror_zc" (0/1, default 1): pageable host batches are
  * gathered into a pinned mirror that the kernel codes in place across PCIe
- * (zero-copy) instead of DMA-ing it to device staging.
+ * (zero-copy) instead of DMA-ing it to device staging.  "ptrs_direct"
+ * (default 16): zero-copy launches of at most this many 4 KiB tiles read
+ * their shard-pointer table from pinned host memory in place instead of
+ * uploading it first (0: always upload).
  * "chunks", "nt_load", "nt_store", "depth", "occ", "early", "spre" and "fuse_tail" default to -2 (auto): a per-shape policy
  * of the fastest variants measured on MI355X; any other value pins the knob,
  * and setting -2 returns it to the policy. */

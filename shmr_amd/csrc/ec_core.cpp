@@ -16,6 +16,7 @@ namespace core {
 namespace {
 
 constexpr int kBounceKibDefault = 8192;   // measured: see bounce_limit()
+constexpr int kPtrsDirectDefault = 16;    // tiles; measured: see ptrs_direct_max()
 
 struct Tuning {
     std::atomic<int> u{kAuto};
@@ -36,6 +37,7 @@ struct Tuning {
 Tuning g_tune[2];   // [kEncode], [kDecode]
 std::atomic<int> g_bounce_kib{kBounceKibDefault};
 std::atomic<int> g_mirror_zc{1};
+std::atomic<int> g_ptrs_direct{kPtrsDirectDefault};
 
 // Measured (tools/tune.py, interleaved A/B in one process): a register ring
 // of depth 2 (one shard of loads in flight per wave) beats depth 3 on every
@@ -111,6 +113,11 @@ int set_tuning(const char* key, int value) {
         g_mirror_zc = value == kAuto ? 1 : (value != 0);
         return SHMR_EC_OK;
     }
+    if (k == "ptrs_direct") {
+        if (value < 0 && value != kAuto) return SHMR_EC_INVALID_ARGUMENT;
+        g_ptrs_direct = value == kAuto ? kPtrsDirectDefault : value;
+        return SHMR_EC_OK;
+    }
     for (int i = first; i <= last; ++i) {
         Tuning& T = g_tune[i];
         if (k == "chunks") {
@@ -161,6 +168,7 @@ int get_tuning(const char* key) {
     const Tuning& T = g_tune[first];
     if (k == "bounce_kib") return g_bounce_kib;
     if (k == "mirror_zc") return g_mirror_zc;
+    if (k == "ptrs_direct") return g_ptrs_direct;
     if (k == "chunks") return T.u;
     if (k == "nt_load") return T.nt_load;
     if (k == "nt_store") return T.nt_store;
@@ -202,6 +210,8 @@ int grid_mode(OpClass op) { return g_tune[op].grid.load(); }
 uint64_t bounce_limit() { return uint64_t(g_bounce_kib.load()) << 10; }
 
 bool mirror_zero_copy() { return g_mirror_zc.load() != 0; }
+
+uint64_t ptrs_direct_max() { return uint64_t(g_ptrs_direct.load()); }
 
 kern::Variant launch_variant(OpClass op, unsigned k, unsigned rows, bool host_mapped, bool ptrs, bool segs) {
     kern::Variant v = resolve_variant(op, k, rows, host_mapped);
@@ -544,6 +554,9 @@ UploadRing* UploadRing::for_device(int dev, int* rc, Kind kind) {
         for (int i = 0; i < kSlots; ++i)
             if (hipEventCreateWithFlags(&ring->ev_[i], hipEventDisableTiming) != hipSuccess)
                 return give_up(SHMR_EC_DEVICE_ERROR);
+        void* hd = nullptr;
+        ring->host_unified_ = hipHostGetDevicePointer(&hd, ring->host_, 0) == hipSuccess && hd == ring->host_;
+        if (!ring->host_unified_) (void)hipGetLastError();
         r = ring;
     }
     *rc = SHMR_EC_OK;

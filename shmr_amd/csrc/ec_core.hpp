@@ -49,6 +49,11 @@ uint64_t bounce_limit();
 // Pageable host batches: code the pinned mirror in place (zero-copy) instead
 // of DMA-ing it to device staging (knob "mirror_zc").
 bool mirror_zero_copy();
+// Zero-copy launches of at most this many 4 KiB tiles (blocks x tiles per
+// shard) read their shard-pointer table straight from the pinned upload slot
+// across PCIe instead of uploading it first (knob "ptrs_direct"; 0 = always
+// upload).
+uint64_t ptrs_direct_max();
 
 // ---- devices --------------------------------------------------------------
 int device_count();
@@ -142,9 +147,16 @@ public:
     int acquire(uint8_t** host, uint8_t** dev, int* slot);
     int upload(int slot, size_t bytes, hipStream_t stream);
     int release_after(int slot, hipStream_t stream);
+    // Device address of the slot's pinned HOST copy (kernels can read the
+    // table across PCIe without an upload), or nullptr if the host ring is not
+    // mapped at the same address.
+    const uint8_t* host_view(int slot) const {
+        return host_unified_ ? host_ + size_t(slot) * kSlotBytes : nullptr;
+    }
 
 private:
     void release_now(int slot);
+    bool host_unified_ = false;
     uint8_t* host_ = nullptr;
     uint8_t* dev_ = nullptr;
     hipEvent_t ev_[kSlots] = {};

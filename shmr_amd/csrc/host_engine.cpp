@@ -316,9 +316,15 @@ int run_mapped(const HostJob& job, const std::vector<uint64_t>& dptrs, bool alig
             uint64_t* tab = reinterpret_cast<uint64_t*>(hslot);
             for (size_t j = 0; j < n; ++j)
                 std::memcpy(tab + j * t, dptrs.data() + mine[c0 + j] * t, t * sizeof(uint64_t));
-            rc = ring->upload(slot, n * t * sizeof(uint64_t), stream);
+            // small launches (few 4 KiB tiles) read the table from the pinned slot
+            // itself: no H2D copy in front of the kernel.  Larger ones upload it --
+            // every workgroup reads its block's table, and across PCIe that costs
+            // concurrent per-block calls 1-4 % of throughput.
+            const uint64_t tiles = n * ((job.len + 4095) / 4096);
+            const uint8_t* direct = tiles <= ptrs_direct_max() ? ring->host_view(slot) : nullptr;
+            if (!direct) rc = ring->upload(slot, n * t * sizeof(uint64_t), stream);
             Layout L{nullptr, nullptr, 0, 0, 0, 0, 0};
-            L.d_ptrs = reinterpret_cast<const uint64_t*>(dslot);
+            L.d_ptrs = reinterpret_cast<const uint64_t*>(direct ? direct : dslot);
             L.total = t;
             L.ptrs_aligned = aligned;
             L.host_mapped = true;

@@ -27,9 +27,11 @@ from shmr_amd._native import _u8p, lib  # noqa: E402
 def main():
     k, p = 8, 3
     out = []
-    cases = [(True, None), (False, 0), (False, 65536)]   # mapped; pageable staged; pageable bounced
+    # mapped (pointer table read in place / uploaded); pageable staged; pageable bounced
+    cases = [(True, None, -2), (True, None, 0), (False, 0, -2), (False, 65536, -2)]
     for S in (4096, 524288):
-        for mapped, bounce in cases:
+        for mapped, bounce, direct in cases:
+            shmr_amd.set_tuning(ptrs_direct=direct)
             if bounce is not None:
                 shmr_amd.set_tuning(bounce_kib=bounce)
             if mapped:
@@ -55,12 +57,13 @@ def main():
                     call()
                     ts.append(time.perf_counter() - t0)
                 rec = {"call": name, "shard_bytes": S,
-                       "buffers": "mapped" if mapped else ("pageable, bounced" if bounce else "pageable, staged DMA"),
+                       "buffers": ("mapped" + ("" if direct else ", pointer table uploaded")) if mapped else
+                                  ("pageable, bounced" if bounce else "pageable, staged DMA"),
                        "median_us": round(float(np.median(ts)) * 1e6, 1), "p10_us": round(float(np.percentile(ts, 10)) * 1e6, 1)}
                 out.append(rec)
                 print(json.dumps(rec), flush=True)
             del keep
-    shmr_amd.set_tuning(bounce_kib=-2)
+    shmr_amd.set_tuning(bounce_kib=-2, ptrs_direct=-2)
     # the reference's shape: per-block encode calls from 8 threads, pageable 4 MiB blocks
     from concurrent.futures import ThreadPoolExecutor
     S = 524288
