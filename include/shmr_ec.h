@@ -99,7 +99,10 @@ int shmr_ec_reconstruct_plan(shmr_ec_t* rs, const uint8_t* present, size_t nshar
  * shards[data..total) are overwritten with parity.  shard_lens[i] is the
  * length of shards[i]; the crate's checks run first and in its order
  * (count -> TOO_FEW/TOO_MANY_SHARDS, len 0 -> EMPTY_SHARD, unequal ->
- * INCORRECT_SHARD_SIZE).  H2D, kernel, D2H on the context's device. */
+ * INCORRECT_SHARD_SIZE).  Runs on the context's device: in place across
+ * PCIe if the shards are mapped host memory (shmr_ec_host_alloc /
+ * shmr_ec_host_register, zero-copy), else through a pooled mapped bounce
+ * buffer (blocks up to "bounce_kib") or per-shard DMA staging. */
 int shmr_ec_encode(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_lens, size_t nshards);
 
 /* ReedSolomon::reconstruct / reconstruct_data (src/vfs/block.rs:560).
@@ -141,9 +144,11 @@ int shmr_ec_reconstruct_batch_dev(shmr_ec_t* rs, uint8_t* d_shards, size_t shard
  * blocks round-robin across `devices` (block b -> devices[b % ndev]); per
  * device the H2D copy, the kernel and the D2H copy of successive chunks
  * overlap on separate streams.  host_shards[b * total + i] points at shard i
- * of block b, each shard_len bytes.  Pinned buffers (shmr_ec_host_alloc) are
- * DMA'd directly; pageable ones are staged through pinned memory by a crew of
- * copy threads.  Synchronous; every block is validated before device work. */
+ * of block b, each shard_len bytes.  Mapped buffers (shmr_ec_host_alloc /
+ * shmr_ec_host_register) are coded in place across PCIe (zero-copy); other
+ * pinned buffers are DMA'd; pageable ones are gathered into a mapped pinned
+ * mirror by a crew of copy threads and coded there ("mirror_zc").
+ * Synchronous; every block is validated before device work. */
 int shmr_ec_encode_blocks_host(shmr_ec_t* rs, uint8_t* const* host_shards, size_t nblocks,
                                size_t shard_len, const int* devices, int ndev);
 
