@@ -202,7 +202,9 @@ int shmr_ec_set_device(shmr_ec_t* rs, int device);
  * (zero-copy) instead of DMA-ing it to device staging.  "ptrs_direct"
  * (default 16): zero-copy launches of at most this many 4 KiB tiles read
  * their shard-pointer table from pinned host memory in place instead of
- * uploading it first (0: always upload).
+ * uploading it first (0: always upload).  "sync_spin_us" (default 0): the
+ * single-call and zero-copy paths poll their stream this long before a
+ * blocking synchronize.
  * "chunks", "nt_load", "nt_store", "depth", "occ", "early", "spre" and "fuse_tail" default to -2 (auto): a per-shape policy
  * of the fastest variants measured on MI355X; any other value pins the knob,
  * and setting -2 returns it to the policy. */

@@ -285,7 +285,7 @@ int shmr_ec_encode(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_le
         if (rc) return rc;
         for (unsigned r = 0; r < p; ++r)
             SHMR_HIP_TRY(hipMemcpyAsync(shards[k + r], s.dbuf + (k + r) * pitch, len, hipMemcpyDeviceToHost, s.stream));
-        SHMR_HIP_TRY(hipStreamSynchronize(s.stream));
+        SHMR_HIP_TRY(core::sync_stream(s.stream));
         return SHMR_EC_OK;
     });
 }
@@ -352,7 +352,7 @@ int shmr_ec_reconstruct(shmr_ec_t* rs, uint8_t* const* shards, const size_t* sha
             const unsigned idx = plan->out_idx[m];
             SHMR_HIP_TRY(hipMemcpyAsync(shards[idx], s.dbuf + idx * pitch, len, hipMemcpyDeviceToHost, s.stream));
         }
-        SHMR_HIP_TRY(hipStreamSynchronize(s.stream));
+        SHMR_HIP_TRY(core::sync_stream(s.stream));
         return SHMR_EC_OK;
     });
 }

@@ -2,6 +2,7 @@
 #include "ec_core.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <string>
 
@@ -17,6 +18,7 @@ namespace {
 
 constexpr int kBounceKibDefault = 8192;   // measured: see bounce_limit()
 constexpr int kPtrsDirectDefault = 16;    // tiles; measured: see ptrs_direct_max()
+constexpr int kSyncSpinDefault = 0;       // us; measured: see sync_stream()
 
 struct Tuning {
     std::atomic<int> u{kAuto};
@@ -38,6 +40,7 @@ Tuning g_tune[2];   // [kEncode], [kDecode]
 std::atomic<int> g_bounce_kib{kBounceKibDefault};
 std::atomic<int> g_mirror_zc{1};
 std::atomic<int> g_ptrs_direct{kPtrsDirectDefault};
+std::atomic<int> g_sync_spin{kSyncSpinDefault};
 
 // Measured (tools/tune.py, interleaved A/B in one process): a register ring
 // of depth 2 (one shard of loads in flight per wave) beats depth 3 on every
@@ -118,6 +121,11 @@ int set_tuning(const char* key, int value) {
         g_ptrs_direct = value == kAuto ? kPtrsDirectDefault : value;
         return SHMR_EC_OK;
     }
+    if (k == "sync_spin_us") {
+        if (value < 0 && value != kAuto) return SHMR_EC_INVALID_ARGUMENT;
+        g_sync_spin = value == kAuto ? kSyncSpinDefault : value;
+        return SHMR_EC_OK;
+    }
     for (int i = first; i <= last; ++i) {
         Tuning& T = g_tune[i];
         if (k == "chunks") {
@@ -169,6 +177,7 @@ int get_tuning(const char* key) {
     if (k == "bounce_kib") return g_bounce_kib;
     if (k == "mirror_zc") return g_mirror_zc;
     if (k == "ptrs_direct") return g_ptrs_direct;
+    if (k == "sync_spin_us") return g_sync_spin;
     if (k == "chunks") return T.u;
     if (k == "nt_load") return T.nt_load;
     if (k == "nt_store") return T.nt_store;
@@ -212,6 +221,18 @@ uint64_t bounce_limit() { return uint64_t(g_bounce_kib.load()) << 10; }
 bool mirror_zero_copy() { return g_mirror_zc.load() != 0; }
 
 uint64_t ptrs_direct_max() { return uint64_t(g_ptrs_direct.load()); }
+
+hipError_t sync_stream(hipStream_t stream) {
+    const int spin = g_sync_spin.load();
+    if (spin > 0) {
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin);
+        do {
+            const hipError_t e = hipStreamQuery(stream);
+            if (e != hipErrorNotReady) return e;
+        } while (std::chrono::steady_clock::now() < until);
+    }
+    return hipStreamSynchronize(stream);
+}
 
 kern::Variant launch_variant(OpClass op, unsigned k, unsigned rows, bool host_mapped, bool ptrs, bool segs) {
     kern::Variant v = resolve_variant(op, k, rows, host_mapped);

@@ -54,6 +54,10 @@ bool mirror_zero_copy();
 // across PCIe instead of uploading it first (knob "ptrs_direct"; 0 = always
 // upload).
 uint64_t ptrs_direct_max();
+// Waits for `stream`: polls it for up to the "sync_spin_us" knob before a
+// blocking hipStreamSynchronize (short single-block calls finish within the
+// spin and skip the blocking wake-up).
+hipError_t sync_stream(hipStream_t stream);
 
 // ---- devices --------------------------------------------------------------
 int device_count();

@@ -341,7 +341,7 @@ int run_mapped(const HostJob& job, const std::vector<uint64_t>& dptrs, bool alig
             const int rc2 = ring->release_after(slot, stream);
             if (rc == SHMR_EC_OK) rc = rc2;
         }
-        if (hipStreamSynchronize(stream) != hipSuccess && rc == SHMR_EC_OK) rc = SHMR_EC_DEVICE_ERROR;
+        if (sync_stream(stream) != hipSuccess && rc == SHMR_EC_OK) rc = SHMR_EC_DEVICE_ERROR;
         result = rc;
     };
     std::vector<std::thread> th;

@@ -29,6 +29,8 @@ def main():
     out = []
     # mapped (pointer table read in place / uploaded); pageable staged; pageable bounced
     cases = [(True, None, -2), (True, None, 0), (False, 0, -2), (False, 65536, -2)]
+    spin = int(os.environ.get("SPIN", "-2"))
+    shmr_amd.set_tuning(sync_spin_us=spin)
     for S in (4096, 524288):
         for mapped, bounce, direct in cases:
             shmr_amd.set_tuning(ptrs_direct=direct)
