@@ -108,6 +108,36 @@ def test_reconstruct_blocks_zero_copy_mixed(gpu, k, p, S, data_only):
                 assert np.array_equal(blocks[b][i], full[b][i]), (b, i)
 
 
+@pytest.mark.parametrize("direct", [0, 1 << 20])
+@pytest.mark.parametrize("k,p,S,B", [(8, 3, 4096, 1), (8, 3, 12288 + 48, 3), (10, 4, 1677722, 2)])
+def test_pointer_table_in_place_or_uploaded(gpu, direct, k, p, S, B):
+    """Shard-pointer tables read in place from the pinned ring slot (ptrs_direct
+    large) or uploaded first (ptrs_direct 0): same bytes either way."""
+    rng = np.random.default_rng([k, S, B, direct])
+    buf, blocks = pinned_blocks(rng, k, p, S, B)
+    rs = shmr_amd.ReedSolomon(k, p)
+    try:
+        shmr_amd.set_tuning(ptrs_direct=direct)
+        with Delta() as d:
+            rs.encode_blocks_host(blocks, devices=[0])
+        assert (d.zero_copy, d.staged) == (B, 0)
+        for blk in blocks:
+            for got, want in zip(blk[k:], oracle_parity(k, p, blk[:k])):
+                assert np.array_equal(got, want)
+        full = [[x.copy() for x in blk] for blk in blocks]
+        present = np.ones((B, k + p), np.uint8)
+        for b in range(B):
+            present[b, [b % k, k + (b % p)]] = 0
+            blocks[b][b % k][:] = 0
+            blocks[b][k + (b % p)][:] = 0
+        rs.reconstruct_blocks_host(blocks, present, devices=[0])
+        for b in range(B):
+            for i in range(k + p):
+                assert np.array_equal(blocks[b][i], full[b][i]), (b, i)
+    finally:
+        shmr_amd.set_tuning(ptrs_direct=-2)
+
+
 def test_single_block_calls_zero_copy(gpu):
     """The drop-in per-block calls (shmr_ec_encode / shmr_ec_reconstruct) on
     mapped shards: in place, no staging."""
