@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="encode83", choices=sorted(CONFIGS))
-    ap.add_argument("--blocks", type=int, default=0, help="blocks per GPU (default: 512 for 4 MiB, 64 for 16 MiB)")
+    ap.add_argument("--blocks", type=int, default=0, help="blocks per GPU (default: 1024 for 1 MiB, 512 for 4 MiB, 64 for 16 MiB blocks)")
     ap.add_argument("--tune", default="", help="kernel knobs, e.g. 'chunks=2,grid=0' (default: library defaults)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the cpu_baseline sample")
@@ -92,7 +92,7 @@ def main():
 
     k, p, block_bytes, erasures = CONFIGS[args.config]
     S = shmr_amd.calculate_shard_size(block_bytes, k)
-    B = args.blocks or (512 if block_bytes <= (4 << 20) else 64)
+    B = args.blocks or (1024 if block_bytes <= (1 << 20) else 512 if block_bytes <= (4 << 20) else 64)
     for kv in filter(None, args.tune.split(",")):
         key, val = kv.split("=")
         shmr_amd.set_tuning(**{key: int(val)})
