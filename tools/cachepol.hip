@@ -27,6 +27,8 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // T > 0: the reconstruct layout -- one [B][T][S] shard array, block j reads
 // shards 0..K of it except e = j % K and writes shard e (R = 1).  T < 0: the
 // same reads, shard e written to the same place of a second [B][-T][S] array.
+// T <= -100: the same reads from a [B][-T-100][S] array, shard e written to a
+// compact [B][1][S] output.
 template <int K, int R, int LA, int SA, int T = 0>
 __global__ __launch_bounds__(256) void probe(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, uint64_t S,
                                              uint64_t tiles_per_block) {
@@ -34,9 +36,12 @@ __global__ __launch_bounds__(256) void probe(const uint8_t* __restrict__ in, uin
     const uint64_t j = tile / tiles_per_block;
     const uint32_t col = uint32_t((tile - j * tiles_per_block) * 4096ull + threadIdx.x * 16);
     const uint32_t e = uint32_t(j % K);
-    constexpr int AT = T < 0 ? -T : T;
+    constexpr int AT = T <= -100 ? -T - 100 : T < 0 ? -T : T;
     const uint8_t* ib = T ? out + j * AT * S : in + j * K * S;
-    uint8_t* ob = T > 0 ? out + j * T * S + e * S : T < 0 ? const_cast<uint8_t*>(in) + j * AT * S + e * S : out + j * R * S;
+    uint8_t* ob = T > 0      ? out + j * T * S + e * S
+                  : T <= -100 ? const_cast<uint8_t*>(in) + j * S
+                  : T < 0     ? const_cast<uint8_t*>(in) + j * AT * S + e * S
+                              : out + j * R * S;
     __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc((void*)ib, 0, 0x7fffffff, 0x00020000);
     __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc((void*)ob, 0, 0x7fffffff, 0x00020000);
     u32x4 acc[R];
@@ -83,7 +88,8 @@ void run(const uint8_t* in, uint8_t* out, uint64_t S, uint64_t B, int iters) {
     const double tbps = double(B) * (K + R) * S / (ms * 1e-3) / 1e12;
     std::printf("{\"pattern\": \"%din%dout%s\", \"load_aux\": %d, \"store_aux\": %d, \"ms\": %.4f, \"TBps\": %.3f, "
                 "\"frac\": %.4f}\n",
-                K, R, T > 0 ? "_in_place" : T < 0 ? "_sparse_out" : "", LA, SA, ms, tbps, tbps / 8.0);
+                K, R, T > 0 ? "_in_place" : T <= -100 ? "_compact_out" : T < 0 ? "_sparse_out" : "", LA, SA, ms, tbps,
+                tbps / 8.0);
     std::fflush(stdout);
     CK(hipEventDestroy(e0));
     CK(hipEventDestroy(e1));
@@ -128,6 +134,7 @@ int main(int argc, char** argv) {
         pattern<8, 1>(in, out, S, B, iters);
         pattern<8, 1, 11>(in, out, S, B, iters);
         pattern<8, 1, -11>(in, out, S, B, iters);
+        pattern<8, 1, -111>(in, out, S, B, iters);
     }
     CK(hipFree(in));
     CK(hipFree(out));
