@@ -1,0 +1,145 @@
+#!/usr/bin/env python3
+"""Randomised multi-threaded soak of the C ABI on one GPU, every result checked
+against the CPU oracle: per-block encode / reconstruct on pageable and mapped
+buffers (zero-copy, bounce, staged DMA), host batches on pageable arrays
+(pinned mirror) and mapped slabs, and device-resident batches on per-thread
+torch streams -- several (k, p) codecs and shard lengths (aligned, tail,
+byte-granular) at once.  Not part of the test suite (minutes of GPU time).
+
+    python tools/soak.py [--seconds 120] [--threads 12]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+import shmr_amd  # noqa: E402
+from oracle import c_oracle  # noqa: E402
+
+SHAPES = [(8, 3, 524288), (8, 3, 4096), (4, 2, 65536 + 16), (10, 4, 100003), (6, 6, 777), (3, 1, 17), (17, 7, 8192)]
+
+
+def oracle_encode(k, p, data):
+    L = len(data[0])
+    sh = [np.ascontiguousarray(d).copy() for d in data] + [np.zeros(L, np.uint8) for _ in range(p)]
+    c_oracle.encode(k, p, sh)
+    return sh
+
+
+def worker(tid, deadline, errors, counts):
+    rng = np.random.default_rng([tid, 2024])
+    stream = torch.cuda.Stream()
+    slab = shmr_amd.PinnedBuffer(4 * 24 * 524288)
+    while time.time() < deadline and not errors:
+        k, p, L = SHAPES[int(rng.integers(0, len(SHAPES)))]
+        rs = shmr_amd.ReedSolomon(k, p)
+        op = int(rng.integers(0, 4))
+        try:
+            if op == 0:        # per-block calls, pageable or mapped
+                mapped = bool(rng.integers(0, 2))
+                if mapped:
+                    arr = slab.array[:(k + p) * L].reshape(k + p, L)
+                    shards = [arr[i] for i in range(k + p)]
+                else:
+                    shards = [np.zeros(L, np.uint8) for _ in range(k + p)]
+                for i in range(k):
+                    shards[i][:] = rng.integers(0, 256, L, dtype=np.uint8)
+                rs.encode(shards)
+                want = oracle_encode(k, p, shards[:k])
+                if not all(np.array_equal(shards[i], want[i]) for i in range(k, k + p)):
+                    errors.append((tid, "encode", k, p, L, mapped))
+                lost = rng.choice(k + p, size=int(rng.integers(1, p + 1)), replace=False)
+                got = [None if i in lost else shards[i].copy() for i in range(k + p)]
+                rs.reconstruct(got)
+                if not all(np.array_equal(got[i], want[i]) for i in range(k + p)):
+                    errors.append((tid, "reconstruct", k, p, L, mapped))
+            elif op == 1:      # host batch on a pageable [B, t, L] array (pinned mirror)
+                B = int(rng.integers(1, 6))
+                blk = np.zeros((B, k + p, L), np.uint8)
+                blk[:, :k] = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+                rs.encode_blocks_host(blk)
+                full = blk.copy()
+                for b in range(B):
+                    want = oracle_encode(k, p, list(blk[b, :k]))
+                    if not all(np.array_equal(blk[b, i], want[i]) for i in range(k, k + p)):
+                        errors.append((tid, "blocks_host encode", k, p, L, B))
+                present = np.ones((B, k + p), np.uint8)
+                for b in range(B):
+                    present[b, rng.choice(k + p, size=int(rng.integers(1, p + 1)), replace=False)] = 0
+                blk[present == 0] = 0
+                rs.reconstruct_blocks_host(blk, present)
+                if not np.array_equal(blk, full):
+                    errors.append((tid, "blocks_host reconstruct", k, p, L, B))
+            elif op == 2:      # host batch on the mapped slab (zero-copy)
+                B = int(min(4, (slab.nbytes // ((k + p) * L))))
+                if B == 0:
+                    continue
+                blk = slab.array[:B * (k + p) * L].reshape(B, k + p, L)
+                blk[:, :k] = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+                rs.encode_blocks_host(blk)
+                for b in range(B):
+                    want = oracle_encode(k, p, list(blk[b, :k]))
+                    if not all(np.array_equal(blk[b, i], want[i]) for i in range(k, k + p)):
+                        errors.append((tid, "mapped batch encode", k, p, L, B))
+            else:              # device-resident batch on this thread's stream
+                B = int(rng.integers(1, 9))
+                P = (L + 255) // 256 * 256
+                with torch.cuda.stream(stream):
+                    d = torch.zeros((B, k + p, P), dtype=torch.uint8, device="cuda")
+                    host = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+                    d[:, :k, :L] = torch.from_numpy(host).cuda()
+                    rs.encode_batch_dev(d[:, :k], d[:, k:], shard_len=L)
+                    present = np.ones((B, k + p), np.uint8)
+                    for b in range(B):
+                        present[b, rng.choice(k + p, size=int(rng.integers(1, p + 1)), replace=False)] = 0
+                    full = d.clone()
+                    d[torch.from_numpy(present == 0).cuda()] = 0
+                    rs.reconstruct_batch_dev(d, present, shard_len=L)
+                    ok = torch.equal(d[:, :, :L], full[:, :, :L])
+                stream.synchronize()
+                h = full.cpu().numpy()
+                for b in range(B):
+                    want = oracle_encode(k, p, list(host[b]))
+                    if not all(np.array_equal(h[b, i, :L], want[i]) for i in range(k, k + p)):
+                        errors.append((tid, "batch_dev encode", k, p, L, B))
+                if not ok:
+                    errors.append((tid, "batch_dev reconstruct", k, p, L, B))
+            counts[tid] += 1
+        except Exception as e:   # surfaced by the main thread
+            errors.append((tid, "exception", op, k, p, L, repr(e)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=120)
+    ap.add_argument("--threads", type=int, default=12)
+    a = ap.parse_args()
+    deadline = time.time() + a.seconds
+    errors, counts = [], [0] * a.threads
+    th = [threading.Thread(target=worker, args=(t, deadline, errors, counts)) for t in range(a.threads)]
+    for t in th:
+        t.start()
+    last = time.time()
+    while any(t.is_alive() for t in th):
+        time.sleep(1)
+        if time.time() - last > 30:
+            print(json.dumps({"progress_ops": sum(counts), "errors": len(errors)}), flush=True)
+            last = time.time()
+    zc, st = shmr_amd.path_stats()
+    print(json.dumps({"ops": sum(counts), "threads": a.threads, "seconds": a.seconds, "errors": errors[:5],
+                      "zero_copy_blocks": zc, "staged_blocks": st}), flush=True)
+    sys.exit(1 if errors else 0)
+
+
+if __name__ == "__main__":
+    main()
