@@ -4,7 +4,9 @@ StorageBlocks, on 1/2/4/8 MI355X (BASELINE.json ``metric``, ``configs[1]``).
 
 A "step" is one pass of the hot path over one batch: encode every block of
 the per-GPU batch (B blocks x 8 data shards x 524,288 B) into 3 parity shards,
-inputs already resident in HBM.  Multi-GPU: one process per GPU, whole blocks
+inputs already resident in HBM (``--config`` selects the other BASELINE
+configs: decodes, RS(10,4), RS(4,2), and ``codec104`` = encode + 2-erasure
+rebuild per step).  Multi-GPU: one process per GPU, whole blocks
 round-robin (global block b -> rank b % N), no collectives on the data path
 (only the timing barrier / max-over-ranks reduction).  ``scaling`` is weak.
 
@@ -45,6 +47,8 @@ CONFIGS = {
     "encode104": (10, 4, 16 << 20, None),
     "decode104": (10, 4, 16 << 20, 2),
     "encode42": (4, 2, 1 << 20, None),
+    # BASELINE config 4 as stated: encode, then rebuild 2 erased shards, per step
+    "codec104": (10, 4, 16 << 20, -2),
 }
 
 
@@ -96,9 +100,14 @@ def main():
     for kv in filter(None, args.tune.split(",")):
         key, val = kv.split("=")
         shmr_amd.set_tuning(**{key: int(val)})
+    codec = erasures is not None and erasures < 0
+    if codec:
+        erasures = -erasures
     op = "encode" if erasures is None else "decode"
     rows = p if erasures is None else erasures
     tuning = shmr_amd.describe_variant(op == "decode", k, rows)
+    if codec:
+        tuning = f"encode: {shmr_amd.describe_variant(False, k, p)}; reconstruct: {tuning}"
     rs = shmr_amd.ReedSolomon(k, p)
 
     # Synthetic blocks, generated on the GPU from a per-rank seed (inputs
@@ -130,9 +139,20 @@ def main():
             present[np.arange(B), gb % 10] = 0                     # config 4: {b%10, (b+3)%10}
             present[np.arange(B), (gb + 3) % 10] = 0
 
-        def step():
-            rs.reconstruct_batch_dev(shards, present, shard_len=S)
-        algo_bytes_per_block = (k + erasures) * S
+        if codec:
+            # encode, then rebuild the erased shards in place: two launches per
+            # step, algorithmic bytes of both ((k+p)S + (k+e)S per block)
+            reference = shards[:, :, :S].clone()
+
+            def step():
+                rs.encode_batch_dev(shards[:, :k], shards[:, k:], shard_len=S,
+                                    data_shard_pitch=pitch, parity_shard_pitch=pitch)
+                rs.reconstruct_batch_dev(shards, present, shard_len=S)
+            algo_bytes_per_block = (k + p) * S + (k + erasures) * S
+        else:
+            def step():
+                rs.reconstruct_batch_dev(shards, present, shard_len=S)
+            algo_bytes_per_block = (k + erasures) * S
         payload_bytes_per_block = k * S
     torch.cuda.synchronize(dev)
 
@@ -191,7 +211,9 @@ def main():
                          "decode83": "RS(8,3) reconstruct, 1 missing data shard (b mod 8), 4 MiB blocks",
                          "encode104": "RS(10,4) encode, 16 MiB StorageBlocks, device-resident",
                          "decode104": "RS(10,4) reconstruct, 2 erasures {b mod 10, (b+3) mod 10}, 16 MiB",
-                         "encode42": "RS(4,2) encode, 1 MiB StorageBlocks, device-resident"}[args.config],
+                         "encode42": "RS(4,2) encode, 1 MiB StorageBlocks, device-resident",
+                         "codec104": "RS(10,4) encode + reconstruct of 2 erasures {b mod 10, (b+3) mod 10} "
+                                     "per step, 16 MiB"}[args.config],
             "data_shards": k, "parity_shards": p, "shard_bytes": S, "blocks_per_gpu": B,
             "global_batch_blocks": B * world,
             "parallelism": f"blocks round-robin over {world} GPU(s), no data-path collectives "
@@ -210,8 +232,38 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if codec:
+        # two launches per step: the roofline figures are per step (both launches)
+        out["roofline"]["launches_per_step"] = 2
+        out["roofline"]["algorithmic_bytes_per_step"] = out["roofline"].pop("algorithmic_bytes_per_launch")
+        out["roofline"]["step_ms_avg"] = out["roofline"].pop("kernel_ms_avg")
+        # the timed steps ran over already-consistent blocks: wipe the parity,
+        # encode, wipe the erased shards, rebuild them, and check every shard
+        # against the originals
+        shards[:, k:] = 0
+        rs.encode_batch_dev(shards[:, :k], shards[:, k:], shard_len=S,
+                            data_shard_pitch=pitch, parity_shard_pitch=pitch)
+        shards[torch.from_numpy(present == 0).to(dev)] = 0
+        rs.reconstruct_batch_dev(shards, present, shard_len=S)
+        torch.cuda.synchronize(dev)
+        out["roofline"]["round_trip_bit_exact"] = bool(torch.equal(shards[:, :, :S], reference))
+        del reference
     if rank == 0 and world == 1 and not args.no_cpu:
-        if erasures is None:
+        if codec:
+            enc = cpu_baseline(k, p, S, block_bytes, shards[:, :k], shards[:, k:], args.cpu_seconds / 2)
+            dec = cpu_baseline_decode(k, p, S, shards, present, args.cpu_seconds / 2)
+            rate = 1.0 / (1.0 / enc["value"] + 1.0 / dec["value"])
+            out["cpu_baseline"] = {
+                "value": round(rate, 3), "unit": "GiB/s", "cores": enc["cores"], "kind": "port",
+                "sample": "encode and reconstruct legs timed separately on bounded samples of the same "
+                          "workload, combined as one step: 1 / (1/encode + 1/reconstruct); "
+                          f"encode: {enc['sample']}; reconstruct: {dec['sample']}",
+                "encode_GiBps": enc["value"], "reconstruct_GiBps": dec["value"],
+                "cpu_model": enc["cpu_model"],
+                "gpu_parity_bit_exact_on_sample": enc["gpu_parity_bit_exact_on_sample"],
+                "gpu_rebuilt_bit_exact_on_sample": dec["gpu_rebuilt_bit_exact_on_sample"],
+            }
+        elif erasures is None:
             out["cpu_baseline"] = cpu_baseline(k, p, S, block_bytes, data, parity, args.cpu_seconds)
         else:
             out["cpu_baseline"] = cpu_baseline_decode(k, p, S, shards, present, args.cpu_seconds)
