@@ -37,6 +37,9 @@ def main():
     ap.add_argument("--algo-bytes", type=int, required=True, help="algorithmic bytes per main launch")
     ap.add_argument("--kernel", default="gf_apply_kernel")
     ap.add_argument("--merge", default="")
+    ap.add_argument("--sum-kernels", action="store_true",
+                    help="steps of several launches (codec104: encode + reconstruct): per-step figures = "
+                         "sum over every matching kernel of its average duration / median counter")
     a = ap.parse_args()
 
     stats = rows(os.path.join(a.dir, "kt", "**", "*kernel_stats.csv"))
@@ -46,24 +49,33 @@ def main():
             dur[r["Name"]] = (int(r["Calls"]), float(r["AverageNs"]))
     # dominant = most total time
     main_name = max(dur, key=lambda n: dur[n][0] * dur[n][1]) if dur else None
+    names = sorted(dur) if a.sum_kernels else [main_name]
 
     def counter(name):
-        vals = [float(r["Counter_Value"]) for r in rows(os.path.join(a.dir, name, "**", "*counter_collection.csv"))
-                if r["Kernel_Name"] == main_name and r["Counter_Name"] == name]
-        return statistics.median(vals) if vals else None
+        recs = rows(os.path.join(a.dir, name, "**", "*counter_collection.csv"))
+        total = 0.0
+        for kn in names:
+            vals = [float(r["Counter_Value"]) for r in recs
+                    if r["Kernel_Name"] == kn and r["Counter_Name"] == name]
+            if not vals:
+                return None
+            total += statistics.median(vals)
+        return total
 
     fetch, write = counter("FETCH_SIZE"), counter("WRITE_SIZE")
     rec = {
         "blocks": a.blocks,
-        "kernel": main_name,
+        "kernel": main_name if not a.sum_kernels else names,
         "calls": dur[main_name][0] if main_name else None,
-        "avg_duration_ns": dur[main_name][1] if main_name else None,
+        "avg_duration_ns": (sum(dur[n][1] for n in names) if main_name else None),
         "FETCH_SIZE_KiB": fetch,
         "WRITE_SIZE_KiB": write,
         "read_bytes_per_launch": 2 * fetch * 1024 if fetch is not None else None,
         "write_bytes_per_launch": write * 1024 if write is not None else None,
         "algorithmic_bytes_per_launch": a.algo_bytes,
     }
+    if a.sum_kernels:
+        rec["per"] = "step (sum over the step's launches; *_per_launch keys hold per-step figures)"
     if fetch is not None and write is not None:
         hbm = 2 * fetch * 1024 + write * 1024
         rec["hbm_bytes_per_launch"] = int(hbm)

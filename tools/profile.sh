@@ -2,10 +2,10 @@
 # rocprofv3 passes for one bench config: kernel trace + stats, then one PMC
 # pass per counter (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950),
 # then tools/pmc_traffic.py merges the summary into gpurun_out/pmc_traffic.json.
-# Usage: tools/profile.sh <tag> <config> <blocks> <algo_bytes_per_launch>
+# Usage: tools/profile.sh <tag> <config> <blocks> <algo_bytes_per_launch> [--sum-kernels]
 set -u
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
-TAG=$1; CFG=$2; BLOCKS=$3; ALGO=$4
+TAG=$1; CFG=$2; BLOCKS=$3; ALGO=$4; EXTRA=${5:-}
 OUT="$ROOT/gpurun_out/prof_${TAG}_${CFG}"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
@@ -21,4 +21,4 @@ done
 # merge into a copy of the tracked table (gpurun_out/ is not pushed to the box)
 [ -f "$ROOT/gpurun_out/pmc_traffic.json" ] || cp "$ROOT/profiles/pmc_traffic.json" "$ROOT/gpurun_out/pmc_traffic.json"
 python3 "$ROOT/tools/pmc_traffic.py" "$OUT" --config "$CFG" --blocks "$BLOCKS" --algo-bytes "$ALGO" \
-  --merge "$ROOT/gpurun_out/pmc_traffic.json"
+  --merge "$ROOT/gpurun_out/pmc_traffic.json" $EXTRA

@@ -12,3 +12,4 @@ bash "$D/profile.sh" "$T" decode83 512 2415919104
 bash "$D/profile.sh" "$T" encode104 64 $((64 * 14 * 1677722))
 bash "$D/profile.sh" "$T" decode104 64 $((64 * 12 * 1677722))
 bash "$D/profile.sh" "$T" encode42 1024 1610612736
+bash "$D/profile.sh" "$T" codec104 64 $((64 * 26 * 1677722)) --sum-kernels
