@@ -5,7 +5,8 @@ Two kinds of data, kept apart on purpose:
 
 * kat.json "published" -- known-answer values of the crate the reference calls
   (reed-solomon-erasure 6.0.0, itself a port of Backblaze JavaReedSolomon):
-  galois multiply/exp KATs and the RS(5,5) encode vector.  These pin the
+  galois multiply/exp/slice-multiply KATs, the matrix multiply/invert tests
+  and the RS(5,5) encode vector.  These pin the
   oracle to the upstream algorithm; they are data, not code.
 * everything else -- produced by this repo's CPU oracle (oracle/rs_oracle.py)
   from seeded inputs: parity rows of the BASELINE configs, small blocks in full
@@ -37,6 +38,9 @@ def sha(a: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
+_SLICE_IN = [0, 1, 2, 3, 4, 5, 6, 10, 50, 100, 150, 174, 201, 255, 99, 32, 67, 85]
+
+
 def published_kats():
     return {
         "source": "reed-solomon-erasure 6.0.0 galois_8 tests / Backblaze JavaReedSolomon (published KATs)",
@@ -45,6 +49,20 @@ def published_kats():
         "encode": [{"data_shards": 5, "parity_shards": 5,
                     "data": [[0, 1], [4, 5], [2, 3], [6, 7], [8, 9]],
                     "parity": [[12, 13], [10, 11], [14, 15], [90, 91], [94, 95]]}],
+        # galois slice multiply (upstream test_slice_mul / galMulSlice): [c, in, expected]
+        "mul_slice": [
+            [25, _SLICE_IN, [0x00, 0x19, 0x32, 0x2b, 0x64, 0x7d, 0x56, 0xfa, 0xb8, 0x6d, 0xc7, 0x85, 0xc3,
+                             0x1f, 0x22, 0x07, 0x25, 0xfe]],
+            [177, _SLICE_IN, [0x00, 0xb1, 0x7f, 0xce, 0xfe, 0x4f, 0x81, 0x9e, 0x03, 0x06, 0xe8, 0x75, 0xbd,
+                              0x40, 0x36, 0xa3, 0x95, 0xcb]],
+        ],
+        # matrix tests (upstream MatrixTest / matrix.rs tests): [a, b, a*b] and [m, inv(m)]
+        "mat_mul": [[[[1, 2], [3, 4]], [[5, 6], [7, 8]], [[11, 22], [19, 42]]]],
+        "mat_invert": [
+            [[[56, 23, 98], [3, 100, 200], [45, 201, 123]], [[175, 133, 33], [130, 13, 245], [112, 35, 126]]],
+            [[[1, 0, 0, 0, 0], [0, 1, 0, 0, 0], [0, 0, 0, 1, 0], [0, 0, 0, 0, 1], [7, 7, 6, 6, 1]],
+             [[1, 0, 0, 0, 0], [0, 1, 0, 0, 0], [123, 123, 1, 122, 122], [0, 0, 1, 0, 0], [0, 0, 0, 1, 0]]],
+        ],
     }
 
 

@@ -50,6 +50,31 @@ def test_encode_kat():
         assert [s.tolist() for s in sh2[k:]] == case["parity"]
 
 
+@pytest.mark.parametrize("c,inp,want", KAT["published"]["mul_slice"])
+def test_mul_slice_kat(c, inp, want):
+    x = np.array(inp, np.uint8)
+    out = np.zeros_like(x)
+    O.mul_slice(c, x, out)
+    assert out.tolist() == want
+    acc = np.array(want, np.uint8)          # mul_slice_xor onto its own product -> zeros
+    O.mul_slice_xor(c, x, acc)
+    assert not acc.any()
+    for variant in (0, 1):                  # scalar table loop and the AVX2 nibble loop (+ byte tail)
+        assert c_oracle.apply(np.array([[c]], np.uint8), [x], len(x), variant=variant)[0].tolist() == want
+
+
+@pytest.mark.parametrize("a,b,want", KAT["published"]["mat_mul"])
+def test_mat_mul_kat(a, b, want):
+    assert O.mat_mul(np.array(a, np.uint8), np.array(b, np.uint8)).tolist() == want
+
+
+@pytest.mark.parametrize("m,want", KAT["published"]["mat_invert"])
+def test_mat_invert_kat(m, want):
+    m = np.array(m, np.uint8)
+    assert O.mat_invert(m).tolist() == want
+    assert c_oracle.invert(m).tolist() == want
+
+
 # ---------------------------------------------------------------- field properties
 def test_field_axioms():
     m = O.MUL_TABLE.astype(np.int64)
