@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--backend", default="gloo", choices=["gloo", "nccl"],
                     help="process group for the timing barrier / max-over-ranks only (the data path "
                          "exchanges nothing between GPUs)")
+    ap.add_argument("--contig", action="store_true",
+                    help="batch buffers in physically contiguous VRAM (shmr_ec_device_alloc) instead of "
+                         "torch's allocator; pays off on multi-GiB batches")
     ap.add_argument("--ramp-seconds", type=float, default=0.5,
                     help="untimed device clock ramp before the warmup steps (MI355X needs ~0.1 s of "
                          "sustained load to reach its steady clock)")
@@ -118,16 +121,28 @@ def main():
     pitch = (S + 255) // 256 * 256
     g = torch.Generator(device=dev)
     g.manual_seed(SEED + rank)
+    bufs = []
+
+    def vram(shape):
+        """Batch tensor: torch's allocator, or with --contig physically
+        contiguous VRAM from shmr_ec_device_alloc (footprint)."""
+        if not args.contig:
+            return torch.empty(shape, dtype=torch.uint8, device=dev)
+        bufs.append(shmr_amd.DeviceBuffer(int(np.prod(shape)), device=dev.index, contiguous=True))
+        return bufs[-1].tensor(shape)
+
     if erasures is None:
-        data = torch.randint(0, 256, (B, k, pitch), dtype=torch.uint8, device=dev, generator=g)
-        parity = torch.empty((B, p, pitch), dtype=torch.uint8, device=dev)
+        data = vram((B, k, pitch))
+        data.copy_(torch.randint(0, 256, (B, k, pitch), dtype=torch.uint8, device=dev, generator=g))
+        parity = vram((B, p, pitch))
 
         def step():
             rs.encode_batch_dev(data, parity, shard_len=S)
         algo_bytes_per_block = (k + p) * S
         payload_bytes_per_block = k * S
     else:
-        shards = torch.zeros((B, k + p, pitch), dtype=torch.uint8, device=dev)
+        shards = vram((B, k + p, pitch))
+        shards.zero_()
         shards[:, :k, :S] = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=dev, generator=g)
         rs.encode_batch_dev(shards[:, :k], shards[:, k:], shard_len=S,
                             data_shard_pitch=pitch, parity_shard_pitch=pitch)
@@ -219,6 +234,7 @@ def main():
             "parallelism": f"blocks round-robin over {world} GPU(s), no data-path collectives "
                            f"({args.backend} only for the timing barrier / max-over-ranks)",
             "tuning": tuning,
+            "memory": "physically contiguous VRAM (shmr_ec_device_alloc)" if args.contig else "torch caching allocator (hipMalloc)",
         },
         "roofline": {
             "bound": "hbm",

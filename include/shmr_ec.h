@@ -174,6 +174,18 @@ void shmr_ec_host_free(void* p);
 int shmr_ec_host_register(void* p, size_t bytes);
 int shmr_ec_host_unregister(void* p);
 
+/* Device memory for block batches (the *_batch_dev entry points), so a caller
+ * (e.g. the Rust shim) needs no HIP bindings of its own.  contiguous == 0 is a
+ * plain hipMalloc; contiguous != 0 asks for physically contiguous VRAM
+ * (hipDeviceMallocContiguous, mapped with large page fragments) and fails
+ * with OUT_OF_MEMORY if the driver cannot supply it (no silent fallback).
+ * Measured on MI355X: contiguous VRAM lifts the XOR-only replica of the
+ * RS(8,3) access pattern over 2,048 blocks (11 GiB) from 76 % to 78.5 % of
+ * HBM peak, but the GF kernel itself runs the same on both (78.8 % at 2,048
+ * blocks, 79.7 % at 512).  Free with shmr_ec_device_free on the same device. */
+int shmr_ec_device_alloc(int device, size_t bytes, int contiguous, void** out);
+int shmr_ec_device_free(int device, void* p);
+
 /* ---- configuration -------------------------------------------------------- */
 
 /* Device used by the host-buffer entry points (default 0). */

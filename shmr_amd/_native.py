@@ -49,6 +49,8 @@ SIGNATURES = [
      [ctypes.c_void_p, _u8pp, _sz, _sz, ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     ("shmr_ec_reconstruct_blocks_host", ctypes.c_int,
      [ctypes.c_void_p, _u8pp, _u8p, _sz, _sz, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    ("shmr_ec_device_alloc", ctypes.c_int, [ctypes.c_int, _sz, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    ("shmr_ec_device_free", ctypes.c_int, [ctypes.c_int, ctypes.c_void_p]),
     ("shmr_ec_host_alloc", ctypes.c_int, [_sz, ctypes.POINTER(ctypes.c_void_p)]),
     ("shmr_ec_host_free", None, [ctypes.c_void_p]),
     ("shmr_ec_host_register", ctypes.c_int, [ctypes.c_void_p, _sz]),

@@ -174,6 +174,40 @@ int shmr_ec_path_stats(uint64_t* zero_copy_blocks, uint64_t* staged_blocks) {
     return SHMR_EC_OK;
 }
 
+// ---- device memory for batches -------------------------------------------------
+int shmr_ec_device_alloc(int device, size_t bytes, int contiguous, void** out) {
+    return guarded([&]() -> int {
+        if (!out) return SHMR_EC_INVALID_ARGUMENT;
+        *out = nullptr;
+        int rc = core::check_device(device);
+        if (rc) return rc;
+        int prev = 0;
+        if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) return SHMR_EC_DEVICE_ERROR;
+        const size_t n = bytes ? bytes : 1;
+        const hipError_t e = contiguous ? hipExtMallocWithFlags(out, n, hipDeviceMallocContiguous) : hipMalloc(out, n);
+        (void)hipSetDevice(prev);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            *out = nullptr;
+            return SHMR_EC_OUT_OF_MEMORY;
+        }
+        return SHMR_EC_OK;
+    });
+}
+
+int shmr_ec_device_free(int device, void* p) {
+    return guarded([&]() -> int {
+        if (!p) return SHMR_EC_OK;
+        int rc = core::check_device(device);
+        if (rc) return rc;
+        int prev = 0;
+        if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) return SHMR_EC_DEVICE_ERROR;
+        const hipError_t e = hipFree(p);
+        (void)hipSetDevice(prev);
+        return e == hipSuccess ? SHMR_EC_OK : SHMR_EC_DEVICE_ERROR;
+    });
+}
+
 // ---- pinned host memory (Block Cache buffers) --------------------------------
 // Mapped + portable: every GPU of the node can address it, so the host-buffer
 // entry points run their kernels on it in place (zero-copy).

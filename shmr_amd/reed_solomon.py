@@ -325,6 +325,45 @@ class PinnedBuffer:
             self._p = None
 
 
+class DeviceBuffer:
+    """VRAM for block batches from shmr_ec_device_alloc; ``contiguous=True``
+    asks for physically contiguous memory (large page fragments: fewer
+    translation misses on multi-GiB batches).  ``tensor(shape)`` views it as
+    a torch.uint8 CUDA tensor (``__cuda_array_interface__``) for the
+    ``*_batch_dev`` entry points; the view keeps the buffer alive."""
+
+    def __init__(self, nbytes: int, device: int = 0, contiguous: bool = True):
+        p = ctypes.c_void_p()
+        _check(lib().shmr_ec_device_alloc(device, nbytes, int(bool(contiguous)), ctypes.byref(p)))
+        self._p = p
+        self.nbytes = nbytes
+        self.device = device
+        self.contiguous = bool(contiguous)
+        self._shape = (nbytes,)
+
+    @property
+    def __cuda_array_interface__(self):
+        return {"shape": self._shape, "typestr": "|u1", "data": (int(self._p.value), False),
+                "version": 2, "strides": None}
+
+    def tensor(self, shape=None):
+        import torch
+        shape = tuple(shape) if shape is not None else (self.nbytes,)
+        if int(np.prod(shape)) > self.nbytes:
+            raise ValueError(f"view of {shape} exceeds the {self.nbytes}-byte buffer")
+        self._shape = shape
+        try:
+            return torch.as_tensor(self, device=torch.device("cuda", self.device))
+        finally:
+            self._shape = (self.nbytes,)
+
+    def __del__(self):
+        p = getattr(self, "_p", None)
+        if p:
+            lib().shmr_ec_device_free(self.device, p)
+            self._p = None
+
+
 def host_register(arr: np.ndarray) -> None:
     """Page-lock and map an existing C-contiguous host array for zero-copy
     use by the host-buffer entry points (shmr_ec_host_register)."""

@@ -177,6 +177,10 @@ def test_compute_without_gpu_fails_loudly():
         rs.encode([np.zeros(4, np.uint8) for _ in range(5)])
     assert e.value.name == "NoDevice"
     assert shmr_amd.device_count() == 0
+    for contiguous in (False, True):
+        with pytest.raises(shmr_amd.Error) as e:
+            shmr_amd.DeviceBuffer(1 << 20, contiguous=contiguous)
+        assert e.value.name == "NoDevice"
 
 
 def test_tuning_api():

@@ -513,3 +513,33 @@ def test_single_block_pageable_paths(gpu, bounce_kib):
                 assert np.array_equal(got[i], shards[i])
     finally:
         shmr_amd.set_tuning(bounce_kib=saved)
+
+
+@pytest.mark.parametrize("contiguous", [False, True])
+def test_encode_reconstruct_in_device_buffer(gpu, contiguous):
+    """Batches in shmr_ec_device_alloc memory (plain and physically contiguous
+    VRAM) viewed as torch tensors: encode + 1-erasure rebuild, bit-exact."""
+    import torch
+    k, p, L, B = 8, 3, 65536, 6
+    buf = shmr_amd.DeviceBuffer(B * (k + p) * L, contiguous=contiguous)
+    shards = buf.tensor((B, k + p, L))
+    assert shards.is_cuda and shards.data_ptr() == buf._p.value
+    g = torch.Generator(device=gpu).manual_seed(7)
+    shards[:, :k] = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=gpu, generator=g)
+    rs = shmr_amd.ReedSolomon(k, p)
+    rs.encode_batch_dev(shards[:, :k], shards[:, k:], shard_len=L, data_shard_pitch=L, parity_shard_pitch=L)
+    torch.cuda.synchronize()
+    host = shards.cpu().numpy()
+    for b in range(B):
+        want = oracle_parity(k, p, [host[b, i] for i in range(k)])
+        for r in range(p):
+            assert np.array_equal(host[b, k + r], want[r])
+    present = np.ones((B, k + p), np.uint8)
+    for b in range(B):
+        present[b, b % k] = 0
+        shards[b, b % k] = 0
+    rs.reconstruct_batch_dev(shards, present, shard_len=L)
+    torch.cuda.synchronize()
+    assert np.array_equal(shards.cpu().numpy(), host)
+    del shards
+    del buf

@@ -6,6 +6,7 @@
 //
 //   hipcc -O3 --offload-arch=gfx950 tools/membench.hip -o tools/_bin/membench
 //   membench [shard_bytes=524288] [blocks=512] [iters=20]
+//   env: MEMBENCH_ALLOC=contig (physically contiguous VRAM), MEMBENCH_ONLY=83
 //
 // Prints one JSON line per (pattern, variant): TB/s of algorithmic bytes
 // (K + R) * S * B and the fraction of the 8 TB/s HBM peak.
@@ -14,6 +15,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -127,8 +129,18 @@ int main(int argc, char** argv) {
     }
     uint8_t *in, *out;
     uint32_t* sink;
-    CK(hipMalloc(&in, B * 10 * S));
-    CK(hipMalloc(&out, B * 4 * S));
+    // MEMBENCH_ALLOC=contig: physically contiguous VRAM (hipDeviceMallocContiguous),
+    // to separate page-translation effects from the access pattern's own ceiling.
+    const char* alloc = std::getenv("MEMBENCH_ALLOC");
+    const bool contig = alloc && std::strcmp(alloc, "contig") == 0;
+    if (contig) {
+        CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&in), B * 10 * S, hipDeviceMallocContiguous));
+        CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&out), B * 4 * S, hipDeviceMallocContiguous));
+    } else {
+        CK(hipMalloc(&in, B * 10 * S));
+        CK(hipMalloc(&out, B * 4 * S));
+    }
+    const char* only = std::getenv("MEMBENCH_ONLY");   // "83": the RS(8,3) encode pattern only
     CK(hipMalloc(&sink, 4));
     CK(hipMemset(in, 0x5a, B * 10 * S));
     CK(hipMemset(out, 0, B * 4 * S));
@@ -137,6 +149,7 @@ int main(int argc, char** argv) {
     CK(hipDeviceSynchronize());
     for (int rep = 0; rep < 2; ++rep) {
         pattern<8, 3>(in, out, S, B, sink, iters);
+        if (only && std::strcmp(only, "83") == 0) continue;
         pattern<8, 1>(in, out, S, B, sink, iters);
         pattern<8, 0>(in, out, S, B, sink, iters);
         pattern<0, 3>(in, out, S, B, sink, iters);
