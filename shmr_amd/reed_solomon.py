@@ -325,6 +325,16 @@ class PinnedBuffer:
             self._p = None
 
 
+class _DeviceView:
+    """One ``__cuda_array_interface__`` view of a DeviceBuffer; the tensor made
+    from it holds this object, which holds the buffer."""
+
+    def __init__(self, buf, shape):
+        self.buf = buf
+        self.__cuda_array_interface__ = {"shape": shape, "typestr": "|u1", "data": (int(buf._p.value), False),
+                                         "version": 2, "strides": None}
+
+
 class DeviceBuffer:
     """VRAM for block batches from shmr_ec_device_alloc; ``contiguous=True``
     asks for physically contiguous memory (large page fragments: fewer
@@ -339,23 +349,13 @@ class DeviceBuffer:
         self.nbytes = nbytes
         self.device = device
         self.contiguous = bool(contiguous)
-        self._shape = (nbytes,)
-
-    @property
-    def __cuda_array_interface__(self):
-        return {"shape": self._shape, "typestr": "|u1", "data": (int(self._p.value), False),
-                "version": 2, "strides": None}
 
     def tensor(self, shape=None):
         import torch
-        shape = tuple(shape) if shape is not None else (self.nbytes,)
+        shape = tuple(int(n) for n in shape) if shape is not None else (self.nbytes,)
         if int(np.prod(shape)) > self.nbytes:
             raise ValueError(f"view of {shape} exceeds the {self.nbytes}-byte buffer")
-        self._shape = shape
-        try:
-            return torch.as_tensor(self, device=torch.device("cuda", self.device))
-        finally:
-            self._shape = (self.nbytes,)
+        return torch.as_tensor(_DeviceView(self, shape), device=torch.device("cuda", self.device))
 
     def __del__(self):
         p = getattr(self, "_p", None)

@@ -543,3 +543,22 @@ def test_encode_reconstruct_in_device_buffer(gpu, contiguous):
     assert np.array_equal(shards.cpu().numpy(), host)
     del shards
     del buf
+
+
+def test_device_buffer_view_keeps_buffer_alive(gpu):
+    """A tensor view holds its DeviceBuffer: dropping the buffer object first
+    does not free the VRAM under the tensor (checked without touching it)."""
+    import gc
+    import weakref
+    buf = shmr_amd.DeviceBuffer(1 << 20, contiguous=False)
+    t = buf.tensor((4, 1 << 18))
+    assert t.shape == (4, 1 << 18) and t.is_cuda
+    ref = weakref.ref(buf)
+    del buf
+    gc.collect()
+    assert ref() is not None
+    del t
+    gc.collect()
+    assert ref() is None
+    with pytest.raises(ValueError):
+        shmr_amd.DeviceBuffer(1024, contiguous=False).tensor((2, 1024))
