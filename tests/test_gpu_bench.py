@@ -1,0 +1,59 @@
+"""bench.py's output contract, on small batches (the driver parses this line).
+
+Each case runs bench.py once as a child process (one GPU process at a time)
+and checks the JSON line: the task's keys, the roofline object, the CPU
+baseline (encode and decode legs, each re-checking the GPU's bytes against the
+CPU restatement), and the codec round trip.
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"}
+
+
+def run_bench(*args):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
+           "--ramp-seconds", "0.05", "--cpu-seconds", "0.2", *args]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=100)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config,blocks", [("encode83", 16), ("decode83", 16), ("codec104", 4)])
+def test_bench_line_contract(gpu, config, blocks):
+    d = run_bench("--config", config, "--blocks", str(blocks))
+    assert KEYS <= set(d)
+    assert d["value"] > 0 and d["unit"] == "GiB/s" and d["n_gpus"] == 1 and d["steps"] == 3
+    assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["dtype"] == "u8"
+    assert d["config"]["workload"] and d["config"]["blocks_per_gpu"] == blocks
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert 0 < r["frac"] < 1 and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    assert "traffic" in r               # null here: the PMC table is keyed by the bench batch size
+    c = d["cpu_baseline"]
+    assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0 and c["sample"]
+    if config == "encode83":
+        assert c["gpu_parity_bit_exact_on_sample"] is True
+    elif config == "decode83":
+        assert c["gpu_rebuilt_bit_exact_on_sample"] is True
+    else:
+        assert r["round_trip_bit_exact"] is True
+        assert c["gpu_parity_bit_exact_on_sample"] is True and c["gpu_rebuilt_bit_exact_on_sample"] is True
+
+
+@pytest.mark.gpu
+def test_bench_contiguous_vram(gpu):
+    d = run_bench("--blocks", "16", "--contig", "--no-cpu")
+    assert d["value"] > 0 and "contiguous" in d["config"]["memory"] and d["cpu_baseline"] is None
