@@ -230,6 +230,25 @@ void test_block_errors() {
     CHECK(fsize(shard_file(*cfg, ec, 0)) == 0);
 }
 
+// calculate_shard_size's f32 hazard (mod.rs:16-18): 16,777,217 / 8 rounds to
+// S = 2,097,152, so a full buffer splits into 9 chunks and block.rs:421's
+// `data - nchunks` underflows u8 (panic in debug, a data chunk overwritten by
+// parity in release).  The mirror refuses before any GPU work or shard write.
+void test_erasure_f32_hazard() {
+    auto cfg = test_config();
+    const uint64_t size = 16777217;
+    VirtualBlock b;
+    CHECK_OK(VirtualBlock::create(11, 0, cfg, size, BlockTopology::erasure(1, 8, 3), &b));
+    CHECK(calculate_shard_size(size, 8) == 2097152 && calculate_shard_size(size, 8) * 8 < size);
+    std::vector<uint8_t> buf(size, 0x5a);
+    size_t n = 0;
+    CHECK_OK(b.write(0, buf.data(), buf.size(), &n));
+    CHECK(n == size);
+    Status st = b.sync_data(true);
+    CHECK(st && st->kind == ShmrError::EcError && st->code == SHMR_EC_TOO_MANY_DATA_SHARDS);
+    CHECK(fsize(shard_file(*cfg, b, 0)) == 0 && fsize(shard_file(*cfg, b, 10)) == 0);
+}
+
 void test_virtual_file_1() {   // mod.rs:322-349
     auto cfg = test_config();
     VirtualFile vf = VirtualFile::new_with(g_rng() >> 16, 0);
@@ -640,6 +659,7 @@ int main(int argc, char** argv) {
         {"virtual_block_buffered", test_virtual_block_buffered},
         {"virtual_block_erasure_buffered", test_virtual_block_erasure_buffered},
         {"block_errors", test_block_errors},
+        {"erasure_f32_hazard", test_erasure_f32_hazard},
         {"virtual_file_1", test_virtual_file_1},
         {"virtual_file_2_4_mb", test_virtual_file_2_4_mb},
         {"virtual_file_errors", test_virtual_file_errors},

@@ -53,6 +53,7 @@ CPU_CASES = [
     "virtual_block_buffered",
     "virtual_block_erasure_buffered",
     "block_errors",
+    "erasure_f32_hazard",
     "virtual_file_1",
     "virtual_file_2_4_mb",
     "virtual_file_errors",
