@@ -22,19 +22,17 @@ import argparse
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
-
-import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
-import torch  # noqa: E402  (before shmr_amd: share one HIP runtime)
-import torch.distributed as dist  # noqa: E402
-
-import shmr_amd  # noqa: E402
-from shmr_amd import placement  # noqa: E402
+# torch and shmr_amd are imported by the worker only (run()): the launcher
+# parent of `--gpus N` must not touch the GPU before it starts its children.
+np = torch = dist = shmr_amd = placement = None
 
 METRIC = "GiB/s erasure-encoded (device-resident), RS(8,3) 4 MiB StorageBlocks, 1/2/4/8 GPUs"
 HBM_PEAK = 8.0e12          # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -71,13 +69,98 @@ def parse():
     ap.add_argument("--ramp-seconds", type=float, default=0.5,
                     help="untimed device clock ramp before the warmup steps (MI355X needs ~0.1 s of "
                          "sustained load to reach its steady clock)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the cpu_baseline leg (default: every core this process may run on, "
+                         "as rayon's default pool; the reference fans blocks out with rayon, mod.rs:93-96)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="launcher rehearsal without a GPU: ranks join the process group, exchange their "
+                         "identities and rank 0 prints one JSON line (tests/test_bench_launch.py)")
     return ap.parse_args()
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(n: int, argv) -> int:
+    """`bench.py --gpus N` started without a torch.distributed launcher: spawn
+    N fresh worker processes of this script (rank r -> GPU r), wait for them
+    and return the first failing exit status (0 if all succeed).  The parent
+    never initialises the GPU and never re-execs itself; the children inherit
+    stdout, where rank 0 prints the one JSON line.  Same partition as the
+    torchrun launch: whole blocks round-robin, one process per GPU
+    (reference per-block fan-out: src/vfs/mod.rs:91-103)."""
+    port = os.environ.get("MASTER_PORT") or str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=port,
+                   SHMR_BENCH_LAUNCHER="spawn")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for pr in list(live):
+            code = pr.poll()
+            if code is None:
+                continue
+            live.remove(pr)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for other in live:          # a rank died: the others would wait in a collective forever
+                    other.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def launch_check(args) -> None:
+    """Process-group rehearsal of a launch (no GPU, gloo): every rank reports
+    its RANK / LOCAL_RANK / pid; rank 0 prints one JSON line."""
+    import torch.distributed as dist_
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    me = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "pid": os.getpid(),
+          "launcher": os.environ.get("SHMR_BENCH_LAUNCHER", "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ else "none")}
+    ranks = [me]
+    seen = 1
+    if os.environ.get("SHMR_BENCH_LAUNCH_FAIL_RANK") == str(rank):
+        sys.exit(3)      # test hook: a rank that dies before joining the group
+    if world > 1:
+        dist_.init_process_group("gloo")
+        seen = dist_.get_world_size()
+        ranks = [None] * seen
+        dist_.all_gather_object(ranks, me)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": args.gpus, "ranks_seen": seen, "ranks": ranks}), flush=True)
+    if world > 1:
+        dist_.destroy_process_group()
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args.gpus, sys.argv[1:]))
+    if args.launch_check:
+        return launch_check(args)
+    run(args)
+
+
+def run(args):
+    global np, torch, dist, shmr_amd, placement
+    import numpy as np  # noqa: F811
+    import torch  # noqa: F811  (before shmr_amd: share one HIP runtime)
+    import torch.distributed as dist  # noqa: F811
+    if args.tune:
+        # kernel knobs are measurement variants: the tools build (DESIGN.md §3)
+        os.environ["SHMR_EC_FLAVOUR"] = "tools"
+    import shmr_amd  # noqa: F811
+    from shmr_amd import _native, placement  # noqa: F811
     if args.gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} needs a torch.distributed.run launch with that many ranks")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE')}")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -96,6 +179,14 @@ def main():
             dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    props = torch.cuda.get_device_properties(dev)
+    me = {"rank": rank, "device": local,
+          "pci_bus_id": f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}",
+          "name": props.name}
+    ranks = [me]
+    if world > 1:
+        ranks = [None] * dist.get_world_size()
+        dist.all_gather_object(ranks, me)      # gloo by default: identities only, no data path
 
     k, p, block_bytes, erasures = CONFIGS[args.config]
     S = shmr_amd.calculate_shard_size(block_bytes, k)
@@ -212,6 +303,11 @@ def main():
         "value": round(value, 3),
         "unit": "GiB/s",
         "n_gpus": world,
+        "ranks_seen": len(ranks),
+        "devices": ranks,
+        "distinct_gpus": len({r["pci_bus_id"] for r in ranks}),
+        "launcher": os.environ.get("SHMR_BENCH_LAUNCHER", "torchrun" if world > 1 else "single"),
+        "library": {"flavour": _native.flavour(), "build_id": _native.lib().shmr_ec_build_id().decode()},
         "steps": args.steps,
         "warmup": args.warmup,
         "clock_ramp": {"seconds": args.ramp_seconds, "steps": ramp_steps},
@@ -242,12 +338,15 @@ def main():
             "peak": HBM_PEAK / 1e9,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK, 4),
-            "traffic": load_traffic(args.config, B),
+            "traffic": None,
             "kernel_ms_avg": round(kern_s * 1e3, 4),
             "algorithmic_bytes_per_launch": algo_bytes_per_block * B,
         },
         "cpu_baseline": None,
     }
+    traffic, source = load_traffic(args.config, B, out["library"]["build_id"], tuning)
+    out["roofline"]["traffic"] = traffic
+    out["roofline"]["traffic_source"] = source
     if codec:
         # two launches per step: the roofline figures are per step (both launches)
         out["roofline"]["launches_per_step"] = 2
@@ -266,8 +365,9 @@ def main():
         del reference
     if rank == 0 and world == 1 and not args.no_cpu:
         if codec:
-            enc = cpu_baseline(k, p, S, block_bytes, shards[:, :k], shards[:, k:], args.cpu_seconds / 2)
-            dec = cpu_baseline_decode(k, p, S, shards, present, args.cpu_seconds / 2)
+            enc = cpu_baseline(k, p, S, block_bytes, shards[:, :k], shards[:, k:], args.cpu_seconds / 2,
+                               args.cpu_threads)
+            dec = cpu_baseline_decode(k, p, S, shards, present, args.cpu_seconds / 2, args.cpu_threads)
             rate = 1.0 / (1.0 / enc["value"] + 1.0 / dec["value"])
             out["cpu_baseline"] = {
                 "value": round(rate, 3), "unit": "GiB/s", "cores": enc["cores"], "kind": "port",
@@ -275,31 +375,58 @@ def main():
                           "workload, combined as one step: 1 / (1/encode + 1/reconstruct); "
                           f"encode: {enc['sample']}; reconstruct: {dec['sample']}",
                 "encode_GiBps": enc["value"], "reconstruct_GiBps": dec["value"],
-                "cpu_model": enc["cpu_model"],
+                "cpu_model": enc["cpu_model"], "cpu_quota_cores": enc["cpu_quota_cores"],
                 "gpu_parity_bit_exact_on_sample": enc["gpu_parity_bit_exact_on_sample"],
                 "gpu_rebuilt_bit_exact_on_sample": dec["gpu_rebuilt_bit_exact_on_sample"],
             }
         elif erasures is None:
-            out["cpu_baseline"] = cpu_baseline(k, p, S, block_bytes, data, parity, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(k, p, S, block_bytes, data, parity, args.cpu_seconds, args.cpu_threads)
         else:
-            out["cpu_baseline"] = cpu_baseline_decode(k, p, S, shards, present, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline_decode(k, p, S, shards, present, args.cpu_seconds, args.cpu_threads)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def load_traffic(config: str, B: int):
-    """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if any."""
-    path = os.path.join(HERE, "profiles", "pmc_traffic.json")
+def load_traffic(config: str, B: int, build_id: str, variant: str):
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py), only if the
+    record was measured on this kernel build and variant at this batch size;
+    otherwise traffic is null and the source says why."""
+    rel = os.path.join("profiles", "pmc_traffic.json")
+    src = {"file": rel, "key": config, "build_id": build_id, "variant": variant}
     try:
-        with open(path) as f:
+        with open(os.path.join(HERE, rel)) as f:
             rec = json.load(f).get(config)
     except (OSError, ValueError):
+        return None, dict(src, status="no record file")
+    if not rec:
+        return None, dict(src, status="no record for this config")
+    for key, want in (("build_id", build_id), ("variant", variant), ("blocks", B)):
+        if rec.get(key) != want:
+            return None, dict(src, status=f"stale: recorded {key} {rec.get(key)!r} != running {want!r}")
+    return rec.get("hbm_bytes_per_launch"), dict(src, status="match")
+
+
+def cpu_threads(requested: int) -> int:
+    """rayon's default pool: one thread per core this process may run on."""
+    if requested > 0:
+        return requested
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
+def cpu_quota():
+    """cgroup v2 CPU quota in cores (None if unlimited / unknown)."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()
+        return None if q == "max" else round(int(q) / int(period), 2)
+    except (OSError, ValueError):
         return None
-    if not rec or rec.get("blocks") != B:
-        return None
-    return rec.get("hbm_bytes_per_launch")
 
 
 def cpu_model() -> str:
@@ -313,13 +440,15 @@ def cpu_model() -> str:
     return platform.processor() or platform.machine()
 
 
-def cpu_baseline(k, p, S, block_bytes, data_t, parity_t, budget_s):
+def cpu_baseline(k, p, S, block_bytes, data_t, parity_t, budget_s, threads=0):
     """CPU restatement of the crate's simd_c AVX2 loop (oracle/, "port"),
-    one block per thread as rayon does over VirtualFile blocks; bounded sample
-    of the same workload; also checks the GPU parity of the sampled blocks."""
+    one block per thread as rayon does over VirtualFile blocks, on every core
+    this process may use (rayon's default pool); bounded sample of the same
+    workload; also checks the GPU parity of the sampled blocks.  A 16-thread
+    and a 1-core figure ride along."""
     from oracle import c_oracle   # cpu_baseline leg: oracle allowed here only
-    cores = min(16, os.cpu_count() or 1)
-    nb = min(256, data_t.shape[0])     # 1 GiB of RS(8,3) data: larger than the host LLC
+    cores = cpu_threads(threads)
+    nb = min(max(256, 4 * cores), data_t.shape[0])   # >= 1 GiB of RS(8,3) data (past the host LLC), >= 4 blocks/thread
     host_data = data_t[:nb, :, :S].contiguous().cpu().numpy().reshape(-1)
     host_par = np.zeros(nb * p * S, dtype=np.uint8)
     reps, secs = 0, 0.0
@@ -329,6 +458,11 @@ def cpu_baseline(k, p, S, block_bytes, data_t, parity_t, budget_s):
     gpu_par = parity_t[:nb, :, :S].contiguous().cpu().numpy().reshape(-1)
     ok = bool(np.array_equal(gpu_par, host_par))
     gib = nb * k * S * reps / secs / 2 ** 30
+    t16 = min(16, cores)
+    reps16, secs16 = 0, 0.0
+    while secs16 < budget_s / 3 or reps16 == 0:
+        secs16 += c_oracle.encode_batch(k, p, host_data, host_par, nb, S, t16, variant=1)
+        reps16 += 1
     single = c_oracle.encode_batch(k, p, host_data[: k * S], host_par[: p * S], 1, S, 1, variant=1)
     # the whole VirtualBlock::sync_data Erasure arm minus disk I/O (block.rs:406-430):
     # chunks(S).to_vec() copies, zero pad, zero shards, encode, per block
@@ -353,6 +487,8 @@ def cpu_baseline(k, p, S, block_bytes, data_t, parity_t, budget_s):
                   f"(one block per thread, AVX2 nibble-pshufb loop restating reed-solomon-erasure "
                   f"6.0.0 simd_c); encode only (erasure_encode_duration scope, block.rs:425-430)",
         "single_core_GiBps": round(k * S / single / 2 ** 30, 3),
+        "threads16_GiBps": round(nb * k * S * reps16 / secs16 / 2 ** 30, 3),
+        "cpu_quota_cores": cpu_quota(),
         "sync_data_GiBps": round(ns * block_bytes * sreps / ssecs / 2 ** 30, 3),
         "sync_data_sample": f"{ns} blocks x {sreps} reps: chunk to_vec copies + zero pad/shards + encode "
                             f"per block (block.rs:406-430), {cores} threads",
@@ -362,15 +498,15 @@ def cpu_baseline(k, p, S, block_bytes, data_t, parity_t, budget_s):
     }
 
 
-def cpu_baseline_decode(k, p, S, shards_t, present, budget_s):
+def cpu_baseline_decode(k, p, S, shards_t, present, budget_s, threads=0):
     """CPU restatement of the crate's reconstruct (first k present shards,
     inverted sub-matrix, SIMD mul_slice loop; oracle/, "port"), one block per
     thread; bounded sample of the same decode workload.  The GPU's rebuilt
     shards of the sampled blocks are checked bit-for-bit against it."""
     from oracle import c_oracle   # cpu_baseline leg: oracle allowed here only
-    cores = min(16, os.cpu_count() or 1)
+    cores = cpu_threads(threads)
     t = k + p
-    nb = min(shards_t.shape[0], max(1, (1 << 30) // (t * S)))
+    nb = min(shards_t.shape[0], max(1, (1 << 30) // (t * S), 4 * cores))
     gpu = np.ascontiguousarray(shards_t[:nb, :, :S].cpu().numpy())
     pr = np.ascontiguousarray(present[:nb], dtype=np.uint8)
     work = gpu.copy()
@@ -380,6 +516,11 @@ def cpu_baseline_decode(k, p, S, shards_t, present, budget_s):
         secs += c_oracle.reconstruct_batch(k, p, work, pr, S, cores)
         reps += 1
     ok = bool(np.array_equal(work, gpu))
+    t16 = min(16, cores)
+    reps16, secs16 = 0, 0.0
+    while secs16 < budget_s / 3 or reps16 == 0:
+        secs16 += c_oracle.reconstruct_batch(k, p, work, pr, S, t16)
+        reps16 += 1
     single = c_oracle.reconstruct_batch(k, p, work[:1], pr[:1], S, 1)
     return {
         "value": round(nb * k * S * reps / secs / 2 ** 30, 3),
@@ -390,6 +531,8 @@ def cpu_baseline_decode(k, p, S, shards_t, present, budget_s):
                   f"~{secs * cores:.0f} core-seconds), {cores} threads (one block per thread; crate reconstruct "
                   f"restated: inv(M[first k present]) + AVX2 nibble-pshufb mul_slice)",
         "single_core_GiBps": round(k * S / single / 2 ** 30, 3),
+        "threads16_GiBps": round(nb * k * S * reps16 / secs16 / 2 ** 30, 3),
+        "cpu_quota_cores": cpu_quota(),
         "cpu_model": cpu_model(),
         "gpu_rebuilt_bit_exact_on_sample": ok,
     }

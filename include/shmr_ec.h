@@ -62,8 +62,17 @@ typedef struct shmr_ec shmr_ec_t;
 /* Human-readable name of a status ("TooFewShardsPresent", ...). */
 const char* shmr_ec_status_name(int status);
 
-/* Library version string. */
+/* Library version string (names the flavour: "product" or "tools"). */
 const char* shmr_ec_version(void);
+
+/* Kernel build ID: hash of the kernel sources, device compile flags and
+ * compiler version (12 hex digits).  Measurement records (PMC traffic) are
+ * keyed by it, so they can be matched to the code that produced them. */
+const char* shmr_ec_build_id(void);
+
+/* 1 in the tools build (libshmr_ec_tools.so: measurement variants and kernel
+ * knobs for tools/), 0 in the product library. */
+int shmr_ec_is_tools_build(void);
 
 /* ---- host logic (no GPU needed) ---------------------------------------- */
 
@@ -191,35 +200,42 @@ int shmr_ec_device_free(int device, void* p);
 /* Device used by the host-buffer entry points (default 0). */
 int shmr_ec_set_device(shmr_ec_t* rs, int device);
 
-/* Kernel tuning knobs (process-wide).  key is one of "chunks" (16-B chunks
- * per lane per tile: 1, 2, 4), "nt_load", "nt_store" (nontemporal 0/1),
- * "scalar_tabs" (0/1), "occ8" (0/1), "grid" (-1 one workgroup per tile,
- * 0 balanced persistent grid, >0 capped persistent grid), "threads" (lanes
- * per workgroup: 128, 256, 512), "depth" (register ring depth = shards of
- * loads in flight + 1: 1, 2, 3, 5, 9), "wgs_per_cu" (0 = no cap, else the
- * most workgroups resident per CU, enforced by LDS padding), "occ" (0, 6, 7:
- * register budget for that many waves per SIMD), "early" (0/1: issue the
- * first data loads before the plan's LDS staging completes), "spre" (0/1:
- * coefficient tables and shard offsets by scalar loads one shard ahead, no
- * LDS), "fuse_tail" (0/1: a shard length that is not a multiple of the
- * tile runs the partial last tile of every block at the head of the full-tile
- * launch instead of in a second launch), "diag" (0/1:
+/* Tuning knobs (process-wide).
+ *
+ * Host-path knobs (both flavours; they choose how bytes move, never what
+ * the kernels compute): "bounce_kib": pageable single-block calls whose
+ * (k+p) x shard bytes fit in this many KiB go through one mapped bounce
+ * buffer and a single zero-copy launch instead of per-shard DMA copies
+ * (default 8192; 0 disables).  "mirror_zc" (0/1, default 1): pageable host
+ * batches are gathered into a pinned mirror that the kernel codes in place
+ * across PCIe (zero-copy) instead of DMA-ing it to device staging.
+ * "ptrs_direct" (default 16): zero-copy launches of at most this many 4 KiB
+ * tiles read their shard-pointer table from pinned host memory in place
+ * instead of uploading it first (0: always upload).  "sync_spin_us"
+ * (default 0): the single-call and zero-copy paths poll their stream this
+ * long before a blocking synchronize.
+ *
+ * Kernel knobs select a measurement variant of the kernel.  In the product
+ * library (libshmr_ec.so) every launch uses the measured per-shape policy and
+ * a kernel knob can only be set to its default (anything else returns
+ * SHMR_EC_INVALID_ARGUMENT); the tools build (libshmr_ec_tools.so) takes:
+ * "chunks" (16-B chunks per lane per tile: 1, 2, 4), "nt_load", "nt_store"
+ * (nontemporal 0/1), "scalar_tabs" (0/1), "occ8" (0/1), "grid" (-1 one
+ * workgroup per tile, 0 balanced persistent grid, >0 capped persistent
+ * grid), "threads" (lanes per workgroup: 128, 256, 512), "depth" (register
+ * ring depth = shards of loads in flight + 1: 1, 2, 3, 5, 9), "wgs_per_cu"
+ * (0 = no cap, else the most workgroups resident per CU, enforced by LDS
+ * padding), "occ" (0, 6, 7: register budget for that many waves per SIMD),
+ * "early" (0/1: issue the first data loads before the plan's LDS staging
+ * completes), "spre" (0/1: coefficient tables and shard offsets by scalar
+ * loads one shard ahead, no LDS), "fuse_tail" (0/1: a shard length that is
+ * not a multiple of the tile runs the partial last tile of every block at the
+ * head of the full-tile launch instead of in a second launch), "diag" (0/1:
  * XOR-only diagnostic kernel, WRONG results, for ceiling measurements).
  * Prefix "encode." or "decode." to set one operation class only.
- * "bounce_kib" (both op classes): pageable single-block calls whose (k+p) x
- * shard bytes fit in this many KiB go through one mapped bounce buffer and a
- * single zero-copy launch instead of per-shard DMA copies (default 8192; 0
- * disables).  "mirror_zc" (0/1, default 1): pageable host batches are
- * gathered into a pinned mirror that the kernel codes in place across PCIe
- * (zero-copy) instead of DMA-ing it to device staging.  "ptrs_direct"
- * (default 16): zero-copy launches of at most this many 4 KiB tiles read
- * their shard-pointer table from pinned host memory in place instead of
- * uploading it first (0: always upload).  "sync_spin_us" (default 0): the
- * single-call and zero-copy paths poll their stream this long before a
- * blocking synchronize.
- * "chunks", "nt_load", "nt_store", "depth", "occ", "early", "spre" and "fuse_tail" default to -2 (auto): a per-shape policy
- * of the fastest variants measured on MI355X; any other value pins the knob,
- * and setting -2 returns it to the policy. */
+ * "chunks", "nt_load", "nt_store", "depth", "occ", "early", "spre" and
+ * "fuse_tail" default to -2 (auto): the per-shape policy; any other value pins
+ * the knob, and setting -2 returns it to the policy. */
 int shmr_ec_set_tuning(const char* key, int value);
 int shmr_ec_get_tuning(const char* key);
 

@@ -1,12 +1,18 @@
 """Loader for the in-tree native library ``shmr_amd/_lib/libshmr_ec.so``.
 
 There is no fallback: if the library is missing or fails to load, importing
-the compute API raises.  ``torch`` is imported first when available so that
+the compute API raises.  ``tools()`` switches the calling code to the tools
+build ``libshmr_ec_tools.so`` (same sources plus the measurement-only kernel
+variants and knobs) for the duration of a ``with`` block; the
+environment variable ``SHMR_EC_FLAVOUR=tools`` makes it the default (tools/
+scripts).  Objects (``ReedSolomon``, buffers) keep the library they were
+created with.  ``torch`` is imported first when available so that
 the library binds to the same HIP runtime instance as PyTorch (both carry the
 SONAME ``libamdhip64.so.7``; loading ours first would map a second runtime).
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 
@@ -17,6 +23,8 @@ except Exception:  # pragma: no cover - torch is part of the image
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libshmr_ec.so")
+TOOLS_LIB_PATH = os.path.join(_HERE, "_lib", "libshmr_ec_tools.so")
+_PATHS = {"product": LIB_PATH, "tools": TOOLS_LIB_PATH}
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u8pp = ctypes.POINTER(_u8p)
@@ -26,6 +34,8 @@ _sz = ctypes.c_size_t
 SIGNATURES = [
     ("shmr_ec_status_name", ctypes.c_char_p, [ctypes.c_int]),
     ("shmr_ec_version", ctypes.c_char_p, []),
+    ("shmr_ec_build_id", ctypes.c_char_p, []),
+    ("shmr_ec_is_tools_build", ctypes.c_int, []),
     ("shmr_ec_shard_size", _sz, [ctypes.c_uint64, ctypes.c_uint32]),
     ("shmr_ec_new", ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),
     ("shmr_ec_free", None, [ctypes.c_void_p]),
@@ -65,25 +75,50 @@ SIGNATURES = [
     ("shmr_ec_device_count", ctypes.c_int, []),
 ]
 
-_lib = None
+_libs = {}
+_flavour = "tools" if os.environ.get("SHMR_EC_FLAVOUR") == "tools" else "product"
 
 
 class NativeLibraryMissing(RuntimeError):
     pass
 
 
-def lib():
-    """Returns the loaded native library; raises if it is not built."""
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
+def _load(flavour: str):
+    L = _libs.get(flavour)
+    if L is None:
+        path = _PATHS[flavour]
+        if not os.path.exists(path):
             raise NativeLibraryMissing(
-                f"{LIB_PATH} is missing: build it with `make -C shmr_amd/csrc` or "
+                f"{path} is missing: build it with `make -C shmr_amd/csrc` or "
                 "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
-        L = ctypes.CDLL(LIB_PATH)
+        L = ctypes.CDLL(path)
         for name, res, args in SIGNATURES:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        _lib = L
-    return _lib
+        _libs[flavour] = L
+    return L
+
+
+def lib():
+    """Returns the active native library (product unless inside ``tools()``);
+    raises if it is not built."""
+    return _load(_flavour)
+
+
+def flavour() -> str:
+    return _flavour
+
+
+@contextlib.contextmanager
+def tools():
+    """Within the block, new objects and the module-level calls use the tools
+    build.  Not thread-safe: for tests and tools/ scripts."""
+    global _flavour
+    prev = _flavour
+    _load("tools")
+    _flavour = "tools"
+    try:
+        yield _libs["tools"]
+    finally:
+        _flavour = prev

@@ -63,7 +63,26 @@ const char* shmr_ec_status_name(int st) {
     }
 }
 
-const char* shmr_ec_version(void) { return "shmr_ec 0.2.0 (gfx950)"; }
+#ifndef SHMR_EC_KERNEL_ID
+#define SHMR_EC_KERNEL_ID "unknown"
+#endif
+#ifdef SHMR_EC_TOOLS
+#define SHMR_EC_FLAVOUR "tools"
+#else
+#define SHMR_EC_FLAVOUR "product"
+#endif
+
+const char* shmr_ec_version(void) { return "shmr_ec 0.3.0 (gfx950, " SHMR_EC_FLAVOUR ")"; }
+
+const char* shmr_ec_build_id(void) { return SHMR_EC_KERNEL_ID; }
+
+int shmr_ec_is_tools_build(void) {
+#ifdef SHMR_EC_TOOLS
+    return 1;
+#else
+    return 0;
+#endif
+}
 
 size_t shmr_ec_shard_size(uint64_t length, uint32_t data_shards) {
     if (data_shards == 0) return 0;

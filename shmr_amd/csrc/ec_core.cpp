@@ -126,6 +126,21 @@ int set_tuning(const char* key, int value) {
         g_sync_spin = value == kAuto ? kSyncSpinDefault : value;
         return SHMR_EC_OK;
     }
+#ifndef SHMR_EC_TOOLS
+    // Product build: the kernel variant of every launch is the measured policy
+    // (variant_policy), the same for every caller in the process.  Kernel knobs
+    // exist to take measurements and live in the tools build
+    // (libshmr_ec_tools.so); here a knob may only be "set" to its default.
+    // In particular "diag" (XOR-only, wrong results) is refused.
+    {
+        static const std::map<std::string, int> kDefaults = {
+            {"chunks", kAuto}, {"nt_load", kAuto}, {"nt_store", kAuto}, {"scalar_tabs", 0}, {"occ8", 0},
+            {"grid", -1},      {"diag", 0},        {"threads", 256},    {"depth", kAuto},   {"wgs_per_cu", 0},
+            {"occ", kAuto},    {"early", kAuto},   {"spre", kAuto},     {"fuse_tail", kAuto}};
+        const auto it = kDefaults.find(k);
+        return (it != kDefaults.end() && it->second == value) ? SHMR_EC_OK : SHMR_EC_INVALID_ARGUMENT;
+    }
+#endif
     for (int i = first; i <= last; ++i) {
         Tuning& T = g_tune[i];
         if (k == "chunks") {
@@ -203,7 +218,9 @@ kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_m
     if (T.nt_store.load() != kAuto) v.nt_store = T.nt_store.load() != 0;
     v.scalar_tabs = T.scalar_tabs.load() != 0;
     v.occ8 = T.occ8.load() != 0;
+#ifdef SHMR_EC_TOOLS
     v.diag = T.diag.load() != 0;
+#endif
     v.threads = T.threads.load();
     if (T.depth.load() != kAuto) v.depth = T.depth.load();
     v.wgs_per_cu = T.wgs_per_cu.load();

@@ -40,7 +40,7 @@ constexpr int kNtLoad = 1;       // nontemporal loads
 constexpr int kNtStore = 2;      // nontemporal stores
 constexpr int kScalarTabs = 4;   // tables/offsets via scalar loads, no LDS staging
 constexpr int kOcc8 = 8;         // ask for 8 waves / SIMD (<= 64 VGPRs)
-constexpr int kDiagXor = 16;     // diagnostics: XOR without GF multiply (wrong results)
+constexpr int kDiagXor = 16;     // diagnostics: XOR without GF multiply (wrong results; tools build only)
 constexpr int kTh128 = 32;       // 128-lane workgroups (default 256)
 constexpr int kTh512 = 64;       // 512-lane workgroups
 constexpr int kDepth5 = 128;     // 4 shards of loads in flight (default 2)
@@ -178,6 +178,7 @@ __device__ __forceinline__ void st(uint8_t* base, uint64_t col, uint64_t len, u3
 template <int R, int F>
 __device__ __forceinline__ void mac(uint32_t (&acc)[R][4], const u32x4& d, const Tab (&tb)[R]) {
     const uint32_t w[4] = {d.x, d.y, d.z, d.w};
+#ifdef SHMR_EC_TOOLS
     if constexpr ((F & kDiagXor) != 0) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -185,6 +186,7 @@ __device__ __forceinline__ void mac(uint32_t (&acc)[R][4], const u32x4& d, const
             for (int r = 0; r < R; ++r) acc[r][j] ^= w[j] + tb[r].t2;
         return;
     }
+#endif
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const uint32_t s0 = w[j] & 0x07070707u;
@@ -714,7 +716,40 @@ hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStr
 // Full-tile variants compiled in: each entry is one (U, F) instantiation.
 // Not every flag combination is compiled: an unsupported combination returns
 // hipErrorInvalidValue (the C ABI reports SHMR_EC_INVALID_ARGUMENT).
-#define SHMR_VARIANTS(X) \
+//
+// The product library (libshmr_ec.so) carries only the variants the tuning
+// policy (ec_core.cpp variant_policy / launch_variant) can select: depth-2
+// ring, nontemporal stores, nontemporal loads unless the shards are mapped
+// host memory, U = 1 or 2, with the early prologue, fused tails, shard-pointer
+// tables and segment launches as launch forms.  Every other instantiation --
+// the measurement variants behind the kernel knobs of shmr_ec_set_tuning and
+// the XOR-only diagnostic kernel (wrong results by design) -- exists only in
+// the tools build (libshmr_ec_tools.so, -DSHMR_EC_TOOLS), which tools/ and
+// the variant tests load explicitly.
+#define SHMR_VARIANTS_PRODUCT(X) \
+    X(1, kNtLoad | kNtStore | kDepth2) \
+    X(2, kNtLoad | kNtStore | kDepth2) \
+    X(1, kNtStore | kDepth2) \
+    X(2, kNtStore | kDepth2) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kFuse) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kFuse) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse) \
+    X(1, kNtStore | kDepth2 | kPtrs) \
+    X(2, kNtStore | kDepth2 | kPtrs) \
+    X(1, kNtStore | kDepth2 | kPtrs | kFuse) \
+    X(2, kNtStore | kDepth2 | kPtrs | kFuse) \
+    X(1, kNtStore | kDepth2 | kPtrs | kSegs) \
+    X(1, kNtStore | kDepth2 | kPtrs | kSegs | kFuse) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kPtrs) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kPtrs)
+
+#ifdef SHMR_EC_TOOLS
+#define SHMR_VARIANTS_TOOLS(X) \
     X(1, 0) \
     X(1, kNtLoad) \
     X(1, kNtStore) \
@@ -734,12 +769,8 @@ hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStr
     X(1, kNtLoad | kNtStore | kDepth9) \
     X(1, kNtLoad | kDepth5) \
     X(1, kNtLoad | kDepth9) \
-    X(1, kNtLoad | kNtStore | kDepth2) \
     X(1, kNtLoad | kNtStore | kDepth1) \
     X(1, kNtLoad | kDepth2) \
-    X(1, kNtStore | kDepth2) \
-    X(2, kNtLoad | kNtStore | kDepth2) \
-    X(2, kNtStore | kDepth2) \
     X(1, kNtLoad | kNtStore | kDepth2 | kTh512) \
     X(1, kNtLoad | kNtStore | kDepth2 | kTh128) \
     X(1, kNtLoad | kNtStore | kDepth2 | kOcc8) \
@@ -748,27 +779,15 @@ hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStr
     X(1, kNtLoad | kNtStore | (6 << kOccShift)) \
     X(1, kNtLoad | kNtStore | (7 << kOccShift)) \
     X(2, kNtLoad | kNtStore | kDepth2 | (6 << kOccShift)) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kEarly) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly) \
     X(1, kNtLoad | kNtStore | kEarly) \
     X(1, kNtLoad | kNtStore | kDepth2 | kEarly | (6 << kOccShift)) \
     X(1, kNtLoad | kNtStore | kDepth2 | kSPre) \
     X(2, kNtLoad | kNtStore | kDepth2 | kSPre) \
-    X(1, kNtLoad | kNtStore | kSPre) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kFuse) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kFuse) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kSegs) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse) \
-    X(1, kNtStore | kDepth2 | kPtrs) \
-    X(2, kNtStore | kDepth2 | kPtrs) \
-    X(1, kNtStore | kDepth2 | kPtrs | kFuse) \
-    X(2, kNtStore | kDepth2 | kPtrs | kFuse) \
-    X(1, kNtStore | kDepth2 | kPtrs | kSegs) \
-    X(1, kNtStore | kDepth2 | kPtrs | kSegs | kFuse) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kPtrs) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kPtrs)
+    X(1, kNtLoad | kNtStore | kSPre)
+#define SHMR_VARIANTS(X) SHMR_VARIANTS_PRODUCT(X) SHMR_VARIANTS_TOOLS(X)
+#else
+#define SHMR_VARIANTS(X) SHMR_VARIANTS_PRODUCT(X)
+#endif
 
 int variant_flags(const Variant& v) {
     return (v.nt_load ? kNtLoad : 0) | (v.nt_store ? kNtStore : 0) | (v.scalar_tabs ? kScalarTabs : 0) |

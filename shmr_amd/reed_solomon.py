@@ -83,40 +83,41 @@ class ReedSolomon:
     """``ReedSolomon::new(data_shards, parity_shards)`` -- raises ``Error``."""
 
     def __init__(self, data_shards: int, parity_shards: int, device: int = 0):
+        self._L = lib()   # the library this codec lives in (product unless _native.tools())
         h = ctypes.c_void_p()
-        _check(lib().shmr_ec_new(data_shards, parity_shards, ctypes.byref(h)))
+        _check(self._L.shmr_ec_new(data_shards, parity_shards, ctypes.byref(h)))
         self._h = h
         if device:
-            _check(lib().shmr_ec_set_device(self._h, device))
+            _check(self._L.shmr_ec_set_device(self._h, device))
 
     def __del__(self):
         h = getattr(self, "_h", None)
         if h:
-            lib().shmr_ec_free(h)
+            self._L.shmr_ec_free(h)
             self._h = None
 
     # -- crate accessors -------------------------------------------------------
     def data_shard_count(self) -> int:
-        return int(lib().shmr_ec_data_shard_count(self._h))
+        return int(self._L.shmr_ec_data_shard_count(self._h))
 
     def parity_shard_count(self) -> int:
-        return int(lib().shmr_ec_parity_shard_count(self._h))
+        return int(self._L.shmr_ec_parity_shard_count(self._h))
 
     def total_shard_count(self) -> int:
-        return int(lib().shmr_ec_total_shard_count(self._h))
+        return int(self._L.shmr_ec_total_shard_count(self._h))
 
     def matrix(self) -> np.ndarray:
         t, k = self.total_shard_count(), self.data_shard_count()
         out = np.zeros(t * k, dtype=np.uint8)
-        _check(lib().shmr_ec_matrix(self._h, _ptr(out), out.size))
+        _check(self._L.shmr_ec_matrix(self._h, _ptr(out), out.size))
         return out.reshape(t, k)
 
     def set_device(self, device: int) -> None:
-        _check(lib().shmr_ec_set_device(self._h, device))
+        _check(self._L.shmr_ec_set_device(self._h, device))
 
     def cache_stats(self):
         h, m = ctypes.c_uint64(), ctypes.c_uint64()
-        _check(lib().shmr_ec_cache_stats(self._h, ctypes.byref(h), ctypes.byref(m)))
+        _check(self._L.shmr_ec_cache_stats(self._h, ctypes.byref(h), ctypes.byref(m)))
         return int(h.value), int(m.value)
 
     def reconstruct_plan(self, present: Sequence[bool], data_only: bool = False):
@@ -127,7 +128,7 @@ class ReedSolomon:
         out_idx = (ctypes.c_uint16 * t)()
         rows = np.zeros(t * k, dtype=np.uint8)
         n = ctypes.c_uint32()
-        _check(lib().shmr_ec_reconstruct_plan(self._h, _ptr(pr), len(pr), int(data_only), in_idx, out_idx,
+        _check(self._L.shmr_ec_reconstruct_plan(self._h, _ptr(pr), len(pr), int(data_only), in_idx, out_idx,
                                               _ptr(rows), rows.size, ctypes.byref(n)))
         m = n.value
         return list(in_idx), list(out_idx)[:m], rows[:m * k].reshape(m, k).copy()
@@ -139,7 +140,7 @@ class ReedSolomon:
         n = len(arrs)
         ptrs = (_u8p * max(n, 1))(*[_ptr(a) for a in arrs])
         lens = (ctypes.c_size_t * max(n, 1))(*[a.size for a in arrs])
-        _check(lib().shmr_ec_encode(self._h, ptrs, lens, n))
+        _check(self._L.shmr_ec_encode(self._h, ptrs, lens, n))
 
     def _reconstruct(self, shards: MutableSequence[Optional[object]], data_only: bool) -> None:
         n = len(shards)
@@ -157,7 +158,7 @@ class ReedSolomon:
                     fill[i] = True
         ptrs = (_u8p * max(n, 1))(*[(_ptr(a) if a is not None else _u8p()) for a in arrs])
         lens = (ctypes.c_size_t * max(n, 1))(*[(a.size if a is not None else 0) for a in arrs])
-        _check(lib().shmr_ec_reconstruct(self._h, ptrs, lens, _ptr(present), n, int(data_only)))
+        _check(self._L.shmr_ec_reconstruct(self._h, ptrs, lens, _ptr(present), n, int(data_only)))
         for i in range(n):
             if fill[i]:
                 shards[i] = arrs[i]
@@ -236,7 +237,7 @@ class ReedSolomon:
         self._check_batch_tensor(parity, self.parity_shard_count(), psp, L)
         self._check_addressable(data, parity)
         dev, stream = self._stream_and_device(data)
-        _check(lib().shmr_ec_encode_batch_dev(self._h, ctypes.c_void_p(data.data_ptr()), dsp, dbp,
+        _check(self._L.shmr_ec_encode_batch_dev(self._h, ctypes.c_void_p(data.data_ptr()), dsp, dbp,
                                               ctypes.c_void_p(parity.data_ptr()), psp, pbp, B, L, dev, stream))
 
     def reconstruct_batch_dev(self, shards, present: np.ndarray, shard_len: Optional[int] = None,
@@ -253,7 +254,7 @@ class ReedSolomon:
         pr = pr.reshape(B, t)
         self._check_addressable(shards)
         dev, stream = self._stream_and_device(shards)
-        _check(lib().shmr_ec_reconstruct_batch_dev(self._h, ctypes.c_void_p(shards.data_ptr()), shards.stride(1),
+        _check(self._L.shmr_ec_reconstruct_batch_dev(self._h, ctypes.c_void_p(shards.data_ptr()), shards.stride(1),
                                                    shards.stride(0), _ptr(pr), B, L, int(data_only), dev, stream))
 
     def _host_ptrs(self, blocks):
@@ -278,6 +279,14 @@ class ReedSolomon:
             if len(blk) != t:
                 raise Error(-1 if len(blk) < t else -2)
         L = next((a.size for blk in arrs for a in blk if a is not None), 0)
+        # The C ABI takes one shard_len for every pointer, so every shard must
+        # hold exactly that many bytes (a shorter buffer would be read or
+        # written past its end).  Crate check order: EmptyShard, then
+        # IncorrectShardSize.
+        if arrs and L == 0:
+            raise Error(-11)                                     # EmptyShard
+        if any(a is not None and a.size != L for blk in arrs for a in blk):
+            raise Error(-9)                                      # IncorrectShardSize
         flat = [a for blk in arrs for a in blk]
         ptrs = (_u8p * max(len(flat), 1))(*[(_ptr(a) if a is not None else _u8p()) for a in flat])
         return arrs, L, ptrs
@@ -289,7 +298,7 @@ class ReedSolomon:
         keep, L, ptrs = self._host_ptrs(blocks)
         n = len(blocks)
         devs = (ctypes.c_int * len(devices))(*devices)
-        _check(lib().shmr_ec_encode_blocks_host(self._h, ptrs, n, L, devs, len(devices)))
+        _check(self._L.shmr_ec_encode_blocks_host(self._h, ptrs, n, L, devs, len(devices)))
         del keep
 
     def reconstruct_blocks_host(self, blocks, present, data_only: bool = False,
@@ -301,7 +310,7 @@ class ReedSolomon:
         n = len(blocks)
         pr = np.ascontiguousarray(present, dtype=np.uint8).reshape(n, self.total_shard_count())
         devs = (ctypes.c_int * len(devices))(*devices)
-        _check(lib().shmr_ec_reconstruct_blocks_host(self._h, ptrs, _ptr(pr), n, L, int(data_only), devs,
+        _check(self._L.shmr_ec_reconstruct_blocks_host(self._h, ptrs, _ptr(pr), n, L, int(data_only), devs,
                                                      len(devices)))
         del keep
 
@@ -311,8 +320,9 @@ class PinnedBuffer:
     host-buffer entry points DMA it without a staging copy."""
 
     def __init__(self, nbytes: int):
+        self._L = lib()
         p = ctypes.c_void_p()
-        _check(lib().shmr_ec_host_alloc(nbytes, ctypes.byref(p)))
+        _check(self._L.shmr_ec_host_alloc(nbytes, ctypes.byref(p)))
         self._p = p
         self.nbytes = nbytes
         self.array = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint8)), shape=(nbytes,))
@@ -321,7 +331,7 @@ class PinnedBuffer:
         p = getattr(self, "_p", None)
         if p:
             self.array = None
-            lib().shmr_ec_host_free(p)
+            self._L.shmr_ec_host_free(p)
             self._p = None
 
 
@@ -343,8 +353,9 @@ class DeviceBuffer:
     ``*_batch_dev`` entry points; the view keeps the buffer alive."""
 
     def __init__(self, nbytes: int, device: int = 0, contiguous: bool = True):
+        self._L = lib()
         p = ctypes.c_void_p()
-        _check(lib().shmr_ec_device_alloc(device, nbytes, int(bool(contiguous)), ctypes.byref(p)))
+        _check(self._L.shmr_ec_device_alloc(device, nbytes, int(bool(contiguous)), ctypes.byref(p)))
         self._p = p
         self.nbytes = nbytes
         self.device = device
@@ -360,7 +371,7 @@ class DeviceBuffer:
     def __del__(self):
         p = getattr(self, "_p", None)
         if p:
-            lib().shmr_ec_device_free(self.device, p)
+            self._L.shmr_ec_device_free(self.device, p)
             self._p = None
 
 

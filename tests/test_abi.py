@@ -31,11 +31,12 @@ def test_header_declares_the_boundary():
         assert required in fns
 
 
-def test_library_exports_every_declared_symbol():
-    lib = _native.lib()
+@pytest.mark.parametrize("flavour", ["product", "tools"])
+def test_library_exports_every_declared_symbol(flavour):
+    lib = _native._load(flavour)
     for fn in declared_functions():
         assert hasattr(lib, fn), fn
-    out = subprocess.run(["nm", "-D", "--defined-only", _native.LIB_PATH], capture_output=True, text=True).stdout
+    out = subprocess.run(["nm", "-D", "--defined-only", _native._PATHS[flavour]], capture_output=True, text=True).stdout
     exported = set(re.findall(r"\bT (shmr_ec_\w+)", out))
     assert set(declared_functions()) <= exported
 
@@ -184,17 +185,21 @@ def test_compute_without_gpu_fails_loudly():
 
 
 def test_tuning_api():
-    saved = shmr_amd.get_tuning("encode.chunks")
-    try:
-        shmr_amd.set_tuning(**{"encode.chunks": 2})
-        assert shmr_amd.get_tuning("encode.chunks") == 2
-        assert "chunks=2" in shmr_amd.describe_variant(False, 8, 3)
-        with pytest.raises(shmr_amd.Error):
-            shmr_amd.set_tuning(chunks=3)
-        with pytest.raises(shmr_amd.Error):
-            shmr_amd.set_tuning(no_such_knob=1)
-    finally:
-        shmr_amd.set_tuning(**{"encode.chunks": saved})
+    # product library: kernel knobs are the measured policy; a knob can only be
+    # "set" to its default (the restore pattern of callers), nothing else
+    assert _native.lib().shmr_ec_is_tools_build() == 0
+    assert b"product" in _native.lib().shmr_ec_version()
+    for key, default in (("encode.chunks", -2), ("chunks", -2), ("grid", -1), ("threads", 256), ("diag", 0),
+                         ("decode.depth", -2), ("occ8", 0)):
+        shmr_amd.set_tuning(**{key: default})
+    for key, value in (("encode.chunks", 2), ("diag", 1), ("decode.diag", 1), ("depth", 3), ("grid", 0),
+                       ("threads", 512), ("spre", 1), ("occ8", 1)):
+        with pytest.raises(shmr_amd.Error) as e:
+            shmr_amd.set_tuning(**{key: value})
+        assert e.value.name == "InvalidArgument", key
+    with pytest.raises(shmr_amd.Error):
+        shmr_amd.set_tuning(no_such_knob=1)
+    assert "diag=0" in shmr_amd.describe_variant(False, 8, 3)
     # the measured policy: 4 output rows -> 2 chunks/lane; NT loads and stores; ring depth 2
     assert "chunks=2" in shmr_amd.describe_variant(False, 10, 4)
     assert "nt_load=1 nt_store=1" in shmr_amd.describe_variant(False, 4, 2)
@@ -239,15 +244,47 @@ def test_native_library_is_required():
     """The package refuses to run without the in-tree .so (no fallback)."""
     assert os.path.exists(_native.LIB_PATH)
     assert _native.LIB_PATH.startswith(os.path.join(ROOT, "shmr_amd"))
-    saved = _native.LIB_PATH
+    saved_paths, saved_libs = dict(_native._PATHS), dict(_native._libs)
     try:
-        _native._lib, keep = None, _native._lib
-        _native.LIB_PATH = "/nonexistent/libshmr_ec.so"
+        _native._libs.clear()
+        _native._PATHS["product"] = "/nonexistent/libshmr_ec.so"
         with pytest.raises(_native.NativeLibraryMissing):
             _native.lib()
     finally:
-        _native.LIB_PATH = saved
-        _native._lib = keep
+        _native._PATHS.clear()
+        _native._PATHS.update(saved_paths)
+        _native._libs.clear()
+        _native._libs.update(saved_libs)
+
+
+def test_tools_build_is_separate():
+    """Measurement-only variants (and the XOR-only diagnostic kernel) live in
+    libshmr_ec_tools.so; objects keep the library they were created with."""
+    with _native.tools() as T:
+        assert T.shmr_ec_is_tools_build() == 1 and b"tools" in T.shmr_ec_version()
+        assert T.shmr_ec_build_id() == _native.lib().shmr_ec_build_id()   # same kernel sources
+        saved = shmr_amd.get_tuning("encode.chunks")
+        try:
+            shmr_amd.set_tuning(**{"encode.chunks": 2})
+            assert shmr_amd.get_tuning("encode.chunks") == 2
+            assert "chunks=2" in shmr_amd.describe_variant(False, 8, 3)
+            shmr_amd.set_tuning(**{"encode.diag": 1})
+            assert "diag=1" in shmr_amd.describe_variant(False, 8, 3)
+            with pytest.raises(shmr_amd.Error):
+                shmr_amd.set_tuning(chunks=3)
+            rs = shmr_amd.ReedSolomon(8, 3)
+        finally:
+            shmr_amd.set_tuning(**{"encode.chunks": saved, "encode.diag": 0})
+    assert rs._L is _native._libs["tools"]
+    assert shmr_amd.ReedSolomon(8, 3)._L is _native._libs["product"]
+    assert _native.flavour() == "product"
+    # the tools knobs never reached the product library
+    assert shmr_amd.get_tuning("encode.chunks") == -2 and shmr_amd.get_tuning("encode.diag") == 0
+
+
+def test_build_id_is_a_kernel_hash():
+    bid = _native.lib().shmr_ec_build_id().decode()
+    assert re.fullmatch(r"[0-9a-f]{12}", bid), bid
 
 
 def test_host_register_rejects_non_contiguous():
@@ -308,3 +345,22 @@ def test_batch_tensor_bounds_checked_before_launch():
 def test_path_stats_api():
     z, s = shmr_amd.path_stats()
     assert z >= 0 and s >= 0
+
+
+def _kernel_flags(path):
+    """Template flags F of every gf_apply_kernel<R, U, MODE, F> in a library."""
+    data = open(path, "rb").read()
+    return {int(m) for m in re.findall(rb"gf_apply_kernelILi\d+ELi\d+ELi\d+ELi(\d+)E", data)}
+
+
+def test_product_library_has_no_diagnostic_kernel():
+    """The XOR-only kernel (flag 16, wrong results by design) and the other
+    measurement-only instantiations are compiled into the tools build only."""
+    KDIAG, KDEPTH2 = 16, 512
+    product = _kernel_flags(_native._PATHS["product"])
+    tools = _kernel_flags(_native._PATHS["tools"])
+    assert product and not any(f & KDIAG for f in product)
+    assert any(f & KDIAG for f in tools)
+    # every product full-tile kernel (MODE 0) is a depth-2 ring with nontemporal stores
+    assert all(f & KDEPTH2 and f & 2 for f in product if f != 0)
+    assert product < tools

@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 import shmr_amd
+from shmr_amd import _native
 from oracle import c_oracle
 from oracle import rs_oracle as O
 
@@ -134,6 +135,15 @@ KNOBS = ("chunks", "nt_load", "nt_store", "scalar_tabs", "occ8", "grid", "thread
 
 
 def _dev_encode_check(gpu, k, p, L, B, pitch=None, **knobs):
+    """Encode on the device and compare with the oracle.  With knobs: the
+    measurement variant from the tools build (libshmr_ec_tools.so)."""
+    if knobs:
+        with _native.tools():
+            return _dev_encode_check_in(gpu, k, p, L, B, pitch, knobs)
+    return _dev_encode_check_in(gpu, k, p, L, B, pitch, knobs)
+
+
+def _dev_encode_check_in(gpu, k, p, L, B, pitch, knobs):
     import torch
     saved = {f"encode.{kk}": shmr_amd.get_tuning(f"encode.{kk}") for kk in KNOBS}
     shmr_amd.set_tuning(**{f"encode.{kk}": v for kk, v in knobs.items()})
@@ -190,7 +200,12 @@ def test_encode_batch_dev_tuning_variants(gpu, knobs, k, p):
 
 
 def test_reconstruct_variants_match(gpu):
-    """Every decode variant produces identical bytes."""
+    """Every decode variant (tools build) produces identical bytes."""
+    with _native.tools():
+        _reconstruct_variants_match(gpu)
+
+
+def _reconstruct_variants_match(gpu):
     import torch
     k, p, S, B = 8, 3, 65536 * 3 + 4096 + 32, 6
     pitch = (S + 255) // 256 * 256
@@ -221,6 +236,11 @@ def test_reconstruct_variants_match(gpu):
 
 
 def test_uncompiled_variant_is_reported(gpu):
+    with _native.tools():
+        _uncompiled_variant_is_reported(gpu)
+
+
+def _uncompiled_variant_is_reported(gpu):
     import torch
     saved = {f"encode.{kk}": shmr_amd.get_tuning(f"encode.{kk}") for kk in KNOBS}
     try:

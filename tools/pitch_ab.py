@@ -20,6 +20,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
+os.environ.setdefault("SHMR_EC_FLAVOUR", "tools")   # kernel knobs: the tools build
 import shmr_amd  # noqa: E402
 
 

@@ -63,7 +63,29 @@ def main():
         return total
 
     fetch, write = counter("FETCH_SIZE"), counter("WRITE_SIZE")
+    # The bench line of the kernel-trace run names the library build and the
+    # kernel variant that ran; bench.py reports this record's traffic only
+    # while both still match (traffic_source).
+    build_id = variant = None
+    logs = [os.path.join(a.dir, "kt.log")] + [os.path.join(a.dir, c + ".log") for c in ("FETCH_SIZE", "WRITE_SIZE")]
+    seen = set()
+    for log in logs:
+        try:
+            with open(log) as f:
+                for line in f:
+                    if line.startswith("{"):
+                        b = json.loads(line)
+                        seen.add((b["library"]["build_id"], b["config"]["tuning"], b["config"]["blocks_per_gpu"]))
+        except (OSError, ValueError, KeyError):
+            pass
+    if len(seen) == 1:
+        build_id, variant, blocks = seen.pop()
+        assert blocks == a.blocks, (blocks, a.blocks)
+    elif seen:
+        raise SystemExit(f"passes ran different builds/variants: {seen}")
     rec = {
+        "build_id": build_id,
+        "variant": variant,
         "blocks": a.blocks,
         "kernel": main_name if not a.sum_kernels else names,
         "calls": dur[main_name][0] if main_name else None,
