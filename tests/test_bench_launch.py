@@ -103,8 +103,17 @@ def test_traffic_is_reported_only_for_the_profiled_build(tmp_path, monkeypatch):
     assert t is None and src["status"] == "no record for this config"
 
 
-def test_cpu_threads_default_is_the_affinity_set():
+def test_cpu_threads_default_is_available_parallelism(monkeypatch):
+    """rayon's default pool = std::thread::available_parallelism(): the
+    affinity set capped by the cgroup v2 quota (rounded up)."""
     sys.path.insert(0, ROOT)
     import bench
-    assert bench.cpu_threads(0) == len(os.sched_getaffinity(0))
+    aff = len(os.sched_getaffinity(0))
+    monkeypatch.setattr(bench, "cpu_quota", lambda: None)
+    assert bench.cpu_threads(0) == aff
+    monkeypatch.setattr(bench, "cpu_quota", lambda: 1.5)
+    assert bench.cpu_threads(0) == min(aff, 2)
+    monkeypatch.setattr(bench, "affinity_cores", lambda: 256)
+    monkeypatch.setattr(bench, "cpu_quota", lambda: 16.0)
+    assert bench.cpu_threads(0) == 16
     assert bench.cpu_threads(5) == 5
