@@ -370,11 +370,45 @@ def calculate_shard_size(length: int, data_shards: int) -> int:
     return int(np.ceil(np.float32(q)))
 
 
-def sync_data_erasure(buffer: bytes, size: int, data: int, parity: int) -> List[np.ndarray]:
+class ReferencePanic(Exception):
+    """Where the reference binary would panic (debug-build integer overflow
+    check, or an ``.unwrap()`` on a crate error).  ``.cause`` names it."""
+
+    def __init__(self, cause: str):
+        super().__init__(cause)
+        self.cause = cause
+
+
+SYNC_MODES = ("release", "debug", "refuse")
+
+
+def sync_data_erasure(buffer: bytes, size: int, data: int, parity: int,
+                      mode: str = "release") -> List[np.ndarray]:
     """src/vfs/block.rs:404-440 -- shards that the Erasure arm writes.
 
     Returns [] for an empty buffer (block.rs:389-391 writes nothing).
+
+    ``block.rs:421`` appends ``parity + (data - nchunks as u8)`` zero shards,
+    computed in u8.  ``nchunks`` exceeds ``data`` only past the f32 shard-size
+    hazard (``calculate_shard_size``; first at 16,777,217 B for k = 8).  What
+    happens then depends on the build (``mode``):
+
+    * ``"release"`` (default; the reference's shipped profile,
+      ``Cargo.toml:10-13``, has no overflow checks): both u8 operations wrap,
+      so with nchunks = k + e it appends ``(p - e) mod 256`` zero shards.  For
+      e <= p that is exactly k + p shards: encode SUCCEEDS and the trailing
+      data chunks k..k+e-1 are overwritten by parity rows (their bytes are
+      lost from the shard files).  (e > p would leave 256 extra shards, the
+      crate's encode would return TooManyShards and the ``.unwrap()`` at
+      ``block.rs:427`` panic; unreachable, since the f32 error keeps k*S
+      within k bytes of ``size``, so e <= 1 <= p.)
+    * ``"debug"``: the subtraction's overflow check panics at block.rs:421.
+    * ``"refuse"``: the MI355X mirror's default -- ``TooManyDataShards``
+      before any shard is written (a documented deviation: it refuses the
+      silent data loss).  Raises RSError("TooManyDataShards").
     """
+    if mode not in SYNC_MODES:
+        raise ValueError(f"mode must be one of {SYNC_MODES}")
     buf = _as_u8(buffer)
     if len(buf) == 0:
         return []
@@ -386,13 +420,19 @@ def sync_data_erasure(buffer: bytes, size: int, data: int, parity: int) -> List[
         chunk = buf[off:off + s]
         c[:len(chunk)] = chunk
         shards.append(c)
-    if len(shards) > data:
-        # block.rs:421 computes `data - nchunks` in u8: this underflows and
-        # the reference panics (debug) or fails encode (release).
-        raise RSError("ShardCountOverflow")
-    for _ in range(parity + (data - len(shards))):     # block.rs:421-423
+    nchunks = len(shards)
+    if nchunks > data:
+        if mode == "refuse":
+            raise RSError("TooManyDataShards")
+        if mode == "debug":
+            raise ReferencePanic("attempt to subtract with overflow (block.rs:421)")
+    extra = (parity + ((data - nchunks) & 0xFF)) & 0xFF   # block.rs:421, u8 arithmetic
+    for _ in range(extra):                              # block.rs:421-423
         shards.append(np.zeros(s, dtype=np.uint8))
-    r.encode(shards)                                    # block.rs:427
+    try:
+        r.encode(shards)                                # block.rs:427
+    except RSError as e:
+        raise ReferencePanic(f"called `Result::unwrap()` on an `Err` value: {e.name} (block.rs:427)") from e
     return shards
 
 

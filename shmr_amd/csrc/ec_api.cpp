@@ -176,6 +176,10 @@ int shmr_ec_describe_variant(int decode, uint32_t data_shards, uint32_t rows, ch
                   v.u, int(v.nt_load), int(v.nt_store), int(v.scalar_tabs), int(v.occ8), v.threads,
                   core::grid_mode(op), int(v.diag), v.depth, v.wgs_per_cu, v.occ, int(v.early), int(v.spre), int(v.fuse_tail),
                   int(compiled));
+    if (v.glds) {   // appended only when set: records keyed by the string stay valid
+        const size_t n = std::strlen(buf);
+        if (n + 1 < len) std::snprintf(buf + n, len - n, " glds=1");
+    }
     return SHMR_EC_OK;
 }
 

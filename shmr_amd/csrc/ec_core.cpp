@@ -35,6 +35,7 @@ struct Tuning {
     std::atomic<int> early{kAuto};
     std::atomic<int> spre{kAuto};
     std::atomic<int> fuse_tail{kAuto};
+    std::atomic<int> glds{kAuto};
 };
 Tuning g_tune[2];   // [kEncode], [kDecode]
 std::atomic<int> g_bounce_kib{kBounceKibDefault};
@@ -136,7 +137,8 @@ int set_tuning(const char* key, int value) {
         static const std::map<std::string, int> kDefaults = {
             {"chunks", kAuto}, {"nt_load", kAuto}, {"nt_store", kAuto}, {"scalar_tabs", 0}, {"occ8", 0},
             {"grid", -1},      {"diag", 0},        {"threads", 256},    {"depth", kAuto},   {"wgs_per_cu", 0},
-            {"occ", kAuto},    {"early", kAuto},   {"spre", kAuto},     {"fuse_tail", kAuto}};
+            {"occ", kAuto},    {"early", kAuto},   {"spre", kAuto},     {"fuse_tail", kAuto},
+            {"glds", kAuto}};
         const auto it = kDefaults.find(k);
         return (it != kDefaults.end() && it->second == value) ? SHMR_EC_OK : SHMR_EC_INVALID_ARGUMENT;
     }
@@ -177,6 +179,8 @@ int set_tuning(const char* key, int value) {
             T.spre = value == kAuto ? kAuto : (value != 0);
         } else if (k == "fuse_tail") {
             T.fuse_tail = value == kAuto ? kAuto : (value != 0);
+        } else if (k == "glds") {
+            T.glds = value == kAuto ? kAuto : (value != 0);
         } else {
             return SHMR_EC_INVALID_ARGUMENT;
         }
@@ -207,6 +211,7 @@ int get_tuning(const char* key) {
     if (k == "early") return T.early;
     if (k == "spre") return T.spre;
     if (k == "fuse_tail") return T.fuse_tail;
+    if (k == "glds") return T.glds;
     return SHMR_EC_INVALID_ARGUMENT;
 }
 
@@ -228,6 +233,8 @@ kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_m
     if (T.early.load() != kAuto) v.early = T.early.load() != 0;
     if (T.spre.load() != kAuto) v.spre = T.spre.load() != 0;
     if (T.fuse_tail.load() != kAuto) v.fuse_tail = T.fuse_tail.load() != 0;
+    if (T.glds.load() != kAuto) v.glds = T.glds.load() != 0;
+    if (v.glds) v.early = v.spre = v.scalar_tabs = false;   // the LDS-DMA ring is a form of the plain tile
     return v;
 }
 
@@ -256,7 +263,7 @@ kern::Variant launch_variant(OpClass op, unsigned k, unsigned rows, bool host_ma
     v.ptrs = ptrs;
     v.segs = segs;
     if (ptrs) {
-        v.early = v.spre = v.scalar_tabs = false;   // only the plain LDS-staged tile reads pointer tables
+        v.early = v.spre = v.scalar_tabs = v.glds = false;   // only the plain LDS-staged tile reads pointer tables
         kern::Variant lean = v;
         lean.fuse_tail = false;
         if (!kern::variant_compiled(lean)) {   // tuned knobs without a pointer-table build: the mapped policy

@@ -57,6 +57,10 @@ constexpr int kFuse = 1 << 18;   // leading partial tiles (ApplyArgs::lead_tails
 // byte-granular kernels (MODE 1, 2) always support both.
 constexpr int kPtrs = 1 << 19;   // shard-pointer tables (ApplyArgs::shard_ptrs)
 constexpr int kSegs = 1 << 20;   // segment launches (ApplyArgs::segs)
+// Input ring in LDS filled by LDS-DMA (global_load_lds_dwordx4): the shards
+// in flight cost no VGPRs, so a wave can keep depth-1 shards of loads in flight
+// at the register budget of one (full tiles only; tails take the register ring).
+constexpr int kGlds = 1 << 21;
 
 template <int MODE, int F>
 constexpr bool has_ptrs() {
@@ -205,6 +209,7 @@ struct Ctx {
     const uint16_t* g_in_idx;   // plan image (kScalarTabs)
     const uint16_t* g_out_idx;
     const uint32_t* g_tab;      // plan image PermTab array, [k][m][8] dwords
+    uint8_t* ring;              // LDS input ring (kGlds): [depth][U][threads][16 B]
 };
 
 template <int R, int F>
@@ -271,6 +276,62 @@ __device__ __forceinline__ void do_tile(const ApplyArgs& a, const Ctx& c, const 
         for (int u = 0; u < U; ++u) mac<R, F>(acc[u], buf[u], tb);
     };
 
+    if constexpr ((F & kGlds) != 0 && MODE == 0) {
+        // LDS ring: slot s holds shard (t mod NB)'s U x 16 B per lane, lane-linear
+        // per wave (LDS-DMA writes wave base + lane * 16).  Each lane reads back
+        // only the bytes its own wave's DMA wrote, so the covering vmcnt orders
+        // the ds_read (no barrier); the slot a DMA refills was last read one step
+        // earlier, and those reads have returned (their values were used).
+        constexpr int NB = depth_of<F>();
+        constexpr int AUX = (F & kNtLoad) ? 2 : 0;   // nt
+        const uint32_t wave_base = (tid & ~63u) * 16;
+        auto gload = [&](int slot, uint32_t t) {
+            const uint32_t tt = t < k ? t : k - 1;
+            const uint8_t* base = ib + in_off<F>(a, c, tt) + col0 + uint64_t(tid) * 16;
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                __builtin_amdgcn_global_load_lds(
+                    (__attribute__((address_space(1))) void*)(uintptr_t)(base + uint64_t(u) * TH * 16),
+                    (__attribute__((address_space(3))) void*)(c.ring + (slot * U + u) * TH * 16 + wave_base), 16, 0,
+                    AUX);
+        };
+        auto consume_lds = [&](int slot, uint32_t t) {
+            Tab tb[R];
+            read_tabs<R, F>(a, c, t, tb);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const u32x4 v = *reinterpret_cast<const u32x4*>(c.ring + ((slot * U + u) * TH + tid) * 16);
+                mac<R, F>(acc[u], v, tb);
+            }
+        };
+        // vmcnt(N) with expcnt / lgkmcnt left alone (gfx9 encoding)
+        constexpr int VM = (NB - 1) * U;
+        constexpr int WAIT = (VM & 15) | ((VM >> 4) << 14) | (7 << 4) | (15 << 8);
+#pragma unroll
+        for (int i = 0; i < NB - 1; ++i) gload(i, i);
+        __builtin_amdgcn_sched_barrier(0);
+        for (uint32_t t = 0; t < k; t += NB) {
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+                gload((i + NB - 1) % NB, t + i + NB - 1);
+                __builtin_amdgcn_s_waitcnt(WAIT);   // shard t+i has landed in slot i
+                __builtin_amdgcn_sched_barrier(0);
+                if (t + i < k) consume_lds(i, t + i);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): no DMA into LDS outlives the tile
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            uint8_t* o = ob + out_off<F>(a, c, r);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                st<MODE, F>(o, col0 + (uint64_t(u) * TH + tid) * 16, len,
+                            u32x4{acc[u][r][0], acc[u][r][1], acc[u][r][2], acc[u][r][3]});
+        }
+        return;
+    }
+
     // sched_barrier(0) pins program order: without it the scheduler sinks the
     // look-ahead loads next to their consumers and the wave drains vmcnt(0)
     // every shard (no overlap of HBM latency with the GF math).
@@ -280,7 +341,9 @@ __device__ __forceinline__ void do_tile(const ApplyArgs& a, const Ctx& c, const 
     // t+1 .. t+NB-1 are in flight.  Every load is unconditional (a branch
     // around a load makes the compiler's waitcnt merge fall back to
     // vmcnt(0)): past the last shard it re-reads shard k-1, an L2 hit.
-    constexpr int NB = depth_of<F>();
+    // (LDS-DMA kernels size their LDS ring by depth; their bounds-checked tail
+    // tiles take a register ring of depth 1: load, wait, multiply)
+    constexpr int NB = (F & kGlds) ? 1 : depth_of<F>();
     u32x4 ring[NB][U];
 #pragma unroll
     for (int i = 0; i < NB - 1; ++i) load(ring[i], i);
@@ -302,6 +365,11 @@ __device__ __forceinline__ void do_tile(const ApplyArgs& a, const Ctx& c, const 
             st<MODE, F>(o, col0 + (uint64_t(u) * TH + tid) * 16, len,
                         u32x4{acc[u][r][0], acc[u][r][1], acc[u][r][2], acc[u][r][3]});
     }
+}
+
+// Byte offset of the LDS input ring (kGlds) behind the staged plan.
+__host__ __device__ inline uint32_t glds_ring_off(uint32_t k, uint32_t R) {
+    return (k * R * 32 + k * 8 + R * 8 + 255) & ~255u;
 }
 
 // Stages rows [row0, row0 + R) of a plan image into LDS:
@@ -335,6 +403,7 @@ __device__ __forceinline__ void stage_plan(const ApplyArgs& a, const uint8_t* pl
     c.s_tab = s_tab;
     c.s_in_off = s_in_off;
     c.s_out_off = s_out_off;
+    c.ring = smem + glds_ring_off(k, R);
 }
 
 // ---- early-prefetch tile (flag kEarly) -------------------------------------
@@ -675,6 +744,8 @@ template <int R, int U, int MODE, int F>
 hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStream_t stream) {
     auto kern = gf_apply_kernel<R, U, MODE, F>;
     size_t lds = (F & (kScalarTabs | kSPre)) ? 0 : size_t(a.k) * R * 32 + size_t(a.k) * 8 + size_t(R) * 8;
+    if constexpr ((F & kGlds) != 0)
+        lds = glds_ring_off(a.k, R) + size_t(depth_of<F>()) * U * threads_of<F>() * 16;
     // Optional occupancy cap: pad the LDS allocation so at most wgs_per_cu
     // workgroups fit in a CU's 160 KiB.
     if (v.wgs_per_cu > 0) {
@@ -783,7 +854,21 @@ hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStr
     X(1, kNtLoad | kNtStore | kDepth2 | kEarly | (6 << kOccShift)) \
     X(1, kNtLoad | kNtStore | kDepth2 | kSPre) \
     X(2, kNtLoad | kNtStore | kDepth2 | kSPre) \
-    X(1, kNtLoad | kNtStore | kSPre)
+    X(1, kNtLoad | kNtStore | kSPre) \
+    X(1, kNtLoad | kNtStore | kGlds) \
+    X(1, kNtLoad | kNtStore | kGlds | kDepth5) \
+    X(1, kNtLoad | kNtStore | kGlds | kDepth9) \
+    X(2, kNtLoad | kNtStore | kGlds) \
+    X(2, kNtLoad | kNtStore | kGlds | kDepth5) \
+    X(1, kNtLoad | kNtStore | kGlds | kFuse) \
+    X(1, kNtLoad | kNtStore | kGlds | kDepth5 | kFuse) \
+    X(1, kNtLoad | kNtStore | kGlds | kDepth9 | kFuse) \
+    X(2, kNtLoad | kNtStore | kGlds | kFuse) \
+    X(2, kNtLoad | kNtStore | kGlds | kDepth5 | kFuse) \
+    X(1, kNtLoad | kNtStore | kGlds | kSegs) \
+    X(1, kNtLoad | kNtStore | kGlds | kDepth5 | kSegs) \
+    X(1, kNtLoad | kNtStore | kGlds | kSegs | kFuse) \
+    X(1, kNtLoad | kNtStore | kGlds | kDepth5 | kSegs | kFuse)
 #define SHMR_VARIANTS(X) SHMR_VARIANTS_PRODUCT(X) SHMR_VARIANTS_TOOLS(X)
 #else
 #define SHMR_VARIANTS(X) SHMR_VARIANTS_PRODUCT(X)
@@ -795,7 +880,7 @@ int variant_flags(const Variant& v) {
            (v.threads == 512 ? kTh512 : 0) | (v.depth == 5 ? kDepth5 : 0) | (v.depth == 9 ? kDepth9 : 0) |
            (v.depth == 2 ? kDepth2 : 0) | (v.depth == 1 ? kDepth1 : 0) | ((v.occ & 15) << kOccShift) |
            (v.early ? kEarly : 0) | (v.spre ? kSPre : 0) | (v.fuse_tail ? kFuse : 0) | (v.ptrs ? kPtrs : 0) |
-           (v.segs ? kSegs : 0);
+           (v.segs ? kSegs : 0) | (v.glds ? kGlds : 0);
 }
 
 template <int R>

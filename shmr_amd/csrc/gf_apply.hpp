@@ -91,6 +91,7 @@ struct Variant {
     bool fuse_tail = false;  // partial last tiles inside the full-tile launch (ApplyArgs::lead_tails)
     bool ptrs = false;       // full-tile kernel that reads shard-pointer tables (set by launch_set)
     bool segs = false;       // full-tile kernel that takes segment launches (set by launch_set)
+    bool glds = false;       // input ring in LDS filled by LDS-DMA (depth = slots; full tiles only)
 };
 
 // rows in [1, kMaxRowsPerLaunch].  mode 0: full tiles, every shard base

@@ -458,16 +458,41 @@ namespace {
 // at i*S (the buffer itself), the last one zero-padded, then zero data shards
 // up to k, then p parity slots -- i.e. the buffer zero-extended to k*S with
 // parity at k*S.  Caller holds the buffer lock.
-Status prepare_erasure(BlockBuffer& buf, const BlockTopology& t, size_t S) {
-    if (buf.size() > size_t(t.data) * S) {
-        // block.rs:421 computes `data - nchunks` in u8: the reference panics
-        // (debug) or overwrites a data chunk with parity (release).
-        return ec_error(SHMR_EC_TOO_MANY_DATA_SHARDS);
-    }
+//
+// A buffer longer than k*S (only past calculate_shard_size's f32 hazard,
+// e.g. 16,777,217 B at k = 8: nchunks = k + 1) makes block.rs:421's
+// `parity + (data - nchunks as u8)` underflow.  Default: refuse with
+// TooManyDataShards before any shard is written.  With
+// VfsOptions::release_u8_wrap the reference's release build is reproduced
+// (Cargo.toml:10-13, no overflow checks): the u8 arithmetic wraps to
+// (p - e) mod 256 zero shards, encode sees exactly k+p shards when e <= p and
+// writes parity over chunks k..k+e-1 -- in the shard files only: the
+// reference encoded copies (chunks().to_vec()), so its Block Cache buffer
+// keeps the data.  The overwritten buffer bytes [k*S, len) are saved in
+// *tail and restore_tail() puts them back after the shard writes.
+Status prepare_erasure(BlockBuffer& buf, const BlockTopology& t, size_t S, bool release_u8_wrap,
+                       std::vector<uint8_t>* tail) {
     const size_t len = buf.size();
+    const size_t kS = size_t(t.data) * S;
+    tail->clear();
+    if (len > kS) {
+        if (!release_u8_wrap) return ec_error(SHMR_EC_TOO_MANY_DATA_SHARDS);
+        const size_t nchunks = (len + S - 1) / S;
+        const unsigned extra = uint8_t(t.parity + uint8_t(t.data - uint8_t(nchunks)));   // block.rs:421, wrapping
+        if (nchunks + extra != size_t(t.data) + t.parity)
+            return ec_error(nchunks + extra < size_t(t.data) + t.parity ? SHMR_EC_TOO_FEW_SHARDS
+                                                                         : SHMR_EC_TOO_MANY_SHARDS);   // .unwrap() panics there
+        buf.reserve((size_t(t.data) + t.parity) * S);
+        tail->assign(buf.data() + kS, buf.data() + len);
+        return std::nullopt;
+    }
     buf.reserve((size_t(t.data) + t.parity) * S);
-    std::memset(buf.data() + len, 0, size_t(t.data) * S - len);
+    std::memset(buf.data() + len, 0, kS - len);
     return std::nullopt;
+}
+
+void restore_tail(BlockBuffer& buf, const BlockTopology& t, size_t S, const std::vector<uint8_t>& tail) {
+    if (!tail.empty()) std::memcpy(buf.data() + size_t(t.data) * S, tail.data(), tail.size());
 }
 
 void shard_ptrs(BlockBuffer& buf, size_t n, size_t S, uint8_t** out) {
@@ -581,16 +606,21 @@ Status VirtualBlock::sync_data(bool force, int device) const {
             if (rc != SHMR_EC_OK) return ec_error(rc);
         }
         const size_t S = shard_size();                                      // block.rs:406
-        if (auto e = prepare_erasure(buffer, topology, S)) return e;
+        std::vector<uint8_t> tail;
+        if (auto e = prepare_erasure(buffer, topology, S, opt_.release_u8_wrap, &tail)) return e;
         const size_t n = size_t(topology.data) + topology.parity;
         std::vector<uint8_t*> ptrs(n);
         shard_ptrs(buffer, n, S, ptrs.data());
         es = r->encode_in_place(ptrs.data(), n, S);   // block.rs:427 (.unwrap() in the reference)
-        if (!es.ok()) return ec_error(es.code);
+        if (!es.ok()) {
+            restore_tail(buffer, topology, S, tail);
+            return ec_error(es.code);
+        }
         parallel_for(std::min(n, nh), 16, [&](size_t i) {   // block.rs:436-439, in parallel
             res[i] = st_->ensure_fd(i, *cfg_);
             if (!res[i]) res[i] = write_path(st_->handles[i].second, ptrs[i], S, opt_.fsync_shards);
         });
+        restore_tail(buffer, topology, S, tail);
     } else {
         const size_t copies = topology.kind == BlockTopology::Single ? 1 : std::min<size_t>(topology.n, nh);
         parallel_for(copies, 16, [&](size_t i) {
@@ -1007,6 +1037,7 @@ Status VirtualFile::sync_data(bool force) {
         parallel_for(need.size(), 16, [&](size_t j) { results[need[j]] = blocks[need[j]].open_handles(); });
     }
     BatchLocks locks;
+    std::vector<std::vector<uint8_t>> tails(blocks.size());   // release_u8_wrap only
     for (auto& kv : groups) {
         Group& g = kv.second;
         std::vector<size_t> live;
@@ -1015,7 +1046,8 @@ Status VirtualFile::sync_data(bool force) {
             VirtualBlock& b = blocks[i];
             locks.held.emplace_back(b.st_->buf_mu);
             if (b.st_->buffer.empty()) continue;   // block.rs:389-391: nothing to write
-            if ((results[i] = prepare_erasure(b.st_->buffer, b.topology, g.S))) continue;
+            if ((results[i] = prepare_erasure(b.st_->buffer, b.topology, g.S, b.opt_.release_u8_wrap, &tails[i])))
+                continue;
             locks.held.emplace_back(b.st_->handles_mu);
             live.push_back(i);
         }
@@ -1070,8 +1102,11 @@ Status VirtualFile::sync_data(bool force) {
         });
         for (size_t t = 0; t < tasks.size(); ++t)
             if (task_res[t] && !results[tasks[t].blk]) results[tasks[t].blk] = task_res[t];
-        for (size_t j = bt.b; j < bt.e; ++j)
-            if (!results[g.members[j]]) blocks[g.members[j]].st_->should_flush.store(false);
+        for (size_t j = bt.b; j < bt.e; ++j) {
+            const size_t i = g.members[j];
+            restore_tail(blocks[i].st_->buffer, blocks[i].topology, g.S, tails[i]);
+            if (!results[i]) blocks[i].st_->should_flush.store(false);
+        }
     };
     const double t1 = now_s();
     double io_busy = 0;

@@ -115,6 +115,13 @@ struct VfsOptions {
     // runs zero-copy on them); falls back to pageable memory when no device is
     // present.
     bool pinned_buffers = false;
+    // sync_data of a buffer longer than k*S (calculate_shard_size's f32
+    // hazard, e.g. 16,777,217 B at Erasure(1,8,3)): off = refuse with
+    // EcError(TooManyDataShards) before any write (the default: the
+    // reference silently loses data there); on = the reference's release
+    // build bit for bit (block.rs:421's u8 arithmetic wraps, parity row 0
+    // overwrites data chunk k in the shard files; Cargo.toml:10-13).
+    bool release_u8_wrap = false;
     // fsync every shard file after writing it (write_path, block.rs:633).
     // Benchmarks may turn it off to separate the device path from the disk.
     bool fsync_shards = true;
@@ -236,6 +243,16 @@ public:
     // block (the file-level form of replace_block; the reference's D-Bus
     // RewriteFile is todo!(), dbus.rs:46): batched load, batched encode.
     Status rewrite_erasure(uint8_t data, uint8_t parity);
+
+    // Durable record of the file: ino, size, chunk_size, every block's ino,
+    // idx, size, BlockTopology and shard paths, block_size -- the fields the
+    // reference's serde derives persist in the superblock as serde_yaml
+    // (src/vfs/mod.rs:35-56, block.rs:22-30,119-158, path.rs:20-28,
+    // databunny.rs:297-327; record.cpp).  A loaded file needs populate(cfg).
+    std::string to_yaml() const;
+    static Status from_yaml(const std::string& text, VirtualFile* out, std::string* err = nullptr);
+    Status save_record(const fs::path& path) const;   // write + fsync a temp file, rename over path
+    static Status load_record(const fs::path& path, VirtualFile* out, std::string* err = nullptr);
 
 private:
     Status allocate_block();

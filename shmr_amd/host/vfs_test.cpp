@@ -249,6 +249,52 @@ void test_erasure_f32_hazard() {
     CHECK(fsize(shard_file(*cfg, b, 0)) == 0 && fsize(shard_file(*cfg, b, 10)) == 0);
 }
 
+// VfsOptions::release_u8_wrap: the same hazard with the reference's release
+// build reproduced (block.rs:421 wraps, Cargo.toml:10-13) on both flush paths
+// -- VirtualBlock::sync_data (block 0) and a batched VirtualFile::sync_data
+// (block 1).  Shard files and the reloaded block are compared with the oracle
+// (sync_data_erasure / load_block_erasure, mode "release") by the Python side;
+// here: the Block Cache buffer still holds the caller's data after the flush
+// (the reference encoded chunks().to_vec() copies).
+void test_erasure_f32_hazard_release() {
+    auto cfg = test_config();
+    auto in = read_input();
+    const uint64_t size = 16777217;
+    CHECK(in.size() == size);
+    VfsOptions o;
+    o.release_u8_wrap = true;
+    o.fsync_shards = false;
+    VirtualBlock b;
+    CHECK_OK(VirtualBlock::create(15, 0, cfg, size, BlockTopology::erasure(1, 8, 3), &b));
+    b.set_options(o);
+    size_t n = 0;
+    CHECK_OK(b.write(0, in.data(), in.size(), &n));
+    CHECK_OK(b.sync_data(true));
+    CHECK(b.buffer_snapshot() == in);
+    print_shards(*cfg, 0, b);
+    CHECK_OK(b.drop_buffer());
+    CHECK_OK(b.drop_handles());
+    std::vector<uint8_t> rb(size);
+    CHECK_OK(b.read(0, rb.data(), rb.size(), &n));
+    CHECK(n == size);
+    FILE* f = std::fopen((g_bucket + "/loaded_release.bin").c_str(), "wb");
+    std::fwrite(rb.data(), 1, rb.size(), f);
+    std::fclose(f);
+
+    VirtualFile vf = VirtualFile::new_with(16, 0);
+    vf.populate(cfg);
+    vf.pipeline_batch_bytes = 0;   // the batched (shmr_ec_encode_blocks_host) flush
+    VirtualBlock c;
+    CHECK_OK(VirtualBlock::create(16, 0, cfg, size, BlockTopology::erasure(1, 8, 3), &c));
+    vf.blocks.push_back(c);
+    vf.set_options(o);
+    CHECK_OK(vf.blocks[0].write(0, in.data(), in.size(), &n));
+    CHECK_OK(vf.sync_data(true));
+    CHECK(vf.last_sync.blocks == 1);
+    CHECK(vf.blocks[0].buffer_snapshot() == in);
+    print_shards(*cfg, 1, vf.blocks[0]);
+}
+
 void test_virtual_file_1() {   // mod.rs:322-349
     auto cfg = test_config();
     VirtualFile vf = VirtualFile::new_with(g_rng() >> 16, 0);
@@ -641,6 +687,126 @@ void test_rewrite_erasure() {
     CHECK_OK(vf.rewrite_erasure(4, 2));   // already Erasure(1, 4, 2): no-op
 }
 
+// The durable VirtualFile record (record.cpp; the reference's serde_yaml
+// superblock value): every topology and awkward strings round-trip, the text
+// has the serde shape, hand-written flow/quoted forms parse, bad records fail.
+void test_virtual_file_record_roundtrip() {
+    auto cfg = std::make_shared<ShmrFsConfig>(*test_config());
+    cfg->pools["test_pool"]["b: #2"] = Bucket{g_bucket, 999, 998, BucketPriority::Normal};
+    VirtualFile vf = VirtualFile::new_with(21, 4242);
+    vf.populate(cfg);
+    vf.block_size = 1 << 20;
+    VirtualBlock s, m, e;
+    CHECK_OK(VirtualBlock::create(21, 1, cfg, 1 << 20, BlockTopology::single(), &s));
+    CHECK_OK(VirtualBlock::create(21, 2, cfg, 1 << 20, BlockTopology::mirror(3), &m));
+    CHECK_OK(VirtualBlock::create(21, 3, cfg, 4 << 20, BlockTopology::erasure(1, 8, 3), &e));
+    m.shards[1].pool = "-odd";
+    m.shards[2].filename = "it's";
+    e.shards[4].bucket = "true";
+    vf.blocks = {s, m, e};
+    const std::string text = vf.to_yaml();
+    CHECK(text.rfind("ino: 21\nsize: 4242\nchunk_size: 4096\nblocks:\n- ino: 21\n  idx: 1\n  size: 1048576\n"
+                     "  topology: Single\n  shards:\n  - pool: test_pool\n    bucket: ", 0) == 0);
+    CHECK(text.find("  topology: !Mirror 3\n") != std::string::npos);
+    CHECK(text.find("  topology: !Erasure\n  - 1\n  - 8\n  - 3\n  shards:\n") != std::string::npos);
+    CHECK(text.find("filename: 21:3_ec83_10.bin\n") != std::string::npos);
+    CHECK(text.find("pool: '-odd'") != std::string::npos && text.find("filename: it's\n") != std::string::npos &&
+          text.find("bucket: 'true'") != std::string::npos);
+    CHECK(text.size() > 13 && text.compare(text.size() - 20, 20, "block_size: 1048576\n") == 0);
+    VirtualFile back;
+    std::string err;
+    CHECK_OK(VirtualFile::from_yaml(text, &back, &err));
+    CHECK(back.ino == 21 && back.size == 4242 && back.chunk_size == 4096 && back.block_size == (1u << 20));
+    CHECK(back.blocks.size() == 3);
+    for (size_t i = 0; i < 3; ++i) {
+        const auto &a = vf.blocks[i], &b = back.blocks[i];
+        CHECK(a.ino == b.ino && a.idx == b.idx && a.size == b.size);
+        CHECK(a.topology.to_string() == b.topology.to_string());
+        CHECK(a.shards.size() == b.shards.size());
+        for (size_t j = 0; j < a.shards.size(); ++j)
+            CHECK(a.shards[j].pool == b.shards[j].pool && a.shards[j].bucket == b.shards[j].bucket &&
+                  a.shards[j].filename == b.shards[j].filename);
+    }
+    CHECK(back.to_yaml() == text);
+    // serde_yaml's other spellings: flow sequence, quoted scalars, document marker
+    const std::string hand =
+        "---\nino: 5\nsize: 10\nchunk_size: 4096\nblocks:\n  - ino: 5\n    idx: 1\n    size: 100\n"
+        "    topology: !Erasure [1, 2, 1]\n    shards:\n      - {pool: x, bucket: y, filename: a}\n";
+    CHECK(VirtualFile::from_yaml(hand, &back, &err));   // flow mappings are not part of the subset
+    const std::string hand2 =
+        "---\nino: 5\nsize: 10\nchunk_size: 4096\nblocks:\n  - ino: 5\n    idx: 1\n    size: 100\n"
+        "    topology: !Erasure [1, 2, 1]   # comment\n    shards:\n      - pool: \"x\"\n        bucket: 'y'\n"
+        "        filename: a\n      - pool: x\n        bucket: y\n        filename: b\n      - pool: x\n"
+        "        bucket: y\n        filename: \"c\\x41\"\nblock_size: 7\n";
+    CHECK_OK(VirtualFile::from_yaml(hand2, &back, &err));
+    CHECK(back.blocks.size() == 1 && back.blocks[0].topology.to_string() == "Erasure(1, 2, 1)");
+    CHECK(back.blocks[0].shards[2].filename == "cA" && back.blocks[0].shards[0].bucket == "y" && back.block_size == 7);
+    CHECK_OK(VirtualFile::from_yaml("ino: 1\nsize: 0\nchunk_size: 4096\nblocks: []\nblock_size: 9\n", &back, &err));
+    CHECK(back.blocks.empty() && back.block_size == 9);
+    // malformed records: FsError(EINVAL) with a reason
+    for (const char* bad : {"ino: 1\n", "ino: x\nsize: 0\nchunk_size: 1\nblocks: []\nblock_size: 1\n",
+                            "ino: 1\nsize: 0\nchunk_size: 1\nblocks:\n- ino: 1\n  idx: 0\n  size: 1\n"
+                            "  topology: !Raid 5\n  shards: []\nblock_size: 1\n",
+                            "ino: 1\nsize: 0\nchunk_size: 1\nblocks:\n- ino: 1\n  idx: 0\n  size: 1\n"
+                            "  topology: !Erasure [1, 300, 1]\n  shards: []\nblock_size: 1\n",
+                            "ino: 1\nsize: 0\nchunk_size: 1\nblocks:\n- ino: 1\n  idx: 0\n  size: 1\n"
+                            "  topology: !Erasure [1, 2, 1]\n  shards: []\nblock_size: 1\n"}) {
+        err.clear();
+        Status st = VirtualFile::from_yaml(bad, &back, &err);
+        CHECK(st && st->kind == ShmrError::FsError && st->code == EINVAL && !err.empty());
+    }
+    // save / load through the file system (temp file + rename)
+    const fs::path rec = fs::path(g_bucket) / "vf21.yaml";
+    CHECK_OK(vf.save_record(rec));
+    CHECK(!fs::exists(rec.string() + ".tmp"));
+    CHECK_OK(VirtualFile::load_record(rec, &back, &err));
+    CHECK(back.to_yaml() == text);
+    Status st = VirtualFile::load_record(fs::path(g_bucket) / "missing.yaml", &back, &err);
+    CHECK(st && st->kind == ShmrError::FsError && st->code == ENOENT);
+}
+
+// a file rewritten to Erasure(1, 8, 3) survives a restart
+// through its record alone -- everything in memory is dropped, the record is
+// reloaded, one shard file of every block is lost, and the file reads back
+// bit-exact (reconstructed on the GPU).
+void test_rewrite_erasure_record_reload() {
+    auto cfg = test_config();
+    auto in = read_input();
+    const fs::path rec = fs::path(g_bucket) / "vf17.yaml";
+    size_t nblk = 0;
+    {
+        VirtualFile vf = VirtualFile::new_with(17, 0);
+        vf.populate(cfg);
+        size_t n = 0;
+        CHECK_OK(vf.write(0, in.data(), in.size(), &n));
+        CHECK_OK(vf.sync_data(true));
+        CHECK_OK(vf.rewrite_erasure(8, 3));
+        nblk = vf.blocks.size();
+        CHECK_OK(vf.save_record(rec));
+        for (size_t i = 0; i < nblk; ++i) print_shards(*cfg, i, vf.blocks[i]);
+        CHECK_OK(vf.drop_buffers());
+        CHECK_OK(vf.drop_handles());
+    }   // the process's view of the file is gone; only the record and the shard files remain
+    VirtualFile vf;
+    std::string err;
+    CHECK_OK(VirtualFile::load_record(rec, &vf, &err));
+    vf.populate(cfg);
+    CHECK(vf.size == in.size() && vf.blocks.size() == nblk);
+    VfsOptions o;
+    o.missing_shard_is_erasure = true;
+    o.pread_from_start = true;
+    vf.set_options(o);
+    for (size_t i = 0; i < nblk; ++i) {
+        CHECK(vf.blocks[i].topology.to_string() == "Erasure(1, 8, 3)");
+        fs::remove(shard_file(*cfg, vf.blocks[i], (3 * i) % 11));
+    }
+    std::vector<uint8_t> rb(in.size());
+    size_t n = 0;
+    CHECK_OK(vf.read(0, rb.data(), rb.size(), &n));
+    CHECK(n == in.size());
+    CHECK_SAME(rb, in, vf.block_size, calculate_shard_size(vf.block_size, 8));
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -660,6 +826,7 @@ int main(int argc, char** argv) {
         {"virtual_block_erasure_buffered", test_virtual_block_erasure_buffered},
         {"block_errors", test_block_errors},
         {"erasure_f32_hazard", test_erasure_f32_hazard},
+        {"erasure_f32_hazard_release", test_erasure_f32_hazard_release},
         {"virtual_file_1", test_virtual_file_1},
         {"virtual_file_2_4_mb", test_virtual_file_2_4_mb},
         {"virtual_file_errors", test_virtual_file_errors},
@@ -671,6 +838,8 @@ int main(int argc, char** argv) {
         {"virtual_file_batched_reconstruct", test_virtual_file_batched_reconstruct},
         {"rewrite_erasure", test_rewrite_erasure},
         {"virtual_file_mapped_per_block_flush", test_virtual_file_mapped_per_block_flush},
+        {"virtual_file_record_roundtrip", test_virtual_file_record_roundtrip},
+        {"rewrite_erasure_record_reload", test_rewrite_erasure_record_reload},
     };
     auto it = cases.find(name);
     if (it == cases.end()) {

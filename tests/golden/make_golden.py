@@ -126,6 +126,23 @@ def large_vectors():
     return out
 
 
+def f32_hazard_release():
+    """block.rs:421's u8 wrap in the reference's release build: a full
+    16,777,217 B Erasure(1,8,3) buffer (9 chunks of S = 2,097,152) encodes
+    into k+p shards with chunk 8 overwritten by parity row 0
+    (oracle sync_data_erasure, mode="release")."""
+    size, k, p = 16777217, 8, 3
+    buf = O.seeded_block(SEED, 9, size)
+    shards = O.sync_data_erasure(buf.tobytes(), size, k, p, mode="release")
+    loaded = O.load_block_erasure([s.tobytes() for s in shards], size, k, p)
+    return {"k": k, "p": p, "block_bytes": size, "buffer_len": size, "seed": [SEED, 9],
+            "shard_bytes": O.calculate_shard_size(size, k),
+            "generator": "numpy.random.default_rng([seed, idx]).integers(0, 256, block_bytes, uint8)",
+            "shard_sha256": [sha(s) for s in shards], "load_block_sha256": sha(loaded),
+            "lost_byte_offset": k * O.calculate_shard_size(size, k), "lost_byte": int(buf[-1]),
+            "loaded_last_byte": int(loaded[-1])}
+
+
 def glue_cases():
     """load_block quirks (src/vfs/block.rs:529-579)."""
     k, p, size = 4, 2, 4096
@@ -148,7 +165,7 @@ def glue_cases():
 
 def main():
     kat = {"published": published_kats(), "build_pins": build_pins(), "large": large_vectors(),
-           "load_block": glue_cases()}
+           "load_block": glue_cases(), "f32_hazard_release": f32_hazard_release()}
     with open(os.path.join(HERE, "kat.json"), "w") as f:
         json.dump(kat, f, indent=1)
     np.savez_compressed(os.path.join(HERE, "small_vectors.npz"), **small_vectors())

@@ -7,6 +7,8 @@ their shard files are compared here, byte for byte, with the CPU oracle's
 restatement of the Erasure arms (oracle.rs_oracle.sync_data_erasure /
 load_block_erasure, block.rs:404-440 / :529-579).
 """
+import hashlib
+import json
 import os
 import subprocess
 
@@ -14,6 +16,12 @@ import numpy as np
 import pytest
 
 from oracle import rs_oracle as O
+
+KAT = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "kat.json")))
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "shmr_amd", "_lib", "shmr_vfs_test")
@@ -58,6 +66,7 @@ CPU_CASES = [
     "virtual_file_2_4_mb",
     "virtual_file_errors",
     "virtual_file_chunk_model",
+    "virtual_file_record_roundtrip",
 ]
 
 
@@ -168,3 +177,50 @@ def test_virtual_file_mapped_per_block_flush(tmp_path, gpu):
         want = O.sync_data_erasure(data[b * MiB:(b + 1) * MiB].tobytes(), MiB, k, p)
         for i, f in enumerate(shards[b]):
             assert np.array_equal(read(f), want[i]), f"block {b} shard {i}"
+
+
+@pytest.mark.gpu
+def test_erasure_f32_hazard_release(tmp_path, gpu):
+    """VfsOptions::release_u8_wrap reproduces the reference's release build at
+    block.rs:421 (u8 wrap: 9 chunks of a 16,777,217 B Erasure(1,8,3) buffer,
+    chunk 8 overwritten by parity row 0 in the shard files) bit for bit, on
+    the per-block and the batched flush; the default refuses (CPU case
+    erasure_f32_hazard)."""
+    size, k, p = 16777217, 8, 3
+    case = KAT["f32_hazard_release"]
+    data = O.seeded_block(*case["seed"], size)
+    shards = run_case("erasure_f32_hazard_release", tmp_path, data)
+    want = O.sync_data_erasure(data.tobytes(), size, k, p, mode="release")
+    assert [sha(w) for w in want] == case["shard_sha256"]
+    assert sorted(shards) == [0, 1]
+    for blk in (0, 1):
+        assert len(shards[blk]) == k + p
+        for i, f in enumerate(shards[blk]):
+            assert np.array_equal(read(f), want[i]), f"block {blk} shard {i}"
+    loaded = read(os.path.join(str(tmp_path), "loaded_release.bin"))
+    assert sha(loaded) == case["load_block_sha256"]
+    assert np.array_equal(loaded, O.load_block_erasure([w.tobytes() for w in want], size, k, p))
+
+
+@pytest.mark.gpu
+def test_rewrite_erasure_record_reload(tmp_path, gpu):
+    """a file rewritten to Erasure(1,8,3) reloads from its
+    durable record (the reference's serde_yaml VirtualFile value) after
+    everything in memory is dropped, loses one shard per block, and reads back
+    bit-exact (checked in C++); the shard files equal the oracle's."""
+    data = O.seeded_block(O.BENCH_SEED, 700, 2 * MiB + 12345)
+    shards = run_case("rewrite_erasure_record_reload", tmp_path, data)
+    assert sorted(shards) == [0, 1, 2]
+    for b, files in sorted(shards.items()):
+        buf = np.zeros(MiB, np.uint8)   # each old Single block loads as a full 1 MiB buffer
+        part = data[b * MiB:(b + 1) * MiB]
+        buf[:len(part)] = part
+        want = O.sync_data_erasure(buf.tobytes(), MiB, 8, 3)
+        assert len(files) == 11
+        for i, f in enumerate(files):
+            if i == (3 * b) % 11:
+                assert not os.path.exists(f) or read(f).size == O.calculate_shard_size(MiB, 8)
+                continue
+            assert np.array_equal(read(f), want[i]), f"block {b} shard {i}"
+    rec = open(os.path.join(str(tmp_path), "vf17.yaml")).read()
+    assert rec.count("topology: !Erasure\n  - 1\n  - 8\n  - 3\n") == 3

@@ -268,8 +268,38 @@ def test_f32_hazard_documented():
     """src/vfs/mod.rs:16-18 uses f32: for sizes past 2^24 the shard size can be
     one short, so buffer.chunks(S) yields k + 1 chunks."""
     assert O.calculate_shard_size(16777217, 8) * 8 < 16777217
-    with pytest.raises(O.RSError):
-        O.sync_data_erasure(np.zeros(16777217, np.uint8).tobytes(), 16777217, 8, 3)
+    buf = np.zeros(16777217, np.uint8).tobytes()
+    with pytest.raises(O.RSError) as e:                     # the mirror's default
+        O.sync_data_erasure(buf, 16777217, 8, 3, mode="refuse")
+    assert e.value.name == "TooManyDataShards"
+    with pytest.raises(O.ReferencePanic):                   # debug build: overflow check
+        O.sync_data_erasure(buf, 16777217, 8, 3, mode="debug")
+    with pytest.raises(ValueError):
+        O.sync_data_erasure(buf, 16777217, 8, 3, mode="fast")
+
+
+def test_f32_hazard_release_semantics():
+    """block.rs:421 in the reference's release build (Cargo.toml:10-13, no
+    overflow checks): 9 chunks of S = 2,097,152 for a 16,777,217 B buffer at
+    Erasure(1,8,3); `3 + (8 - 9 as u8)` wraps to 2 zero shards, so encode sees
+    k+p = 11 shards and succeeds, overwriting chunk 8 (the buffer's last byte)
+    with parity row 0.  A later load_block returns that parity byte as the
+    block's last byte (concat of all k+p shards, [..size], block.rs:567-576)."""
+    size, k, p = 16777217, 8, 3
+    S = O.calculate_shard_size(size, k)
+    buf = O.seeded_block(O.BENCH_SEED, 9, size)
+    shards = O.sync_data_erasure(buf.tobytes(), size, k, p)           # release is the default
+    assert len(shards) == k + p and all(len(s) == S for s in shards)
+    for i in range(k):
+        assert np.array_equal(shards[i], buf[i * S:(i + 1) * S])
+    assert O.ReedSolomon(k, p).verify(shards)
+    case = KAT["f32_hazard_release"]
+    assert case["block_bytes"] == size and case["shard_bytes"] == S
+    assert [sha(s) for s in shards] == case["shard_sha256"]
+    loaded = O.load_block_erasure([s.tobytes() for s in shards], size, k, p)
+    assert len(loaded) == size and np.array_equal(loaded[:k * S], buf[:k * S])
+    assert loaded[k * S] == shards[k][0]                               # parity, not buf[k*S]
+    assert sha(loaded) == case["load_block_sha256"]
 
 
 def test_sync_data_partial_buffer_layout():

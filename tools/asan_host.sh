@@ -39,7 +39,7 @@ build)
     $HIPCC -O1 -g -std=c++17 $SAN -I"$ROOT/include" -o "$ROOT/tools/_bin/abi_check_asan" "$ROOT/tools/abi_check.cpp" \
         -L"$L" -lshmr_ec -Wl,-rpath,'$ORIGIN/asan_lib'
     $HIPCC -O1 -g -std=c++17 $SAN -Wall -I"$ROOT/include" -I"$ROOT/shmr_amd/host" -o "$BIN" \
-        "$ROOT/shmr_amd/host/vfs_test.cpp" "$ROOT/shmr_amd/host/vfs.cpp" \
+        "$ROOT/shmr_amd/host/vfs_test.cpp" "$ROOT/shmr_amd/host/vfs.cpp" "$ROOT/shmr_amd/host/record.cpp" \
         -L"$L" -lshmr_ec -Wl,-rpath,'$ORIGIN/asan_lib' -lpthread
     ;;
 run)
