@@ -197,7 +197,13 @@ int shmr_ec_device_free(int device, void* p);
 
 /* ---- configuration -------------------------------------------------------- */
 
-/* Device used by the host-buffer entry points (default 0). */
+/* Device used by the host-buffer entry points (default 0; negative ->
+ * SHMR_EC_INVALID_ARGUMENT).  Device IDs are checked at every compute call:
+ * an ID >= the number of GPUs returns SHMR_EC_INVALID_ARGUMENT
+ * (SHMR_EC_NO_DEVICE without a GPU); the *_blocks_host calls check every
+ * entry of their device list the same way, and a NULL list or ndev <= 0 is
+ * INVALID_ARGUMENT -- all before any buffer is touched.  A device listed
+ * twice gets two shares of the blocks. */
 int shmr_ec_set_device(shmr_ec_t* rs, int device);
 
 /* Tuning knobs (process-wide).
@@ -253,6 +259,25 @@ int shmr_ec_device_count(void);
 /* Blocks the host-buffer entry points served zero-copy (mapped memory) and
  * through device staging since the library was loaded.  Either may be NULL. */
 int shmr_ec_path_stats(uint64_t* zero_copy_blocks, uint64_t* staged_blocks);
+
+/* Per-device counters since the library was loaded, for the device ID the
+ * caller passed (blocks b -> devices[b % ndev] of the *_blocks_host calls, the
+ * context's device, or a *_batch_dev call's device): out[i] for i < n in the
+ * order below.  Every per-device object (plan images, upload rings, staging
+ * streams) is created per device ID, so N GPUs show N sets.  In the tools
+ * build, tuning key "alias_devices" = a adds IDs n .. n+a-1 that run on
+ * physical GPU (id mod n) with their own per-device state (a one-GPU
+ * rehearsal of multi-device bookkeeping); the product library has none. */
+enum {
+    SHMR_EC_DEV_BLOCKS_ENCODED = 0,
+    SHMR_EC_DEV_BLOCKS_RECONSTRUCTED = 1, /* blocks with at least one absent shard */
+    SHMR_EC_DEV_LAUNCHES = 2,             /* full-tile launch groups (<= 4 rows each) */
+    SHMR_EC_DEV_PLAN_IMAGES = 3,          /* coefficient plans uploaded to this device */
+    SHMR_EC_DEV_UPLOAD_RINGS = 4,         /* pinned upload rings created for this device */
+    SHMR_EC_DEV_STAGING_STREAMS = 5,      /* staging / pipeline streams created for this device */
+    SHMR_EC_DEV_COUNTERS = 6
+};
+int shmr_ec_device_stats(int device, uint64_t* out, size_t n);
 
 #ifdef __cplusplus
 }

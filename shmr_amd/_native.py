@@ -73,6 +73,7 @@ SIGNATURES = [
     ("shmr_ec_cache_stats", ctypes.c_int,
      [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     ("shmr_ec_device_count", ctypes.c_int, []),
+    ("shmr_ec_device_stats", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), _sz]),
 ]
 
 _libs = {}

@@ -192,6 +192,12 @@ int shmr_ec_cache_stats(const shmr_ec_t* rs, uint64_t* hits, uint64_t* misses) {
 
 int shmr_ec_device_count(void) { return core::device_count(); }
 
+int shmr_ec_device_stats(int device, uint64_t* out, size_t n) {
+    if (!out || device < 0) return SHMR_EC_INVALID_ARGUMENT;
+    core::device_stats(device, out, n);
+    return SHMR_EC_OK;
+}
+
 int shmr_ec_path_stats(uint64_t* zero_copy_blocks, uint64_t* staged_blocks) {
     core::path_stats(zero_copy_blocks, staged_blocks);
     return SHMR_EC_OK;
@@ -204,11 +210,13 @@ int shmr_ec_device_alloc(int device, size_t bytes, int contiguous, void** out) {
         *out = nullptr;
         int rc = core::check_device(device);
         if (rc) return rc;
-        int prev = 0;
-        if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) return SHMR_EC_DEVICE_ERROR;
-        const size_t n = bytes ? bytes : 1;
-        const hipError_t e = contiguous ? hipExtMallocWithFlags(out, n, hipDeviceMallocContiguous) : hipMalloc(out, n);
-        (void)hipSetDevice(prev);
+        hipError_t e;
+        {
+            core::DeviceScope scope(device);
+            if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
+            const size_t n = bytes ? bytes : 1;
+            e = contiguous ? hipExtMallocWithFlags(out, n, hipDeviceMallocContiguous) : hipMalloc(out, n);
+        }
         if (e != hipSuccess) {
             (void)hipGetLastError();
             *out = nullptr;
@@ -223,11 +231,9 @@ int shmr_ec_device_free(int device, void* p) {
         if (!p) return SHMR_EC_OK;
         int rc = core::check_device(device);
         if (rc) return rc;
-        int prev = 0;
-        if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) return SHMR_EC_DEVICE_ERROR;
-        const hipError_t e = hipFree(p);
-        (void)hipSetDevice(prev);
-        return e == hipSuccess ? SHMR_EC_OK : SHMR_EC_DEVICE_ERROR;
+        core::DeviceScope scope(device);
+        if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
+        return hipFree(p) == hipSuccess ? SHMR_EC_OK : SHMR_EC_DEVICE_ERROR;
     });
 }
 

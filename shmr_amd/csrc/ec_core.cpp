@@ -42,6 +42,7 @@ std::atomic<int> g_bounce_kib{kBounceKibDefault};
 std::atomic<int> g_mirror_zc{1};
 std::atomic<int> g_ptrs_direct{kPtrsDirectDefault};
 std::atomic<int> g_sync_spin{kSyncSpinDefault};
+std::atomic<int> g_alias_devices{0};   // tools build: alias device IDs (see ec_core.hpp)
 
 // Measured (tools/tune.py, interleaved A/B in one process): a register ring
 // of depth 2 (one shard of loads in flight per wave) beats depth 3 on every
@@ -127,6 +128,16 @@ int set_tuning(const char* key, int value) {
         g_sync_spin = value == kAuto ? kSyncSpinDefault : value;
         return SHMR_EC_OK;
     }
+    if (k == "alias_devices") {   // not per op class; tools build only (see ec_core.hpp)
+        const int v = value == kAuto ? 0 : value;
+#ifdef SHMR_EC_TOOLS
+        if (v < 0 || v > 32) return SHMR_EC_INVALID_ARGUMENT;
+        g_alias_devices = v;
+        return SHMR_EC_OK;
+#else
+        return v == 0 ? SHMR_EC_OK : SHMR_EC_INVALID_ARGUMENT;
+#endif
+    }
 #ifndef SHMR_EC_TOOLS
     // Product build: the kernel variant of every launch is the measured policy
     // (variant_policy), the same for every caller in the process.  Kernel knobs
@@ -197,6 +208,7 @@ int get_tuning(const char* key) {
     if (k == "mirror_zc") return g_mirror_zc;
     if (k == "ptrs_direct") return g_ptrs_direct;
     if (k == "sync_spin_us") return g_sync_spin;
+    if (k == "alias_devices") return g_alias_devices;
     if (k == "chunks") return T.u;
     if (k == "nt_load") return T.nt_load;
     if (k == "nt_store") return T.nt_store;
@@ -293,11 +305,35 @@ int device_count() {
     return n;
 }
 
-int check_device(int dev) {
+namespace {
+constexpr int kMaxDevIds = 64;
+std::atomic<uint64_t> g_dev_counters[kMaxDevIds][kDevCounters];
+}  // namespace
+
+int logical_device_count() {
     const int n = device_count();
+    return n > 0 ? n + g_alias_devices.load() : 0;
+}
+
+int physical_device(int dev) {
+    const int n = device_count();
+    return (n > 0 && dev >= n) ? dev % n : dev;
+}
+
+int check_device(int dev) {
+    const int n = logical_device_count();
     if (n <= 0) return SHMR_EC_NO_DEVICE;
-    if (dev < 0 || dev >= n) return SHMR_EC_INVALID_ARGUMENT;
+    if (dev < 0 || dev >= n || dev >= kMaxDevIds) return SHMR_EC_INVALID_ARGUMENT;
     return SHMR_EC_OK;
+}
+
+void count_device(int dev, DevCounter c, uint64_t n) {
+    if (dev >= 0 && dev < kMaxDevIds) g_dev_counters[dev][c].fetch_add(n, std::memory_order_relaxed);
+}
+
+void device_stats(int dev, uint64_t* out, size_t n) {
+    for (size_t i = 0; i < n && i < size_t(kDevCounters); ++i)
+        out[i] = (dev >= 0 && dev < kMaxDevIds) ? g_dev_counters[dev][i].load() : 0;
 }
 
 uint32_t plan_tab_off(unsigned k, unsigned m) {
@@ -319,6 +355,7 @@ int plan_on_device(Plan& plan, int dev, const uint8_t** out) {
         return SHMR_EC_DEVICE_ERROR;
     }
     plan.dev_image[dev] = d;
+    count_device(dev, kDevPlanImages);
     *out = static_cast<const uint8_t*>(d);
     return SHMR_EC_OK;
 }
@@ -351,6 +388,7 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
                                     aligned16(L.out_spitch);
     for (uint32_t row0 = 0; row0 < plan.m; row0 += kern::kMaxRowsPerLaunch) {
         const uint32_t rows = std::min<uint32_t>(kern::kMaxRowsPerLaunch, plan.m - row0);
+        count_device(dev, kDevLaunches);
         kern::Variant var = launch_variant(op, plan.k, rows, L.host_mapped, ptrs, bs.segs != nullptr);
         const uint64_t tb = kern::tile_bytes(var.u, var.threads);
         kern::ApplyArgs a{};
@@ -419,6 +457,7 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
 int encode_on_device(Codec& c, int dev, const Layout& L, uint64_t nblocks, uint64_t len, hipStream_t stream) {
     BlockSet bs;
     bs.n = nblocks;
+    count_device(dev, kDevBlocksEncoded, nblocks);
     return launch_set(*c.encode_plan(), dev, L, bs, len, stream, kEncode);
 }
 
@@ -454,6 +493,7 @@ int reconstruct_on_device(Codec& c, int dev, const Layout& L, const uint8_t* pre
         groups[key].push_back(b);
     }
     if (groups.empty()) return SHMR_EC_OK;
+    for (auto& g : groups) count_device(dev, kDevBlocksReconstructed, g.second.size());
     // Patterns with the same number of rebuilt shards share one multi-plan
     // launch set: the kernel picks each block's plan from a device table, so a
     // batch with many erasure patterns is still one launch (plus a tail).
@@ -603,6 +643,7 @@ UploadRing* UploadRing::for_device(int dev, int* rc, Kind kind) {
         ring->host_unified_ = hipHostGetDevicePointer(&hd, ring->host_, 0) == hipSuccess && hd == ring->host_;
         if (!ring->host_unified_) (void)hipGetLastError();
         r = ring;
+        count_device(dev, kDevUploadRings);
     }
     *rc = SHMR_EC_OK;
     return r;
@@ -679,6 +720,7 @@ Staging* StagingPool::acquire(int dev, size_t bytes, int* rc) {
             *rc = SHMR_EC_DEVICE_ERROR;
             return nullptr;
         }
+        count_device(dev, kDevStagingStreams);
     }
     if (s->cap < bytes) {
         if (s->dbuf) (void)hipFree(s->dbuf);

@@ -60,14 +60,35 @@ uint64_t ptrs_direct_max();
 hipError_t sync_stream(hipStream_t stream);
 
 // ---- devices --------------------------------------------------------------
-int device_count();
+// Device IDs.  Every per-device object (plan images, upload rings, staging
+// pools and pipes, the counters below) is keyed by the caller's device ID.
+// The tools build can add alias IDs (knob "alias_devices" = a): IDs n .. n+a-1
+// of an n-GPU process run on physical GPU (id mod n) but keep their own
+// per-device state -- a one-GPU rehearsal of the multi-device bookkeeping.
+int device_count();           // physical GPUs
+int logical_device_count();   // physical + alias IDs (0 without a GPU)
+int physical_device(int dev);
 int check_device(int dev);   // SHMR_EC_OK / NO_DEVICE / INVALID_ARGUMENT
+
+// Per-device counters (shmr_ec_device_stats; index order of the header's
+// SHMR_EC_DEV_* constants).
+enum DevCounter {
+    kDevBlocksEncoded = 0,
+    kDevBlocksReconstructed,
+    kDevLaunches,
+    kDevPlanImages,
+    kDevUploadRings,
+    kDevStagingStreams,
+    kDevCounters
+};
+void count_device(int dev, DevCounter c, uint64_t n = 1);
+void device_stats(int dev, uint64_t* out, size_t n);
 
 // Sets the calling thread's device for the scope, restoring the previous one.
 class DeviceScope {
 public:
     explicit DeviceScope(int dev) {
-        ok_ = hipGetDevice(&prev_) == hipSuccess && hipSetDevice(dev) == hipSuccess;
+        ok_ = hipGetDevice(&prev_) == hipSuccess && hipSetDevice(physical_device(dev)) == hipSuccess;
     }
     ~DeviceScope() {
         if (ok_) (void)hipSetDevice(prev_);

@@ -148,8 +148,10 @@ Codec::Codec(unsigned k, unsigned p) : k_(k), p_(p), matrix_(build_matrix(k, k +
 Codec::~Codec() {
     auto release = [](Plan& pl) {
         for (auto& kv : pl.dev_image) {
-            int prev = 0;
-            if (hipGetDevice(&prev) == hipSuccess && hipSetDevice(kv.first) == hipSuccess) {
+            // kv.first is the caller's device ID (an alias ID maps to a physical GPU)
+            int prev = 0, n = 0;
+            const int phys = (hipGetDeviceCount(&n) == hipSuccess && n > 0 && kv.first >= n) ? kv.first % n : kv.first;
+            if (hipGetDevice(&prev) == hipSuccess && hipSetDevice(phys) == hipSuccess) {
                 (void)hipFree(kv.second);
                 (void)hipSetDevice(prev);
             }

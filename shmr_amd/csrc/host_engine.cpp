@@ -131,11 +131,14 @@ constexpr int kStageSets = 3;
 struct DevicePipe {
     std::mutex mu;
     StageSet sets[kStageSets];
-    int ensure(size_t dbytes, size_t hbytes) {
+    int ensure(int dev, size_t dbytes, size_t hbytes) {
         for (auto& s : sets) {
-            if (!s.stream && (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
-                              hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess))
-                return SHMR_EC_DEVICE_ERROR;
+            if (!s.stream) {
+                if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
+                    hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess)
+                    return SHMR_EC_DEVICE_ERROR;
+                count_device(dev, kDevStagingStreams);
+            }
             if (s.dcap < dbytes) {
                 if (s.dbuf) (void)hipFree(s.dbuf);
                 s.dbuf = nullptr;
@@ -523,7 +526,7 @@ int run_host_job(const HostJob& job, const int* devices, int ndev) {
                 if (sets[i].stream) (void)hipStreamSynchronize(sets[i].stream);
         };
         {
-            const int rc = dp.ensure(C * block_bytes, pinned ? 0 : C * block_bytes);
+            const int rc = dp.ensure(dev, C * block_bytes, pinned ? 0 : C * block_bytes);
             if (rc) {
                 result = rc;
                 return;

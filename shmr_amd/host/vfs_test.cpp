@@ -127,6 +127,14 @@ void test_block_topology_try_from() {   // block.rs:647-659
     CHECK(BlockTopology::erasure(1, 8, 3).to_string() == "Erasure(1, 8, 3)");
     auto rt = BlockTopology::try_from(BlockTopology::erasure(1, 8, 3).to_string());
     CHECK(rt && rt->data == 8 && rt->parity == 3);
+    auto e104 = BlockTopology::try_from("Erasure(1,10,4)");
+    CHECK(e104 && e104->kind == BlockTopology::Erasure && e104->data == 10 && e104->parity == 4);
+    CHECK(BlockTopology::mirror(2).to_string() == "Mirror(2)" && BlockTopology::single().to_string() == "Single");
+    auto m3 = BlockTopology::try_from(BlockTopology::mirror(3).to_string());
+    CHECK(m3 && m3->kind == BlockTopology::Mirror && m3->n == 3);
+    // Display "Single" does not parse back (block.rs:57-59); missing or non-u8 fields fail
+    for (const char* bad : {"Single", "Erasure(1, 8)", "Erasure(x, 8, 3)", "Erasure(1, 8, 300)", "Mirror(a)"})
+        CHECK(!BlockTopology::try_from(bad));
 }
 
 void test_virtual_block_new_block() {   // block.rs:661-675

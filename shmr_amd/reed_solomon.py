@@ -221,10 +221,13 @@ class ReedSolomon:
         return dev, ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 
     def encode_batch_dev(self, data, parity, shard_len: Optional[int] = None,
-                         data_shard_pitch: Optional[int] = None, parity_shard_pitch: Optional[int] = None) -> None:
+                         data_shard_pitch: Optional[int] = None, parity_shard_pitch: Optional[int] = None,
+                         device: Optional[int] = None) -> None:
         """data: uint8 [B, k, pitch] (or [B, k*pitch]); parity: uint8 [B, p, pitch'].
 
-        Enqueued on torch's current stream of the tensors' device."""
+        Enqueued on torch's current stream of the tensors' device.  ``device``:
+        the device ID passed to the library (default: the tensors' device; the
+        tools build's alias IDs run on the same GPU, shmr_ec.h)."""
         B = data.shape[0]
         dbp = data.stride(0)
         pbp = parity.stride(0)
@@ -237,11 +240,12 @@ class ReedSolomon:
         self._check_batch_tensor(parity, self.parity_shard_count(), psp, L)
         self._check_addressable(data, parity)
         dev, stream = self._stream_and_device(data)
+        dev = dev if device is None else int(device)
         _check(self._L.shmr_ec_encode_batch_dev(self._h, ctypes.c_void_p(data.data_ptr()), dsp, dbp,
                                               ctypes.c_void_p(parity.data_ptr()), psp, pbp, B, L, dev, stream))
 
     def reconstruct_batch_dev(self, shards, present: np.ndarray, shard_len: Optional[int] = None,
-                              data_only: bool = False) -> None:
+                              data_only: bool = False, device: Optional[int] = None) -> None:
         """shards: uint8 [B, total, pitch] on the GPU; present: host bool/uint8 [B, total]."""
         if shards.dim() != 3:
             raise TypeError("shards must be a [blocks, total, bytes] tensor")
@@ -254,6 +258,7 @@ class ReedSolomon:
         pr = pr.reshape(B, t)
         self._check_addressable(shards)
         dev, stream = self._stream_and_device(shards)
+        dev = dev if device is None else int(device)
         _check(self._L.shmr_ec_reconstruct_batch_dev(self._h, ctypes.c_void_p(shards.data_ptr()), shards.stride(1),
                                                    shards.stride(0), _ptr(pr), B, L, int(data_only), dev, stream))
 
@@ -396,3 +401,16 @@ def path_stats():
     z, st = ctypes.c_uint64(), ctypes.c_uint64()
     _check(lib().shmr_ec_path_stats(ctypes.byref(z), ctypes.byref(st)))
     return int(z.value), int(st.value)
+
+
+DEVICE_COUNTERS = ("blocks_encoded", "blocks_reconstructed", "launches", "plan_images", "upload_rings",
+                   "staging_streams")
+
+
+def device_stats(device: int) -> dict:
+    """Per-device counters of the current library (include/shmr_ec.h
+    SHMR_EC_DEV_*): work done on that device ID and the per-device objects
+    (plan images, upload rings, staging streams) created for it."""
+    out = (ctypes.c_uint64 * len(DEVICE_COUNTERS))()
+    _check(lib().shmr_ec_device_stats(int(device), out, len(DEVICE_COUNTERS)))
+    return {name: int(out[i]) for i, name in enumerate(DEVICE_COUNTERS)}

@@ -364,3 +364,34 @@ def test_product_library_has_no_diagnostic_kernel():
     # every product full-tile kernel (MODE 0) is a depth-2 ring with nontemporal stores
     assert all(f & KDEPTH2 and f & 2 for f in product if f != 0)
     assert product < tools
+
+
+def test_device_list_and_stats_api():
+    """Device-list checks that precede any device use (CPU-only here): a NULL
+    list or ndev <= 0 is InvalidArgument; per-device counters read zero without
+    a GPU; alias device IDs exist only in the tools build."""
+    import ctypes
+    L = _native.lib()
+    h = ctypes.c_void_p()
+    assert L.shmr_ec_new(8, 3, ctypes.byref(h)) == 0
+    shard = np.zeros(4096, np.uint8)
+    ptrs = (_native._u8p * 11)(*[shard.ctypes.data_as(_native._u8p)] * 11)
+    devs = (ctypes.c_int * 1)(0)
+    pr = np.ones(11, np.uint8)
+    for d, n in ((None, 1), (devs, 0), (devs, -2)):
+        assert L.shmr_ec_encode_blocks_host(h, ptrs, 1, 4096, d, n) == -100
+        assert L.shmr_ec_reconstruct_blocks_host(h, ptrs, pr.ctypes.data_as(_native._u8p), 1, 4096, 0, d, n) == -100
+    assert L.shmr_ec_set_device(h, -1) == -100
+    L.shmr_ec_free(h)
+    out = (ctypes.c_uint64 * 6)(*([7] * 6))
+    assert L.shmr_ec_device_stats(-1, out, 6) == -100
+    assert L.shmr_ec_device_stats(0, None, 6) == -100
+    assert L.shmr_ec_device_stats(0, out, 6) == 0 and list(out) == [0] * 6
+    assert shmr_amd.device_stats(3) == {k: 0 for k in shmr_amd.reed_solomon.DEVICE_COUNTERS}
+    assert L.shmr_ec_set_tuning(b"alias_devices", 1) == -100
+    assert L.shmr_ec_set_tuning(b"alias_devices", 0) == 0
+    with _native.tools() as T:
+        assert T.shmr_ec_set_tuning(b"alias_devices", 3) == 0 and T.shmr_ec_get_tuning(b"alias_devices") == 3
+        assert T.shmr_ec_set_tuning(b"alias_devices", 33) == -100
+        assert T.shmr_ec_set_tuning(b"alias_devices", 0) == 0
+    assert L.shmr_ec_get_tuning(b"alias_devices") == 0
