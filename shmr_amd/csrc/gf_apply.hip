@@ -855,6 +855,15 @@ hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStr
     X(1, kNtLoad | kNtStore | kDepth2 | kSPre) \
     X(2, kNtLoad | kNtStore | kDepth2 | kSPre) \
     X(1, kNtLoad | kNtStore | kSPre) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSegs) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse) \
+    X(1, kNtLoad | kNtStore | kSegs) \
+    X(1, kNtLoad | kNtStore | kSegs | kFuse) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kTh512) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kTh128) \
+    X(2, kNtLoad | kNtStore | kFuse) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kTh128) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kFuse | kTh512) \
     X(1, kNtLoad | kNtStore | kGlds) \
     X(1, kNtLoad | kNtStore | kGlds | kDepth5) \
     X(1, kNtLoad | kNtStore | kGlds | kDepth9) \
