@@ -176,9 +176,10 @@ int shmr_ec_describe_variant(int decode, uint32_t data_shards, uint32_t rows, ch
                   v.u, int(v.nt_load), int(v.nt_store), int(v.scalar_tabs), int(v.occ8), v.threads,
                   core::grid_mode(op), int(v.diag), v.depth, v.wgs_per_cu, v.occ, int(v.early), int(v.spre), int(v.fuse_tail),
                   int(compiled));
-    if (v.glds) {   // appended only when set: records keyed by the string stay valid
+    // appended only when set: records keyed by the string stay valid
+    for (const auto& kv : {std::make_pair(v.glds, " glds=1"), std::make_pair(v.serial, " serial=1")}) {
         const size_t n = std::strlen(buf);
-        if (n + 1 < len) std::snprintf(buf + n, len - n, " glds=1");
+        if (kv.first && n + 1 < len) std::snprintf(buf + n, len - n, "%s", kv.second);
     }
     return SHMR_EC_OK;
 }

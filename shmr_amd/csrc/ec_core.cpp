@@ -36,6 +36,7 @@ struct Tuning {
     std::atomic<int> spre{kAuto};
     std::atomic<int> fuse_tail{kAuto};
     std::atomic<int> glds{kAuto};
+    std::atomic<int> serial{kAuto};
 };
 Tuning g_tune[2];   // [kEncode], [kDecode]
 std::atomic<int> g_bounce_kib{kBounceKibDefault};
@@ -149,7 +150,7 @@ int set_tuning(const char* key, int value) {
             {"chunks", kAuto}, {"nt_load", kAuto}, {"nt_store", kAuto}, {"scalar_tabs", 0}, {"occ8", 0},
             {"grid", -1},      {"diag", 0},        {"threads", 256},    {"depth", kAuto},   {"wgs_per_cu", 0},
             {"occ", kAuto},    {"early", kAuto},   {"spre", kAuto},     {"fuse_tail", kAuto},
-            {"glds", kAuto}};
+            {"glds", kAuto},   {"serial", kAuto}};
         const auto it = kDefaults.find(k);
         return (it != kDefaults.end() && it->second == value) ? SHMR_EC_OK : SHMR_EC_INVALID_ARGUMENT;
     }
@@ -192,6 +193,8 @@ int set_tuning(const char* key, int value) {
             T.fuse_tail = value == kAuto ? kAuto : (value != 0);
         } else if (k == "glds") {
             T.glds = value == kAuto ? kAuto : (value != 0);
+        } else if (k == "serial") {
+            T.serial = value == kAuto ? kAuto : (value != 0);
         } else {
             return SHMR_EC_INVALID_ARGUMENT;
         }
@@ -224,6 +227,7 @@ int get_tuning(const char* key) {
     if (k == "spre") return T.spre;
     if (k == "fuse_tail") return T.fuse_tail;
     if (k == "glds") return T.glds;
+    if (k == "serial") return T.serial;
     return SHMR_EC_INVALID_ARGUMENT;
 }
 
@@ -246,6 +250,7 @@ kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_m
     if (T.spre.load() != kAuto) v.spre = T.spre.load() != 0;
     if (T.fuse_tail.load() != kAuto) v.fuse_tail = T.fuse_tail.load() != 0;
     if (T.glds.load() != kAuto) v.glds = T.glds.load() != 0;
+    if (T.serial.load() != kAuto) v.serial = T.serial.load() != 0;
     if (v.glds) v.early = v.spre = v.scalar_tabs = false;   // the LDS-DMA ring is a form of the plain tile
     return v;
 }

@@ -61,6 +61,11 @@ constexpr int kSegs = 1 << 20;   // segment launches (ApplyArgs::segs)
 // in flight cost no VGPRs, so a wave can keep depth-1 shards of loads in flight
 // at the register budget of one (full tiles only; tails take the register ring).
 constexpr int kGlds = 1 << 21;
+// GF math one dword at a time: a scheduling fence after each of a lane's four
+// dwords keeps the scheduler from computing every perm of a 16-byte chunk
+// before the first XOR (48 live temporaries at R = 4), trading ILP inside a
+// wave for registers (more waves per SIMD).
+constexpr int kSerial = 1 << 22;
 
 template <int MODE, int F>
 constexpr bool has_ptrs() {
@@ -181,7 +186,7 @@ __device__ __forceinline__ void st(uint8_t* base, uint64_t col, uint64_t len, u3
 
 template <int R, int F>
 __device__ __forceinline__ void mac(uint32_t (&acc)[R][4], const u32x4& d, const Tab (&tb)[R]) {
-    const uint32_t w[4] = {d.x, d.y, d.z, d.w};
+    uint32_t w[4] = {d.x, d.y, d.z, d.w};
 #ifdef SHMR_EC_TOOLS
     if constexpr ((F & kDiagXor) != 0) {
 #pragma unroll
@@ -198,6 +203,15 @@ __device__ __forceinline__ void mac(uint32_t (&acc)[R][4], const u32x4& d, const
         const uint32_t s2 = (w[j] >> 6) & 0x03030303u;
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r][j] = gf_mac4(acc[r][j], tb[r], s0, s1, s2);
+        if constexpr ((F & kSerial) != 0) {
+            // An empty asm that "writes" this dword's sums and the next input
+            // dword: dword j+1's math can only start once dword j's is done.
+            if (j < 3) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) asm volatile("" : "+v"(acc[r][j]));
+                asm volatile("" : "+v"(w[j + 1]));
+            }
+        }
     }
 }
 
@@ -864,6 +878,16 @@ hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStr
     X(2, kNtLoad | kNtStore | kFuse) \
     X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kTh128) \
     X(1, kNtLoad | kNtStore | kDepth2 | kFuse | kTh512) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSerial) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSerial) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kFuse | kSerial) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kSerial) \
+    X(1, kNtLoad | kNtStore | kSerial) \
+    X(1, kNtLoad | kNtStore | kFuse | kSerial) \
+    X(1, kNtLoad | kNtStore | kDepth5 | kSerial) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kSerial) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kSerial) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial) \
     X(1, kNtLoad | kNtStore | kGlds) \
     X(1, kNtLoad | kNtStore | kGlds | kDepth5) \
     X(1, kNtLoad | kNtStore | kGlds | kDepth9) \
@@ -889,7 +913,7 @@ int variant_flags(const Variant& v) {
            (v.threads == 512 ? kTh512 : 0) | (v.depth == 5 ? kDepth5 : 0) | (v.depth == 9 ? kDepth9 : 0) |
            (v.depth == 2 ? kDepth2 : 0) | (v.depth == 1 ? kDepth1 : 0) | ((v.occ & 15) << kOccShift) |
            (v.early ? kEarly : 0) | (v.spre ? kSPre : 0) | (v.fuse_tail ? kFuse : 0) | (v.ptrs ? kPtrs : 0) |
-           (v.segs ? kSegs : 0) | (v.glds ? kGlds : 0);
+           (v.segs ? kSegs : 0) | (v.glds ? kGlds : 0) | (v.serial ? kSerial : 0);
 }
 
 template <int R>

@@ -92,6 +92,7 @@ struct Variant {
     bool ptrs = false;       // full-tile kernel that reads shard-pointer tables (set by launch_set)
     bool segs = false;       // full-tile kernel that takes segment launches (set by launch_set)
     bool glds = false;       // input ring in LDS filled by LDS-DMA (depth = slots; full tiles only)
+    bool serial = false;     // GF math one dword at a time (fewer live registers, more waves)
 };
 
 // rows in [1, kMaxRowsPerLaunch].  mode 0: full tiles, every shard base

@@ -131,7 +131,7 @@ def test_reconstruct_all_patterns_10_4(gpu):
 
 # --------------------------------------------------------------- device batch API
 KNOBS = ("chunks", "nt_load", "nt_store", "scalar_tabs", "occ8", "grid", "threads", "depth", "wgs_per_cu", "occ", "early", "spre",
-         "fuse_tail", "glds")
+         "fuse_tail", "glds", "serial")
 
 
 def _dev_encode_check(gpu, k, p, L, B, pitch=None, **knobs):
@@ -172,7 +172,7 @@ def test_encode_batch_dev(gpu, k, p, L, B):
 
 
 BASE = dict(chunks=1, nt_load=0, nt_store=0, scalar_tabs=0, occ8=0, grid=-1, threads=256, depth=3, wgs_per_cu=0, occ=0, early=0, spre=0,
-            fuse_tail=0, glds=0)
+            fuse_tail=0, glds=0, serial=0)
 VARIANTS = [dict(BASE, **v) for v in (
     {}, dict(nt_load=1), dict(nt_store=1), dict(nt_load=1, nt_store=1),
     dict(scalar_tabs=1, nt_load=1, nt_store=1), dict(occ8=1, nt_load=1, nt_store=1),
@@ -196,7 +196,12 @@ VARIANTS = [dict(BASE, **v) for v in (
     dict(nt_load=1, nt_store=1, glds=1, depth=9), dict(chunks=2, nt_load=1, nt_store=1, glds=1),
     dict(chunks=2, nt_load=1, nt_store=1, glds=1, depth=5), dict(nt_load=1, nt_store=1, glds=1, fuse_tail=1),
     dict(nt_load=1, nt_store=1, glds=1, depth=5, fuse_tail=1), dict(chunks=2, nt_load=1, nt_store=1, glds=1, fuse_tail=1),
-    dict(nt_load=1, nt_store=1, glds=1, depth=5, grid=0))]
+    dict(nt_load=1, nt_store=1, glds=1, depth=5, grid=0),
+    # GF math ordered one dword at a time (fewer live registers)
+    dict(nt_load=1, nt_store=1, depth=2, serial=1), dict(chunks=2, nt_load=1, nt_store=1, depth=2, serial=1),
+    dict(nt_load=1, nt_store=1, depth=2, fuse_tail=1, serial=1),
+    dict(chunks=2, nt_load=1, nt_store=1, depth=2, fuse_tail=1, serial=1), dict(nt_load=1, nt_store=1, serial=1),
+    dict(nt_load=1, nt_store=1, depth=2, early=1, serial=1), dict(nt_load=1, nt_store=1, depth=5, serial=1))]
 
 
 @pytest.mark.parametrize("knobs", VARIANTS, ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items() if BASE[k] != v) or "base")
