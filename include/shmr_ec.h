@@ -231,16 +231,18 @@ int shmr_ec_set_device(shmr_ec_t* rs, int device);
  * grid), "threads" (lanes per workgroup: 128, 256, 512), "depth" (register
  * ring depth = shards of loads in flight + 1: 1, 2, 3, 5, 9), "wgs_per_cu"
  * (0 = no cap, else the most workgroups resident per CU, enforced by LDS
- * padding), "occ" (0, 6, 7: register budget for that many waves per SIMD),
+ * padding; auto: 7 for single-row reconstructs, else no cap), "occ" (0, 6, 7: register budget for that many waves per SIMD),
  * "early" (0/1: issue the first data loads before the plan's LDS staging
  * completes), "spre" (0/1: coefficient tables and shard offsets by scalar
  * loads one shard ahead, no LDS), "fuse_tail" (0/1: a shard length that is
  * not a multiple of the tile runs the partial last tile of every block at the
- * head of the full-tile launch instead of in a second launch), "diag" (0/1:
- * XOR-only diagnostic kernel, WRONG results, for ceiling measurements).
+ * head of the full-tile launch instead of in a second launch), "glds" (0/1:
+ * input ring in LDS filled by global_load_lds_dwordx4, depth = ring slots),
+ * "serial" (0/1: GF math ordered one dword at a time, fewer VGPRs), "diag"
+ * (0/1: XOR-only diagnostic kernel, WRONG results, for ceiling measurements).
  * Prefix "encode." or "decode." to set one operation class only.
- * "chunks", "nt_load", "nt_store", "depth", "occ", "early", "spre" and
- * "fuse_tail" default to -2 (auto): the per-shape policy; any other value pins
+ * "chunks", "nt_load", "nt_store", "depth", "wgs_per_cu", "occ", "early",
+ * "spre", "fuse_tail", "glds" and "serial" default to -2 (auto): the per-shape policy; any other value pins
  * the knob, and setting -2 returns it to the policy. */
 int shmr_ec_set_tuning(const char* key, int value);
 int shmr_ec_get_tuning(const char* key);

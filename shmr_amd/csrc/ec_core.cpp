@@ -30,7 +30,7 @@ struct Tuning {
     std::atomic<int> diag{0};
     std::atomic<int> threads{256};
     std::atomic<int> depth{kAuto};
-    std::atomic<int> wgs_per_cu{0};
+    std::atomic<int> wgs_per_cu{kAuto};
     std::atomic<int> occ{kAuto};
     std::atomic<int> early{kAuto};
     std::atomic<int> spre{kAuto};
@@ -76,8 +76,14 @@ std::atomic<int> g_alias_devices{0};   // tools build: alias device IDs (see ec_
 // cross PCIe) are bound by the link, not HBM: there plain (temporal) loads
 // measured 72 GB/s of RS(8,3) encode traffic vs 64 with nontemporal loads
 // (tools/pcie_probe.py), and the shard-pointer tile has no early prologue.
+// Single-row reconstructs (one lost shard: RS(8,3) decode) fit 8 waves/SIMD
+// (39 VGPRs); capping residency at 7 workgroups per CU (LDS padding) measured
+// +1.4 to +1.7 points of HBM peak on two boxes (73.9-74.7 vs 72.6-73.0 %;
+// caps of 6, 5, 4 lose; profiles/r02/ab_occ*_decode83.txt).  Neutral for
+// RS(10,4) 2-row decodes and RS(8,3) encodes, so only there.
 kern::Variant variant_policy(OpClass op, unsigned k, unsigned rows, bool host_mapped) {
     kern::Variant v;
+    if (op == kDecode && rows == 1 && !host_mapped) v.wgs_per_cu = 7;
     v.u = (op == kEncode && rows >= 4) ? 2 : 1;
     v.nt_store = true;
     v.nt_load = !host_mapped;
@@ -148,7 +154,7 @@ int set_tuning(const char* key, int value) {
     {
         static const std::map<std::string, int> kDefaults = {
             {"chunks", kAuto}, {"nt_load", kAuto}, {"nt_store", kAuto}, {"scalar_tabs", 0}, {"occ8", 0},
-            {"grid", -1},      {"diag", 0},        {"threads", 256},    {"depth", kAuto},   {"wgs_per_cu", 0},
+            {"grid", -1},      {"diag", 0},        {"threads", 256},    {"depth", kAuto},   {"wgs_per_cu", kAuto},
             {"occ", kAuto},    {"early", kAuto},   {"spre", kAuto},     {"fuse_tail", kAuto},
             {"glds", kAuto},   {"serial", kAuto}};
         const auto it = kDefaults.find(k);
@@ -180,7 +186,7 @@ int set_tuning(const char* key, int value) {
             if (value != 1 && value != 2 && value != 3 && value != 5 && value != 9 && value != kAuto) return SHMR_EC_INVALID_ARGUMENT;
             T.depth = value;
         } else if (k == "wgs_per_cu") {
-            if (value < 0 || value > 32) return SHMR_EC_INVALID_ARGUMENT;
+            if ((value < 0 || value > 32) && value != kAuto) return SHMR_EC_INVALID_ARGUMENT;
             T.wgs_per_cu = value;
         } else if (k == "occ") {
             if (value != 0 && value != 6 && value != 7 && value != kAuto) return SHMR_EC_INVALID_ARGUMENT;
@@ -244,7 +250,7 @@ kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_m
 #endif
     v.threads = T.threads.load();
     if (T.depth.load() != kAuto) v.depth = T.depth.load();
-    v.wgs_per_cu = T.wgs_per_cu.load();
+    if (T.wgs_per_cu.load() != kAuto) v.wgs_per_cu = T.wgs_per_cu.load();
     if (T.occ.load() != kAuto) v.occ = T.occ.load();
     if (T.early.load() != kAuto) v.early = T.early.load() != 0;
     if (T.spre.load() != kAuto) v.spre = T.spre.load() != 0;
