@@ -224,9 +224,17 @@ public:
 private:
     static bool is_item(const std::string& t) { return t == "-" || t.rfind("- ", 0) == 0; }
 
+    // The record is 5 levels deep; anything far deeper is not a record (and
+    // must not exhaust the stack of the recursive descent).
+    static constexpr int kMaxDepth = 32;
+    int depth_ = 0;
+
     Node block(int indent) {
         if (pos_ >= lines_.size()) throw ParseError{"missing value"};
-        return is_item(lines_[pos_].text) ? seq(indent) : map(indent);
+        if (++depth_ > kMaxDepth) throw ParseError{"nesting deeper than " + std::to_string(kMaxDepth)};
+        Node n = is_item(lines_[pos_].text) ? seq(indent) : map(indent);
+        --depth_;
+        return n;
     }
 
     Node seq(int indent) {

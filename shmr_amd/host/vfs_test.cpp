@@ -763,6 +763,13 @@ void test_virtual_file_record_roundtrip() {
         Status st = VirtualFile::from_yaml(bad, &back, &err);
         CHECK(st && st->kind == ShmrError::FsError && st->code == EINVAL && !err.empty());
     }
+    {   // pathological nesting is refused, not recursed into
+        std::string deep = "ino: 1\nsize: 0\nchunk_size: 1\nblock_size: 1\nblocks:\n";
+        for (int d = 0; d < 5000; ++d) deep += std::string(size_t(d), ' ') + "-\n";
+        err.clear();
+        Status st = VirtualFile::from_yaml(deep, &back, &err);
+        CHECK(st && st->code == EINVAL && err.find("nesting") != std::string::npos);
+    }
     // save / load through the file system (temp file + rename)
     const fs::path rec = fs::path(g_bucket) / "vf21.yaml";
     CHECK_OK(vf.save_record(rec));
