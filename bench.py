@@ -73,6 +73,9 @@ def parse():
                     help="threads of the cpu_baseline leg (default: rayon's default pool size, "
                          "available_parallelism = sched affinity capped by the cgroup CPU quota; the "
                          "reference fans blocks out with rayon, mod.rs:93-96)")
+    ap.add_argument("--pitch-align", type=int, default=4096,
+                    help="device shard pitch = S rounded up to this many bytes (DESIGN.md section 4: 4 KiB "
+                         "measured +0.7-1.0 point of HBM peak over 256 B for RS(10,4)'s S = 1,677,722)")
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher rehearsal without a GPU: ranks join the process group, exchange their "
                          "identities and rank 0 prints one JSON line (tests/test_bench_launch.py)")
@@ -207,10 +210,12 @@ def run(args):
 
     # Synthetic blocks, generated on the GPU from a per-rank seed (inputs
     # resident in HBM before timing).  HBM layout: shard i of block b at
-    # (b*k + i) * pitch with pitch = S rounded up to 256 B -- for S = 524,288
+    # (b*k + i) * pitch with pitch = S rounded up to 4 KiB -- for S = 524,288
     # this IS the reference's block buffer (shards contiguous at i*S); for
-    # S = 1,677,722 (RS(10,4) 16 MiB) it is the 16-B aligned pitched layout.
-    pitch = (S + 255) // 256 * 256
+    # S = 1,677,722 (RS(10,4) 16 MiB) it is the page-aligned pitched layout
+    # (1,679,360 B per shard slot, 0.1 % padding).
+    a = max(16, args.pitch_align)
+    pitch = (S + a - 1) // a * a
     g = torch.Generator(device=dev)
     g.manual_seed(SEED + rank)
     bufs = []
@@ -332,6 +337,7 @@ def run(args):
                            f"({args.backend} only for the timing barrier / max-over-ranks)",
             "tuning": tuning,
             "memory": "physically contiguous VRAM (shmr_ec_device_alloc)" if args.contig else "torch caching allocator (hipMalloc)",
+            "shard_pitch_bytes": pitch,
         },
         "roofline": {
             "bound": "hbm",
