@@ -888,6 +888,11 @@ hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStr
     X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kSerial) \
     X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kSerial) \
     X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial) \
+    X(1, kDiagXor | kNtLoad | kNtStore | kDepth2) \
+    X(2, kDiagXor | kNtLoad | kNtStore | kDepth2) \
+    X(1, kDiagXor | kNtLoad | kNtStore | kDepth2 | kFuse) \
+    X(2, kDiagXor | kNtLoad | kNtStore | kDepth2 | kFuse) \
+    X(1, kDiagXor | kNtLoad | kNtStore | kDepth2 | kSegs) \
     X(1, kNtLoad | kNtStore | kGlds) \
     X(1, kNtLoad | kNtStore | kGlds | kDepth5) \
     X(1, kNtLoad | kNtStore | kGlds | kDepth9) \
