@@ -11,11 +11,12 @@ BIN="$ROOT/tools/_bin/vfs_test_asan"
 HIPCC=/opt/rocm/bin/hipcc
 CPU_CASES="block_topology_try_from virtual_block_new_block virtual_block_unbuffered_backing virtual_block_unbuffered
 virtual_block_buffered virtual_block_erasure_buffered block_errors virtual_file_1 virtual_file_2_4_mb virtual_file_errors
-virtual_file_chunk_model"
+virtual_file_chunk_model erasure_f32_hazard virtual_file_record_roundtrip"
 # GPU cases with the input sizes tests/test_host_cpp.py gives them
 GPU_CASES="erasure_block_sync_load:700001 erasure_block_missing_shards:1048576 virtual_file_erasure_batch:6291456
 replace_block_erasure:300000 virtual_file_batched_reconstruct:12582912 rewrite_erasure:2109497
-virtual_file_mapped_per_block_flush:10485760"
+virtual_file_mapped_per_block_flush:10485760 erasure_f32_hazard_release:16777217
+rewrite_erasure_record_reload:2109497"
 case "${1:-}" in
 build)
     # libshmr_ec.so's host code (C ABI, launch core, host engine) instrumented
