@@ -134,7 +134,8 @@ std::string strip_comment(const std::string& s) {
     for (size_t i = 0; i < s.size(); ++i) {
         const char c = s[i];
         if (q) {
-            if (c == q) q = 0;
+            if (q == '"' && c == '\\') ++i;   // escaped character inside "..."
+            else if (c == q) q = 0;
             continue;
         }
         if (c == '\'' || c == '"') q = c;
@@ -186,7 +187,8 @@ bool split_key(const std::string& t, std::string* key, std::string* rest) {
     for (size_t i = 0; i < t.size(); ++i) {
         const char c = t[i];
         if (q) {
-            if (c == q) q = 0;
+            if (q == '"' && c == '\\') ++i;   // escaped character inside "..."
+            else if (c == q) q = 0;
             continue;
         }
         if ((c == '\'' || c == '"') && i == 0) q = c;
@@ -321,10 +323,12 @@ private:
             cur.clear();
         };
         char q = 0;
-        for (char c : body) {
+        for (size_t i = 0; i < body.size(); ++i) {
+            const char c = body[i];
             if (q) {
                 cur += c;
-                if (c == q) q = 0;
+                if (q == '"' && c == '\\' && i + 1 < body.size()) cur += body[++i];   // escaped character
+                else if (c == q) q = 0;
             } else if (c == '\'' || c == '"') {
                 q = c;
                 cur += c;

@@ -780,6 +780,61 @@ void test_virtual_file_record_roundtrip() {
     CHECK(st && st->kind == ShmrError::FsError && st->code == ENOENT);
 }
 
+// Record fuzz: random files (every topology, random shard strings drawn from
+// printable ASCII, YAML indicators, quotes, '#', ': ' and control bytes)
+// round-trip exactly; random truncations and byte flips of valid records
+// either parse or fail with FsError(EINVAL) -- never crash or hang.
+void test_virtual_file_record_fuzz() {
+    std::mt19937_64 rng(0x5EC0DE);
+    auto rnd = [&](uint64_t n) { return uint64_t(rng() % n); };
+    const std::string alphabet =
+        "abcXYZ019_-.:/ #'\"!&*[]{},|>%@`?~\t\x01\x7f";
+    auto rstr = [&]() {
+        std::string t;
+        const size_t n = rnd(12);
+        for (size_t i = 0; i < n; ++i) t += alphabet[rnd(alphabet.size())];
+        if (rnd(8) == 0) t = "true";
+        if (rnd(8) == 0) t = "0x1F";
+        return t;
+    };
+    for (int it = 0; it < 400; ++it) {
+        VirtualFile vf = VirtualFile::new_with(rng(), rng() >> rnd(64));
+        vf.chunk_size = 1 + rnd(1 << 20);
+        vf.block_size = rng() >> rnd(64);
+        const size_t nb = rnd(5);
+        for (size_t b = 0; b < nb; ++b) {
+            VirtualBlock blk;
+            blk.ino = rng();
+            blk.idx = rnd(1000);
+            blk.size = rng() >> rnd(64);
+            const uint64_t kind = rnd(3);
+            size_t n = 1;
+            if (kind == 1) {
+                blk.topology = BlockTopology::mirror(uint8_t(rnd(256)));
+                n = blk.topology.n;
+            } else if (kind == 2) {
+                blk.topology = BlockTopology::erasure(uint8_t(rnd(256)), uint8_t(rnd(20)), uint8_t(rnd(20)));
+                n = size_t(blk.topology.data) + blk.topology.parity;
+            }
+            for (size_t i = 0; i < n; ++i) blk.shards.push_back({rstr(), rstr(), rstr()});
+            vf.blocks.push_back(blk);
+        }
+        const std::string text = vf.to_yaml();
+        VirtualFile back;
+        std::string err;
+        Status st = VirtualFile::from_yaml(text, &back, &err);
+        if (st) throw Failure{"round trip failed: " + err + "\n" + text};
+        if (back.to_yaml() != text) throw Failure{"round trip changed the record:\n" + text + "\n---\n" + back.to_yaml()};
+        for (int m = 0; m < 8; ++m) {   // mutations: parse or EINVAL, nothing else
+            std::string bad = text;
+            if (m % 2 == 0 && !bad.empty()) bad.resize(rnd(bad.size()));
+            else if (!bad.empty()) bad[rnd(bad.size())] = alphabet[rnd(alphabet.size())];
+            Status ms = VirtualFile::from_yaml(bad, &back, &err);
+            CHECK(!ms || (ms->kind == ShmrError::FsError && ms->code == EINVAL));
+        }
+    }
+}
+
 // a file rewritten to Erasure(1, 8, 3) survives a restart
 // through its record alone -- everything in memory is dropped, the record is
 // reloaded, one shard file of every block is lost, and the file reads back
@@ -854,6 +909,7 @@ int main(int argc, char** argv) {
         {"rewrite_erasure", test_rewrite_erasure},
         {"virtual_file_mapped_per_block_flush", test_virtual_file_mapped_per_block_flush},
         {"virtual_file_record_roundtrip", test_virtual_file_record_roundtrip},
+        {"virtual_file_record_fuzz", test_virtual_file_record_fuzz},
         {"rewrite_erasure_record_reload", test_rewrite_erasure_record_reload},
     };
     auto it = cases.find(name);

@@ -67,6 +67,7 @@ CPU_CASES = [
     "virtual_file_errors",
     "virtual_file_chunk_model",
     "virtual_file_record_roundtrip",
+    "virtual_file_record_fuzz",
 ]
 
 
