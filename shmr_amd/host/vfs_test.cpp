@@ -135,6 +135,21 @@ void test_block_topology_try_from() {   // block.rs:647-659
     // Display "Single" does not parse back (block.rs:57-59); missing or non-u8 fields fail
     for (const char* bad : {"Single", "Erasure(1, 8)", "Erasure(x, 8, 3)", "Erasure(1, 8, 300)", "Mirror(a)"})
         CHECK(!BlockTopology::try_from(bad));
+    // random strings from the parser's alphabet: no crash, and whatever
+    // parses (other than Single) re-parses from its Display form unchanged
+    std::mt19937_64 rng(77);
+    const std::string al = "SingleMirorEasu(), 0123456789 -+x";
+    for (int it = 0; it < 20000; ++it) {
+        std::string t;
+        const size_t n = rng() % 24;
+        for (size_t i = 0; i < n; ++i) t += al[rng() % al.size()];
+        if (rng() % 3 == 0) t = std::string(rng() % 2 ? "Erasure(" : "Mirror(") + t;
+        auto r = BlockTopology::try_from(t);
+        if (r && r->kind != BlockTopology::Single) {
+            auto again = BlockTopology::try_from(r->to_string());
+            CHECK(again && again->to_string() == r->to_string());
+        }
+    }
 }
 
 void test_virtual_block_new_block() {   // block.rs:661-675
