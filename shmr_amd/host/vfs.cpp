@@ -420,6 +420,42 @@ int read_slot(int fd, uint8_t* slot, size_t S, bool from_start, bool* odd) {
     return 0;
 }
 
+std::atomic<uint64_t> g_shard_reads{0};   // shard files read by loads (shard_reads_total)
+
+int read_slot_counted(int fd, uint8_t* slot, size_t S, bool from_start, bool* odd) {
+    g_shard_reads.fetch_add(1, std::memory_order_relaxed);
+    return read_slot(fd, slot, S, from_start, odd);
+}
+
+// VfsOptions::read_needed_shards: which shard files of an Erasure block a
+// load reads (plan[i]: kRead, kPresentUnread, or kAbsent).  The file sizes
+// decide: a shard whose file is exactly S bytes is intact; the first k intact
+// shards in index order -- exactly the reconstruct's inputs (first k present,
+// the crate's rule) -- are read, the other intact ones count as present
+// without being read.  Their slots are never observable: a load returns
+// [..size] with size <= k*S (checked by the caller), and every flush
+// re-encodes parity from the data.  A missing file is absent; a file of
+// another length is absent under short_shard_is_erasure, and otherwise the
+// reference's zero-pad-and-keep rule needs its bytes, so everything is read
+// (returns false).  If a planned read fails, the caller reads the rest.
+enum ReadPlan : uint8_t { kAbsent = 0, kRead = 1, kPresentUnread = 2 };
+bool plan_needed_reads(const int* fds, size_t n, size_t k, size_t S, bool short_is_erasure, uint8_t* plan) {
+    size_t inputs = 0;
+    for (size_t i = 0; i < n; ++i) {
+        plan[i] = kAbsent;
+        if (fds[i] < 0) continue;
+        struct stat st {};
+        if (::fstat(fds[i], &st) != 0) return false;
+        if (uint64_t(st.st_size) != S) {
+            if (!short_is_erasure) return false;
+            continue;
+        }
+        plan[i] = inputs < k ? kRead : kPresentUnread;
+        inputs += plan[i] == kRead;
+    }
+    return true;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -686,15 +722,34 @@ Status VirtualBlock::load_block(bool* reconstructed, int device) const {
         if (buffer.size() < size) buffer.set_len_uninit(size);   // every slot byte is overwritten below
         std::vector<uint8_t*> ptrs(n);
         shard_ptrs(buffer, n, S, ptrs.data());
-        std::vector<uint8_t> present(n, 0), odd(n, 0);
-        parallel_for(n, 16, [&](size_t i) {
-            const int fd = st_->handles[i].second;
+        std::vector<uint8_t> present(n, 0), odd(n, 0), plan(n, kRead);
+        std::vector<int> fds(n);
+        for (size_t i = 0; i < n; ++i) fds[i] = st_->handles[i].second;
+        const bool planned = opt_.read_needed_shards && opt_.pread_from_start && size <= size_t(topology.data) * S &&
+                             plan_needed_reads(fds.data(), n, topology.data, S, opt_.short_shard_is_erasure, plan.data());
+        if (!planned) std::fill(plan.begin(), plan.end(), uint8_t(kRead));
+        auto read_one = [&](size_t i) {
             bool o = false;
-            if (fd >= 0 && read_slot(fd, ptrs[i], S, opt_.pread_from_start, &o) == 0) {   // Err -> None
+            if (fds[i] >= 0 && read_slot_counted(fds[i], ptrs[i], S, opt_.pread_from_start, &o) == 0) {   // Err -> None
                 present[i] = !(o && opt_.short_shard_is_erasure);
                 odd[i] = o;
             }
+        };
+        parallel_for(n, 16, [&](size_t i) {
+            if (plan[i] == kRead) read_one(i);
+            else if (plan[i] == kPresentUnread) present[i] = 1;
         });
+        if (planned) {   // a planned read failed or changed length: read the rest as well
+            bool redo = false;
+            for (size_t i = 0; i < n; ++i) redo |= plan[i] == kRead && (!present[i] || odd[i]);
+            if (redo)
+                parallel_for(n, 16, [&](size_t i) {
+                    if (plan[i] == kPresentUnread) {
+                        present[i] = 0;
+                        read_one(i);
+                    }
+                });
+        }
         bool missing = false;
         for (size_t i = 0; i < n; ++i) missing |= !present[i] || odd[i];
         if (missing) {
@@ -1200,6 +1255,7 @@ Status VirtualFile::load_blocks(const std::vector<size_t>& block_indices,
         size_t blk, shard, S;
         uint8_t* slot;
         int fd;
+        uint8_t plan;
     };
     std::vector<Task> tasks;
     std::map<size_t, size_t> first_task;   // block -> index of its shard 0 task
@@ -1214,7 +1270,16 @@ Status VirtualFile::load_blocks(const std::vector<size_t>& block_indices,
             if (st.buffer.size() < blocks[i].size) st.buffer.set_len_uninit(blocks[i].size);   // slots overwritten
             first_task[i] = tasks.size();
             for (size_t s = 0; s < n; ++s)
-                tasks.push_back({i, s, g.S, st.buffer.data() + s * g.S, s < st.handles.size() ? st.handles[s].second : -1});
+                tasks.push_back({i, s, g.S, st.buffer.data() + s * g.S, s < st.handles.size() ? st.handles[s].second : -1,
+                                 uint8_t(kRead)});
+            const VfsOptions& o = blocks[i].opt_;
+            if (o.read_needed_shards && o.pread_from_start && blocks[i].size <= size_t(g.k) * g.S) {
+                std::vector<int> fds(n);
+                std::vector<uint8_t> plan(n);
+                for (size_t s = 0; s < n; ++s) fds[s] = tasks[first_task[i] + s].fd;
+                if (plan_needed_reads(fds.data(), n, g.k, g.S, o.short_shard_is_erasure, plan.data()))
+                    for (size_t s = 0; s < n; ++s) tasks[first_task[i] + s].plan = plan[s];
+            }
         }
     }
     last_load.prepare_s = now_s() - t0;
@@ -1237,16 +1302,35 @@ Status VirtualFile::load_blocks(const std::vector<size_t>& block_indices,
         const size_t n = size_t(bt.g->k) + bt.g->p;
         const size_t t0b = first_task[bt.g->members[bt.b]];
         const size_t nt = (bt.e - bt.b) * n;   // a batch's tasks are contiguous
-        parallel_for(nt, 32, [&](size_t q) {
-            const size_t t = t0b + q;
+        auto read_task = [&](size_t t) {
             const Task& tk = tasks[t];
             const VfsOptions& o = blocks[tk.blk].opt_;
             bool od = false;
-            if (tk.fd >= 0 && read_slot(tk.fd, tk.slot, tk.S, o.pread_from_start, &od) == 0) {
+            if (tk.fd >= 0 && read_slot_counted(tk.fd, tk.slot, tk.S, o.pread_from_start, &od) == 0) {
                 present[t] = !(od && o.short_shard_is_erasure);
                 odd[t] = od;
             }
+        };
+        parallel_for(nt, 32, [&](size_t q) {
+            const size_t t = t0b + q;
+            if (tasks[t].plan == kRead) read_task(t);
+            else if (tasks[t].plan == kPresentUnread) present[t] = 1;
         });
+        // read_needed_shards: a block whose planned read failed reads the rest too
+        std::vector<size_t> redo;
+        for (size_t q = 0; q < nt; ++q) {
+            const size_t t = t0b + q;
+            if (tasks[t].plan == kRead && (!present[t] || odd[t]))
+                for (size_t s = 0; s < n; ++s) {
+                    const size_t u = first_task[tasks[t].blk] + s;
+                    if (tasks[u].plan == kPresentUnread) {
+                        tasks[u].plan = kRead;
+                        present[u] = 0;
+                        redo.push_back(u);
+                    }
+                }
+        }
+        parallel_for(redo.size(), 32, [&](size_t q) { read_task(redo[q]); });
     };
     auto reconstruct_batch = [&](const Batch& bt) {
         const Group& g = *bt.g;
@@ -1377,5 +1461,7 @@ Status VirtualFile::rewrite_erasure(uint8_t data, uint8_t parity) {
 }
 
 size_t block_cache_trim() { return BufferPool::get().trim(); }
+
+uint64_t shard_reads_total() { return g_shard_reads.load(); }
 
 }  // namespace shmr

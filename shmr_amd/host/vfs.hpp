@@ -111,6 +111,14 @@ struct VfsOptions {
     // load_block: a shard whose length is not S is an erasure (the reference
     // zero-pads it and keeps it present, block.rs:548-551).
     bool short_shard_is_erasure = false;
+    // load_block with pread_from_start: read only the shard files a load
+    // needs -- the first k files of exactly S bytes (the reconstruct's
+    // inputs, the crate's first-k-present rule); other intact shards count as
+    // present unread.  Reads 8 of 11 RS(8,3) shards instead of 10-11; the
+    // loaded data is byte-identical (the unread parity slots are never
+    // returned, and every flush re-encodes parity).  Falls back to reading
+    // everything where the reference's short-shard rule needs the bytes.
+    bool read_needed_shards = false;
     // Block Cache buffers in mapped host memory (shmr_ec_host_alloc: the codec
     // runs zero-copy on them); falls back to pageable memory when no device is
     // present.
@@ -187,6 +195,9 @@ private:
 // by capacity, up to 16 GiB, because pinning memory costs more than filling
 // it).  Returns the bytes freed.
 size_t block_cache_trim();
+
+// Shard files read by Erasure-block loads since the library was loaded.
+uint64_t shard_reads_total();
 
 // VirtualFile (src/vfs/mod.rs:35-272)
 class VirtualFile {

@@ -38,6 +38,7 @@ double now_s() {
 
 struct Result {
     double write_s = 0, sync_s = 0, read_s = 0, per_block_sync_s = 0;
+    double shard_reads_per_block = 0;
     IoStats sync, load;
 };
 
@@ -84,9 +85,11 @@ Result run_once(const std::shared_ptr<const ShmrFsConfig>& cfg, uint64_t ino, co
         fs::remove(p);
     }
     std::vector<uint8_t> back(src.size());
+    const uint64_t reads0 = shard_reads_total();
     t = now_s();
     DIE_IF(vf.read(0, back.data(), back.size(), &n));   // batched shard reads + reconstruct
     r.read_s = now_s() - t;
+    r.shard_reads_per_block = double(shard_reads_total() - reads0) / double(nblk);
     r.load = vf.last_load;
     if (n != src.size() || back != src) {
         std::fprintf(stderr, "verification FAILED\n");
@@ -134,9 +137,12 @@ int main(int argc, char** argv) {
     // batch sizes: auto policy, one batch, and explicit pipeline batches (MiB)
     std::vector<size_t> batch_mib = {VirtualFile::kAutoBatch, 0};
     for (int i = 6; i < argc; ++i) batch_mib.push_back(std::strtoull(argv[i], nullptr, 10));
+    // read_needed_shards (8 of 11 shard reads per load) for the auto batch
     for (int pinned = 1; pinned >= 0; --pinned)
-    for (size_t bm : batch_mib) {
+    for (size_t bm : batch_mib)
+    for (int needed = 0; needed <= (bm == VirtualFile::kAutoBatch ? 1 : 0); ++needed) {
         VfsOptions o;
+        o.read_needed_shards = needed != 0;
         o.missing_shard_is_erasure = true;
         o.pread_from_start = true;
         o.short_shard_is_erasure = true;
@@ -156,6 +162,7 @@ int main(int argc, char** argv) {
             if (r.read_s < best.read_s) {
                 best.read_s = r.read_s;
                 best.load = r.load;
+                best.shard_reads_per_block = r.shard_reads_per_block;
             }
             best.write_s = std::min(best.write_s, r.write_s);
             best.per_block_sync_s = std::min(best.per_block_sync_s, r.per_block_sync_s);
@@ -177,14 +184,15 @@ int main(int argc, char** argv) {
             "\"write_GiBps\": %s, \"sync_GiBps\": %s, \"sync_encode_GiBps\": %s, \"sync_shard_io_GiBps\": %s, "
             "\"sync_pipeline_GiBps\": %s, \"per_block_sync_GiBps\": %s, \"read_with_erasure_GiBps\": %s, "
             "\"read_reconstruct_GiBps\": %s, \"read_shard_io_GiBps\": %s, \"read_pipeline_GiBps\": %s, "
-            "\"reconstructed_blocks\": %zu, \"sync_prepare_ms\": %.2f, \"read_prepare_ms\": %.2f, \"verified\": true}\n",
+            "\"reconstructed_blocks\": %zu, \"sync_prepare_ms\": %.2f, \"read_prepare_ms\": %.2f, "
+            "\"read_needed_shards\": %s, \"shard_reads_per_block\": %.2f, \"verified\": true}\n",
             pinned ? "mapped Block Cache (shmr_ec_host_alloc)" : "pageable", (unsigned long long)(zc1 - zc0),
             (unsigned long long)(st1 - st0), batch_name.c_str(), (unsigned long long)file_mib,
             (unsigned long long)block_mib, int(do_fsync), reps, rate(best.write_s).c_str(), rate(best.sync_s).c_str(),
             rate(best.sync.codec_s).c_str(), rate(best.sync.io_s).c_str(), rate(best.sync.total_s).c_str(),
             rate(best.per_block_sync_s).c_str(), rate(best.read_s).c_str(), rate(best.load.codec_s).c_str(),
             rate(best.load.io_s).c_str(), rate(best.load.total_s).c_str(), best.load.blocks, best.sync.prepare_s * 1e3,
-            best.load.prepare_s * 1e3);
+            best.load.prepare_s * 1e3, needed ? "true" : "false", best.shard_reads_per_block);
         std::fflush(stdout);
     }
     return 0;

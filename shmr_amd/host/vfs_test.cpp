@@ -892,6 +892,93 @@ void test_rewrite_erasure_record_reload() {
     CHECK_SAME(rb, in, vf.block_size, calculate_shard_size(vf.block_size, 8));
 }
 
+// VfsOptions::read_needed_shards: a load reads only the first k intact shard
+// files (per-block and batched paths) and returns the same bytes as the
+// read-everything load; a shard of another length without
+// short_shard_is_erasure falls back to reading all of them (reference rule).
+void test_read_needed_shards() {
+    auto cfg = test_config();
+    auto in = read_input();
+    const uint64_t bs = 1024 * 1024;
+    const size_t nblk = in.size() / bs;
+    CHECK(nblk * bs == in.size() && nblk >= 2);
+    VirtualFile vf = VirtualFile::new_with(18, 0);
+    vf.populate(cfg);
+    for (size_t i = 0; i < nblk; ++i) {
+        VirtualBlock b;
+        CHECK_OK(VirtualBlock::create(18, i + 1, cfg, bs, BlockTopology::erasure(1, 8, 3), &b));
+        vf.blocks.push_back(b);
+    }
+    size_t n = 0;
+    CHECK_OK(vf.write(0, in.data(), in.size(), &n));
+    CHECK_OK(vf.sync_data(true));
+    CHECK_OK(vf.drop_buffers());
+    CHECK_OK(vf.drop_handles());
+    VfsOptions o;
+    o.missing_shard_is_erasure = true;
+    o.pread_from_start = true;
+    o.read_needed_shards = true;
+    vf.set_options(o);
+    const size_t S = calculate_shard_size(bs, 8);
+    std::vector<uint8_t> rb(in.size());
+    auto load_all = [&](size_t* reads) {
+        const uint64_t r0 = shard_reads_total();
+        std::fill(rb.begin(), rb.end(), 0xEE);
+        CHECK_OK(vf.read(0, rb.data(), rb.size(), &n));
+        CHECK(n == in.size());
+        *reads = size_t(shard_reads_total() - r0);
+        CHECK_OK(vf.drop_buffers());
+    };
+    size_t reads = 0;
+    load_all(&reads);   // batched path, all intact
+    CHECK_SAME(rb, in, bs, S);
+    CHECK(reads == 8 * nblk);
+    // lose data shard (i % 8) and parity shard 9 of every block: still 8 reads each
+    CHECK_OK(vf.drop_handles());
+    for (size_t i = 0; i < nblk; ++i) {
+        fs::remove(shard_file(*cfg, vf.blocks[i], i % 8));
+        fs::remove(shard_file(*cfg, vf.blocks[i], 9));
+    }
+    load_all(&reads);   // the flush in drop_buffers repairs the files
+    CHECK_SAME(rb, in, bs, S);
+    CHECK(reads == 8 * nblk);
+    CHECK(fsize(shard_file(*cfg, vf.blocks[0], 0)) == S && fsize(shard_file(*cfg, vf.blocks[0], 9)) == S);
+    // per-block path (VirtualBlock::read)
+    CHECK_OK(vf.drop_handles());
+    VirtualBlock& b = vf.blocks[1];
+    fs::remove(shard_file(*cfg, b, 3));
+    std::vector<uint8_t> one(bs);
+    uint64_t r0 = shard_reads_total();
+    CHECK_OK(b.read(0, one.data(), one.size(), &n));
+    CHECK(shard_reads_total() - r0 == 8);
+    CHECK(std::equal(one.begin(), one.end(), in.begin() + bs));
+    CHECK_OK(b.drop_buffer());
+    CHECK_OK(b.drop_handles());
+    // a truncated data shard (reference rule: zero-padded and kept): every file
+    // is read, and the load equals the read-everything load.  Fresh views of
+    // the block, so no flush repairs the file between the two loads.
+    fs::resize_file(shard_file(*cfg, b, 2), 100);
+    auto view = [&](bool needed) {
+        VirtualBlock v;
+        v.ino = b.ino;
+        v.idx = b.idx;
+        v.size = b.size;
+        v.topology = b.topology;
+        v.shards = b.shards;
+        v.populate(cfg);
+        VfsOptions vo = o;
+        vo.read_needed_shards = needed;
+        v.set_options(vo);
+        const uint64_t r = shard_reads_total();
+        CHECK_OK(v.read(0, one.data(), one.size(), &n));
+        CHECK(shard_reads_total() - r == 11);
+        return v.buffer_snapshot();
+    };
+    const auto planned = view(true);
+    CHECK(fsize(shard_file(*cfg, b, 2)) == 100);
+    CHECK(planned == view(false));
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -926,6 +1013,7 @@ int main(int argc, char** argv) {
         {"virtual_file_record_roundtrip", test_virtual_file_record_roundtrip},
         {"virtual_file_record_fuzz", test_virtual_file_record_fuzz},
         {"rewrite_erasure_record_reload", test_rewrite_erasure_record_reload},
+        {"read_needed_shards", test_read_needed_shards},
     };
     auto it = cases.find(name);
     if (it == cases.end()) {

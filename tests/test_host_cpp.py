@@ -204,6 +204,16 @@ def test_erasure_f32_hazard_release(tmp_path, gpu):
 
 
 @pytest.mark.gpu
+def test_read_needed_shards(tmp_path, gpu):
+    """VfsOptions::read_needed_shards: intact and degraded loads read 8 of 11
+    RS(8,3) shard files per block (batched and per-block paths) and return the
+    written bytes; a truncated shard under the reference's zero-pad rule reads
+    all 11 and loads the same buffer as the read-everything path (checked in
+    C++)."""
+    data = O.seeded_block(O.BENCH_SEED, 701, 4 * MiB)
+    run_case("read_needed_shards", tmp_path, data)
+
+
 def test_rewrite_erasure_record_reload(tmp_path, gpu):
     """a file rewritten to Erasure(1,8,3) reloads from its
     durable record (the reference's serde_yaml VirtualFile value) after
