@@ -88,7 +88,12 @@ kern::Variant variant_policy(OpClass op, unsigned k, unsigned rows, bool host_ma
     v.nt_store = true;
     v.nt_load = !host_mapped;
     v.depth = 2;
-    v.early = op == kEncode && k < 8 && !host_mapped;
+    // early prologue for small k; for 4-row encodes (RS(10,4)) early plus the
+    // per-dword math order (fewer live VGPRs at U = 2): +0.5 - 1.0 point in
+    // three interleaved A/Bs (profiles/r02/tune_encode104_early_serial*.txt);
+    // serial loses on RS(8,3) encode (profiles/r02/tune_encode83_early_serial.txt)
+    v.early = op == kEncode && (k < 8 || rows >= 4) && !host_mapped;
+    v.serial = op == kEncode && rows >= 4 && !host_mapped;
     v.fuse_tail = true;   // only where len % tile != 0 (RS(10,4): -5.5 % encode, -5.8 % decode time)
     return v;
 }
@@ -287,6 +292,7 @@ kern::Variant launch_variant(OpClass op, unsigned k, unsigned rows, bool host_ma
     v.segs = segs;
     if (ptrs) {
         v.early = v.spre = v.scalar_tabs = v.glds = false;   // only the plain LDS-staged tile reads pointer tables
+        if (g_tune[op].serial.load() == kAuto) v.serial = false;   // the policy's serial goes with early
         kern::Variant lean = v;
         lean.fuse_tail = false;
         if (!kern::variant_compiled(lean)) {   // tuned knobs without a pointer-table build: the mapped policy

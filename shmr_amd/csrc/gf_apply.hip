@@ -822,6 +822,8 @@ hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStr
     X(2, kNtLoad | kNtStore | kDepth2 | kFuse) \
     X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse) \
     X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial) \
     X(1, kNtLoad | kNtStore | kDepth2 | kSegs) \
     X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse) \
     X(1, kNtStore | kDepth2 | kPtrs) \
@@ -888,6 +890,7 @@ hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStr
     X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kSerial) \
     X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kSerial) \
     X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial) \
     X(1, kDiagXor | kNtLoad | kNtStore | kDepth2) \
     X(2, kDiagXor | kNtLoad | kNtStore | kDepth2) \
     X(1, kDiagXor | kNtLoad | kNtStore | kDepth2 | kFuse) \

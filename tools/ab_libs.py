@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--config", default="encode83")
     ap.add_argument("--rounds", type=int, default=9)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--pitch-align", type=int, default=256, help="shard pitch alignment (bench.py uses 4096)")
     a = ap.parse_args()
     k, p, block, er, B = CFG[a.config]
     libs = {"current": load(_native.LIB_PATH)}
@@ -50,7 +51,7 @@ def main():
         libs[os.path.basename(o)] = load(os.path.abspath(o))
     dev = torch.device("cuda", 0)
     S = int(libs["current"].shmr_ec_shard_size(block, k))
-    pitch = (S + 255) // 256 * 256
+    pitch = (S + a.pitch_align - 1) // a.pitch_align * a.pitch_align
     st = torch.cuda.current_stream()
     sp = ctypes.c_void_p(st.cuda_stream)
     g = torch.Generator(device=dev)
