@@ -233,12 +233,14 @@ int shmr_ec_set_device(shmr_ec_t* rs, int device);
  * (0 = no cap, else the most workgroups resident per CU, enforced by LDS
  * padding; auto: 7 for single-row reconstructs, else no cap), "occ" (0, 6, 7: register budget for that many waves per SIMD),
  * "early" (0/1: issue the first data loads before the plan's LDS staging
- * completes), "spre" (0/1: coefficient tables and shard offsets by scalar
+ * completes; auto: encodes with fewer than 8 data shards or 4 output rows),
+ * "spre" (0/1: coefficient tables and shard offsets by scalar
  * loads one shard ahead, no LDS), "fuse_tail" (0/1: a shard length that is
  * not a multiple of the tile runs the partial last tile of every block at the
  * head of the full-tile launch instead of in a second launch), "glds" (0/1:
  * input ring in LDS filled by global_load_lds_dwordx4, depth = ring slots),
- * "serial" (0/1: GF math ordered one dword at a time, fewer VGPRs), "diag"
+ * "serial" (0/1: GF math ordered one dword at a time, fewer VGPRs; auto:
+ * encodes of 4 output rows), "diag"
  * (0/1: XOR-only diagnostic kernel, WRONG results, for ceiling measurements).
  * Prefix "encode." or "decode." to set one operation class only.
  * "chunks", "nt_load", "nt_store", "depth", "wgs_per_cu", "occ", "early",
