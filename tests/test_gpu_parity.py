@@ -166,7 +166,10 @@ def _dev_encode_check_in(gpu, k, p, L, B, pitch, knobs):
 
 
 @pytest.mark.parametrize("k,p,L,B", [(8, 3, 524288, 16), (4, 2, 262144, 8), (10, 4, 1677722, 3),
-                                     (6, 3, 8192 * 3 + 16, 5), (3, 5, 16, 7)])
+                                     (6, 3, 8192 * 3 + 16, 5), (3, 5, 16, 7),
+                                     # 4-row encodes (early + serial policy): tile-multiple length,
+                                     # and 6 rows = a 4-row and a 2-row launch with partial tiles
+                                     (10, 4, 8192 * 40, 3), (5, 6, 8192 * 5 + 7, 4)])
 def test_encode_batch_dev(gpu, k, p, L, B):
     _dev_encode_check(gpu, k, p, L, B, pitch=(L + 255) // 256 * 256)
 
@@ -201,7 +204,10 @@ VARIANTS = [dict(BASE, **v) for v in (
     dict(nt_load=1, nt_store=1, depth=2, serial=1), dict(chunks=2, nt_load=1, nt_store=1, depth=2, serial=1),
     dict(nt_load=1, nt_store=1, depth=2, fuse_tail=1, serial=1),
     dict(chunks=2, nt_load=1, nt_store=1, depth=2, fuse_tail=1, serial=1), dict(nt_load=1, nt_store=1, serial=1),
-    dict(nt_load=1, nt_store=1, depth=2, early=1, serial=1), dict(nt_load=1, nt_store=1, depth=5, serial=1))]
+    dict(nt_load=1, nt_store=1, depth=2, early=1, serial=1), dict(nt_load=1, nt_store=1, depth=5, serial=1),
+    dict(nt_load=1, nt_store=1, depth=2, early=1, fuse_tail=1, serial=1),
+    dict(chunks=2, nt_load=1, nt_store=1, depth=2, early=1, serial=1),
+    dict(chunks=2, nt_load=1, nt_store=1, depth=2, early=1, fuse_tail=1, serial=1))]
 
 
 @pytest.mark.parametrize("knobs", VARIANTS, ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items() if BASE[k] != v) or "base")
