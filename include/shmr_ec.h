@@ -231,7 +231,7 @@ int shmr_ec_set_device(shmr_ec_t* rs, int device);
  * grid), "threads" (lanes per workgroup: 128, 256, 512), "depth" (register
  * ring depth = shards of loads in flight + 1: 1, 2, 3, 5, 9), "wgs_per_cu"
  * (0 = no cap, else the most workgroups resident per CU, enforced by LDS
- * padding; auto: 7 for single-row reconstructs, else no cap), "occ" (0, 6, 7: register budget for that many waves per SIMD),
+ * padding; auto: 7 for single-row reconstructs, else no cap), "occ" (0, 5, 6, 7: register budget for that many waves per SIMD),
  * "early" (0/1: issue the first data loads before the plan's LDS staging
  * completes; auto: encodes with fewer than 8 data shards or 4 output rows),
  * "spre" (0/1: coefficient tables and shard offsets by scalar

@@ -194,7 +194,7 @@ int set_tuning(const char* key, int value) {
             if ((value < 0 || value > 32) && value != kAuto) return SHMR_EC_INVALID_ARGUMENT;
             T.wgs_per_cu = value;
         } else if (k == "occ") {
-            if (value != 0 && value != 6 && value != 7 && value != kAuto) return SHMR_EC_INVALID_ARGUMENT;
+            if (value != 0 && value != 5 && value != 6 && value != 7 && value != kAuto) return SHMR_EC_INVALID_ARGUMENT;
             T.occ = value;
         } else if (k == "early") {
             T.early = value == kAuto ? kAuto : (value != 0);
