@@ -979,6 +979,47 @@ void test_read_needed_shards() {
     CHECK(planned == view(false));
 }
 
+// CPU-only view of the same plan: shard files written directly (no encode), all
+// present, so a load needs no codec call.  With the option the load reads the 8
+// data shard files; without it all 11; the loaded bytes are the data shards.
+void test_read_needed_shards_plan() {
+    auto cfg = test_config();
+    const uint64_t size = 1024 * 1024 - 4096;   // partial last data shard
+    VirtualBlock b;
+    CHECK_OK(VirtualBlock::create(19, 0, cfg, size, BlockTopology::erasure(1, 8, 3), &b));
+    const size_t S = calculate_shard_size(size, 8);
+    std::vector<uint8_t> want;
+    for (size_t i = 0; i < 11; ++i) {
+        const auto bytes = random_data(S);   // parity files hold noise: never read, never returned
+        if (i < 8) want.insert(want.end(), bytes.begin(), bytes.end());
+        FILE* f = std::fopen(shard_file(*cfg, b, i).c_str(), "wb");
+        CHECK(f != nullptr);
+        CHECK(std::fwrite(bytes.data(), 1, S, f) == S);
+        std::fclose(f);
+    }
+    want.resize(size);
+    for (bool needed : {true, false}) {
+        VirtualBlock v;
+        v.ino = b.ino;
+        v.idx = b.idx;
+        v.size = b.size;
+        v.topology = b.topology;
+        v.shards = b.shards;
+        v.populate(cfg);
+        VfsOptions o;
+        o.pread_from_start = true;
+        o.read_needed_shards = needed;
+        v.set_options(o);
+        std::vector<uint8_t> rb(size);
+        size_t n = 0;
+        const uint64_t r0 = shard_reads_total();
+        CHECK_OK(v.read(0, rb.data(), rb.size(), &n));
+        CHECK(n == size);
+        CHECK(shard_reads_total() - r0 == (needed ? 8u : 11u));
+        CHECK(rb == want);
+    }
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -1014,6 +1055,7 @@ int main(int argc, char** argv) {
         {"virtual_file_record_fuzz", test_virtual_file_record_fuzz},
         {"rewrite_erasure_record_reload", test_rewrite_erasure_record_reload},
         {"read_needed_shards", test_read_needed_shards},
+        {"read_needed_shards_plan", test_read_needed_shards_plan},
     };
     auto it = cases.find(name);
     if (it == cases.end()) {

@@ -68,6 +68,7 @@ CPU_CASES = [
     "virtual_file_chunk_model",
     "virtual_file_record_roundtrip",
     "virtual_file_record_fuzz",
+    "read_needed_shards_plan",
 ]
 
 

@@ -11,7 +11,7 @@ BIN="$ROOT/tools/_bin/vfs_test_asan"
 HIPCC=/opt/rocm/bin/hipcc
 CPU_CASES="block_topology_try_from virtual_block_new_block virtual_block_unbuffered_backing virtual_block_unbuffered
 virtual_block_buffered virtual_block_erasure_buffered block_errors virtual_file_1 virtual_file_2_4_mb virtual_file_errors
-virtual_file_chunk_model erasure_f32_hazard virtual_file_record_roundtrip virtual_file_record_fuzz"
+virtual_file_chunk_model erasure_f32_hazard virtual_file_record_roundtrip virtual_file_record_fuzz read_needed_shards_plan"
 # GPU cases with the input sizes tests/test_host_cpp.py gives them
 GPU_CASES="erasure_block_sync_load:700001 erasure_block_missing_shards:1048576 virtual_file_erasure_batch:6291456
 replace_block_erasure:300000 virtual_file_batched_reconstruct:12582912 rewrite_erasure:2109497
