@@ -19,3 +19,12 @@ def gpu():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda", 0)
+
+
+def pytest_collection_modifyitems(config, items):
+    """A test that takes the `gpu` fixture without the `gpu` marker would be
+    skipped on CPU and deselected by `-m gpu`, i.e. never run: refuse it."""
+    unmarked = [it.nodeid for it in items
+                if "gpu" in getattr(it, "fixturenames", ()) and it.get_closest_marker("gpu") is None]
+    if unmarked:
+        raise pytest.UsageError("tests use the gpu fixture without @pytest.mark.gpu: " + ", ".join(unmarked))

@@ -215,6 +215,7 @@ def test_read_needed_shards(tmp_path, gpu):
     run_case("read_needed_shards", tmp_path, data)
 
 
+@pytest.mark.gpu
 def test_rewrite_erasure_record_reload(tmp_path, gpu):
     """a file rewritten to Erasure(1,8,3) reloads from its
     durable record (the reference's serde_yaml VirtualFile value) after
