@@ -9,6 +9,7 @@ Reference call sites: ReedSolomon::encode (src/vfs/block.rs:427) and
 ReedSolomon::reconstruct / reconstruct_data (block.rs:560).
 """
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -20,6 +21,9 @@ from shmr_amd._native import _u8p, lib
 pytestmark = pytest.mark.gpu
 
 SENTINEL = 0xA5
+# SHMR_SWEEP_SCALE=N multiplies the number of seeded cases (long sweeps on the
+# GPU box: tools/sweep_long.sh); the default suite runs scale 1.
+SCALE = max(1, int(os.environ.get("SHMR_SWEEP_SCALE", "1")))
 
 
 def _shape(rng):
@@ -42,7 +46,7 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
-@pytest.mark.parametrize("case", range(40))
+@pytest.mark.parametrize("case", range(40 * SCALE))
 def test_random_encode_batch_dev(gpu, case):
     import torch
     rng = np.random.default_rng([0x5EED, case])
@@ -70,7 +74,7 @@ def test_random_encode_batch_dev(gpu, case):
     assert np.array_equal(par, expect), (k, p, L, B, spitch, off)
 
 
-@pytest.mark.parametrize("case", range(40))
+@pytest.mark.parametrize("case", range(40 * SCALE))
 def test_random_reconstruct_batch_dev(gpu, case):
     import torch
     rng = np.random.default_rng([0xDEC0, case])
@@ -116,7 +120,7 @@ def test_random_reconstruct_batch_dev(gpu, case):
     assert np.array_equal(got, expect), (k, p, L, B, spitch, off, data_only)
 
 
-@pytest.mark.parametrize("case", range(16))
+@pytest.mark.parametrize("case", range(16 * SCALE))
 def test_random_host_blocks(gpu, case):
     """Host-buffer batches: pageable and mapped buffers, random erasures."""
     rng = np.random.default_rng([0x4057, case])
