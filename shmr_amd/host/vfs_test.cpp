@@ -10,6 +10,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -1020,6 +1021,64 @@ void test_read_needed_shards_plan() {
     }
 }
 
+// Randomised Erasure-block round trips against a byte model: random (k, p) and
+// block sizes, random writes, flush, lose up to p shard files (and sometimes
+// truncate one, an erasure under short_shard_is_erasure), reload, compare;
+// then more writes into the loaded block and another round.  Options (mapped
+// Block Cache, needed-shards reads) vary per block.
+void test_virtual_block_erasure_fuzz() {
+    auto cfg = test_config();
+    const std::pair<int, int> codes[] = {{4, 2}, {8, 3}, {10, 4}, {5, 5}, {3, 1}, {6, 3}};
+    for (int it = 0; it < 120; ++it) {
+        const auto [k, p] = codes[g_rng() % 6];
+        const uint64_t size = 1 + g_rng() % (3 << 20);
+        VirtualBlock b;
+        CHECK_OK(VirtualBlock::create(20, it, cfg, size, BlockTopology::erasure(1, k, p), &b));
+        VfsOptions o;
+        o.missing_shard_is_erasure = true;
+        o.short_shard_is_erasure = true;
+        o.pread_from_start = true;
+        o.pinned_buffers = g_rng() % 2;
+        o.read_needed_shards = g_rng() % 2;
+        b.set_options(o);
+        std::vector<uint8_t> model(size, 0);
+        for (int round = 0; round < 2; ++round) {
+            const int writes = 1 + int(g_rng() % 5);
+            for (int w = 0; w < writes; ++w) {
+                const uint64_t pos = g_rng() % size;
+                const size_t len = size_t(1 + g_rng() % std::min<uint64_t>(size - pos, 1 << 20));
+                const auto bytes = random_data(len);
+                size_t n = 0;
+                CHECK_OK(b.write(pos, bytes.data(), len, &n));
+                CHECK(n == len);
+                std::memcpy(model.data() + pos, bytes.data(), len);
+            }
+            CHECK_OK(b.sync_data(true));
+            CHECK_OK(b.drop_buffer());
+            CHECK_OK(b.drop_handles());
+            const size_t lose = g_rng() % (p + 1);
+            std::vector<size_t> idx(k + p);
+            for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
+            std::shuffle(idx.begin(), idx.end(), g_rng);
+            for (size_t i = 0; i < lose; ++i) {
+                if (i == 0 && g_rng() % 3 == 0) fs::resize_file(shard_file(*cfg, b, idx[i]), g_rng() % 4096);
+                else fs::remove(shard_file(*cfg, b, idx[i]));
+            }
+            std::vector<uint8_t> rb(size);
+            size_t n = 0;
+            CHECK_OK(b.read(0, rb.data(), rb.size(), &n));
+            CHECK(n == size);
+            if (rb != model)
+                throw Failure{"iteration " + std::to_string(it) + " round " + std::to_string(round) + " RS(" +
+                              std::to_string(k) + "," + std::to_string(p) + ") size " + std::to_string(size) +
+                              diff_report(rb, model, size, calculate_shard_size(size, k))};
+        }
+        CHECK_OK(b.drop_buffer());   // repairs the lost files
+        CHECK_OK(b.drop_handles());
+        for (size_t i = 0; i < size_t(k + p); ++i) CHECK(fsize(shard_file(*cfg, b, i)) == calculate_shard_size(size, k));
+    }
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -1056,6 +1115,7 @@ int main(int argc, char** argv) {
         {"rewrite_erasure_record_reload", test_rewrite_erasure_record_reload},
         {"read_needed_shards", test_read_needed_shards},
         {"read_needed_shards_plan", test_read_needed_shards_plan},
+        {"virtual_block_erasure_fuzz", test_virtual_block_erasure_fuzz},
     };
     auto it = cases.find(name);
     if (it == cases.end()) {

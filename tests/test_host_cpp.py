@@ -216,6 +216,15 @@ def test_read_needed_shards(tmp_path, gpu):
 
 
 @pytest.mark.gpu
+def test_virtual_block_erasure_fuzz(tmp_path, gpu):
+    """120 random Erasure blocks (RS(3,1) .. RS(10,4), 1 B .. 3 MiB): random
+    writes, flush, up to p shard files lost or truncated, reload, compare with
+    a byte model -- twice per block, with mapped Block Cache and needed-shards
+    reads chosen at random (checked in C++)."""
+    run_case("virtual_block_erasure_fuzz", tmp_path, timeout=300)
+
+
+@pytest.mark.gpu
 def test_rewrite_erasure_record_reload(tmp_path, gpu):
     """a file rewritten to Erasure(1,8,3) reloads from its
     durable record (the reference's serde_yaml VirtualFile value) after
