@@ -1079,6 +1079,76 @@ void test_virtual_block_erasure_fuzz() {
     }
 }
 
+// File-level twin of the Erasure-block fuzz: random codes, block counts,
+// Block-Cache kinds, batch sizes and needed-shards reads; whole-file batched
+// flushes and loads with shard files lost or truncated in random blocks, and
+// block-level rewrites in between, against a byte model of the file.
+void test_virtual_file_erasure_fuzz() {
+    auto cfg = test_config();
+    const std::pair<int, int> codes[] = {{4, 2}, {8, 3}, {10, 4}, {5, 5}, {3, 1}};
+    const size_t batches[] = {VirtualFile::kAutoBatch, 0, 1 << 20, 3 << 20};
+    for (int it = 0; it < 16; ++it) {
+        const auto [k, p] = codes[g_rng() % 5];
+        const uint64_t bs = uint64_t(1 + g_rng() % 2) << 20;
+        const size_t nblk = 2 + g_rng() % 9;
+        VirtualFile vf = VirtualFile::new_with(30 + it, 0);
+        vf.populate(cfg);
+        vf.block_size = bs;
+        vf.pipeline_batch_bytes = batches[g_rng() % 4];
+        for (size_t i = 0; i < nblk; ++i) {
+            VirtualBlock b;
+            CHECK_OK(VirtualBlock::create(30 + it, i + 1, cfg, bs, BlockTopology::erasure(1, k, p), &b));
+            vf.blocks.push_back(b);
+        }
+        VfsOptions o;
+        o.missing_shard_is_erasure = true;
+        o.short_shard_is_erasure = true;
+        o.pread_from_start = true;
+        o.pinned_buffers = g_rng() % 2;
+        o.read_needed_shards = g_rng() % 2;
+        vf.set_options(o);
+        std::vector<uint8_t> model = random_data(nblk * bs);
+        size_t n = 0;
+        CHECK_OK(vf.write(0, model.data(), model.size(), &n));
+        CHECK(n == model.size());
+        const size_t S = calculate_shard_size(bs, k);
+        for (int round = 0; round < 3; ++round) {
+            CHECK_OK(vf.sync_data(true));
+            CHECK_OK(vf.drop_buffers());
+            CHECK_OK(vf.drop_handles());
+            for (size_t i = 0; i < nblk; ++i) {
+                const size_t lose = g_rng() % (p + 1);
+                std::vector<size_t> idx(k + p);
+                for (size_t j = 0; j < idx.size(); ++j) idx[j] = j;
+                std::shuffle(idx.begin(), idx.end(), g_rng);
+                for (size_t j = 0; j < lose; ++j) {
+                    if (j == 0 && g_rng() % 3 == 0) fs::resize_file(shard_file(*cfg, vf.blocks[i], idx[j]), g_rng() % S);
+                    else fs::remove(shard_file(*cfg, vf.blocks[i], idx[j]));
+                }
+            }
+            std::vector<uint8_t> rb(model.size());
+            CHECK_OK(vf.read(0, rb.data(), rb.size(), &n));
+            CHECK(n == model.size());
+            if (rb != model)
+                throw Failure{"iteration " + std::to_string(it) + " round " + std::to_string(round) + " RS(" +
+                              std::to_string(k) + "," + std::to_string(p) + ") " + std::to_string(nblk) + " x " +
+                              std::to_string(bs) + diff_report(rb, model, bs, S)};
+            // block-level rewrites into the loaded blocks
+            for (int w = int(g_rng() % 4); w > 0; --w) {
+                const size_t i = g_rng() % nblk;
+                const uint64_t pos = g_rng() % bs;
+                const size_t len = size_t(1 + g_rng() % (bs - pos));
+                const auto bytes = random_data(len);
+                CHECK_OK(vf.blocks[i].write(pos, bytes.data(), len, &n));
+                std::memcpy(model.data() + i * bs + pos, bytes.data(), len);
+            }
+        }
+        CHECK_OK(vf.sync_data(true));
+        CHECK_OK(vf.drop_buffers());
+        CHECK_OK(vf.drop_handles());
+    }
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -1116,6 +1186,7 @@ int main(int argc, char** argv) {
         {"read_needed_shards", test_read_needed_shards},
         {"read_needed_shards_plan", test_read_needed_shards_plan},
         {"virtual_block_erasure_fuzz", test_virtual_block_erasure_fuzz},
+        {"virtual_file_erasure_fuzz", test_virtual_file_erasure_fuzz},
     };
     auto it = cases.find(name);
     if (it == cases.end()) {

@@ -225,6 +225,16 @@ def test_virtual_block_erasure_fuzz(tmp_path, gpu):
 
 
 @pytest.mark.gpu
+def test_virtual_file_erasure_fuzz(tmp_path, gpu):
+    """16 random files of 2-10 Erasure blocks (RS(3,1) .. RS(10,4), 1-2 MiB):
+    three rounds of batched flush, random shard files lost or truncated in
+    every block, batched load compared with a byte model, block-level
+    rewrites; Block-Cache kind, batch size and needed-shards reads at random
+    (checked in C++)."""
+    run_case("virtual_file_erasure_fuzz", tmp_path, timeout=300)
+
+
+@pytest.mark.gpu
 def test_rewrite_erasure_record_reload(tmp_path, gpu):
     """a file rewritten to Erasure(1,8,3) reloads from its
     durable record (the reference's serde_yaml VirtualFile value) after
