@@ -428,7 +428,8 @@ int read_slot_counted(int fd, uint8_t* slot, size_t S, bool from_start, bool* od
 }
 
 // VfsOptions::read_needed_shards: which shard files of an Erasure block a
-// load reads (plan[i]: kRead, kPresentUnread, or kAbsent).  The file sizes
+// load reads (plan[i]: kRead, kPresentUnread, or kAbsent).  The reference
+// reads all k+p (block.rs:531-556) and returns ec_data[..size] (block.rs:576).  The file sizes
 // decide: a shard whose file is exactly S bytes is intact; the first k intact
 // shards in index order -- exactly the reconstruct's inputs (first k present,
 // the crate's rule) -- are read, the other intact ones count as present
