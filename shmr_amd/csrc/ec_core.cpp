@@ -84,7 +84,10 @@ std::atomic<int> g_alias_devices{0};   // tools build: alias device IDs (see ec_
 kern::Variant variant_policy(OpClass op, unsigned k, unsigned rows, bool host_mapped) {
     kern::Variant v;
     if (op == kDecode && rows == 1 && !host_mapped) v.wgs_per_cu = 7;
-    v.u = (op == kEncode && rows >= 4) ? 2 : 1;
+    // U = 2 (8 KiB tiles) for 4-row launches, encode and reconstruct alike: a
+    // 4-erasure RS(10,4) rebuild 73.8 vs 67.8-68.9 % at U = 1, while 2- and
+    // 3-row rebuilds lose 5-7 points at U = 2 (profiles/r02/tune_decode*.txt)
+    v.u = rows >= 4 ? 2 : 1;
     v.nt_store = true;
     v.nt_load = !host_mapped;
     v.depth = 2;

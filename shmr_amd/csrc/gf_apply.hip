@@ -826,12 +826,16 @@ hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStr
     X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial) \
     X(1, kNtLoad | kNtStore | kDepth2 | kSegs) \
     X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSegs) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse) \
     X(1, kNtStore | kDepth2 | kPtrs) \
     X(2, kNtStore | kDepth2 | kPtrs) \
     X(1, kNtStore | kDepth2 | kPtrs | kFuse) \
     X(2, kNtStore | kDepth2 | kPtrs | kFuse) \
     X(1, kNtStore | kDepth2 | kPtrs | kSegs) \
     X(1, kNtStore | kDepth2 | kPtrs | kSegs | kFuse) \
+    X(2, kNtStore | kDepth2 | kPtrs | kSegs) \
+    X(2, kNtStore | kDepth2 | kPtrs | kSegs | kFuse) \
     X(1, kNtLoad | kNtStore | kDepth2 | kPtrs) \
     X(2, kNtLoad | kNtStore | kDepth2 | kPtrs)
 
@@ -871,8 +875,6 @@ hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStr
     X(1, kNtLoad | kNtStore | kDepth2 | kSPre) \
     X(2, kNtLoad | kNtStore | kDepth2 | kSPre) \
     X(1, kNtLoad | kNtStore | kSPre) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kSegs) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse) \
     X(1, kNtLoad | kNtStore | kSegs) \
     X(1, kNtLoad | kNtStore | kSegs | kFuse) \
     X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kTh512) \

@@ -27,6 +27,9 @@ CFG = {
     "decode83": (8, 3, 4 << 20, 1, 512),
     "encode104": (10, 4, 16 << 20, 0, 64),
     "decode104": (10, 4, 16 << 20, 2, 64),
+    "decode104e4": (10, 4, 16 << 20, 4, 64),   # worst-case rebuild: 4 erasures per block
+    "decode104e3": (10, 4, 16 << 20, 3, 64),
+    "decode83e3": (8, 3, 4 << 20, 3, 512),
     "encode42": (4, 2, 1 << 20, 0, 1024),
 }
 
@@ -74,8 +77,8 @@ def main():
         if er == 1:
             present[rows, b % k] = 0
         else:
-            present[rows, b % 10] = 0
-            present[rows, (b + 3) % 10] = 0
+            for j in range(er):   # {b, b+3, b+6, b+9} mod 10: distinct
+                present[rows, (b + 3 * j) % 10] = 0
         algo = B * (k + er) * S
 
         def run():
