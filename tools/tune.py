@@ -51,9 +51,10 @@ def main():
     a = ap.parse_args()
     if a.config in CFG:
         k, p, block, er, B = CFG[a.config]
-    else:  # "k,p,block_MiB,blocks"
-        kk, pp, mb, bb = a.config.split(",")
-        k, p, block, er, B = int(kk), int(pp), int(mb) << 20, 0, int(bb)
+    else:  # "k,p,block_MiB,blocks[,erasures]" (erasures {b, b+3, ...} mod 10, or b mod k for one)
+        parts = a.config.split(",")
+        kk, pp, mb, bb = parts[:4]
+        k, p, block, er, B = int(kk), int(pp), int(mb) << 20, int(parts[4]) if len(parts) > 4 else 0, int(bb)
     S = shmr_amd.calculate_shard_size(block, k)
     dev = torch.device("cuda", 0)
     rs = shmr_amd.ReedSolomon(k, p)
@@ -77,8 +78,9 @@ def main():
         if er == 1:
             present[rows, b % k] = 0
         else:
-            for j in range(er):   # {b, b+3, b+6, b+9} mod 10: distinct
-                present[rows, (b + 3 * j) % 10] = 0
+            n = min(k + p, 10)
+            for j in range(er):   # {b, b+3, b+6, b+9} mod n (n = 10, or k+p if smaller): distinct for n >= 3*er - 2
+                present[rows, (b + 3 * j) % n] = 0
         algo = B * (k + er) * S
 
         def run():
