@@ -76,6 +76,11 @@ def parse():
     ap.add_argument("--pitch-align", type=int, default=4096,
                     help="device shard pitch = S rounded up to this many bytes (DESIGN.md section 4: 4 KiB "
                          "measured +0.7-1.0 point of HBM peak over 256 B for RS(10,4)'s S = 1,677,722)")
+    ap.add_argument("--pitch-pad", type=int, default=-1,
+                    help="bytes added to every shard slot after alignment; -1 (auto): one 4 KiB page when the "
+                         "aligned pitch is a multiple of 64 KiB (power-of-two shard sizes: RS(8,3) 4 MiB, RS(4,2) "
+                         "1 MiB), whose shards would otherwise all start on the same HBM channel; 0 = the "
+                         "reference's contiguous block buffer for those sizes (DESIGN.md section 4)")
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher rehearsal without a GPU: ranks join the process group, exchange their "
                          "identities and rank 0 prints one JSON line (tests/test_bench_launch.py)")
@@ -210,12 +215,15 @@ def run(args):
 
     # Synthetic blocks, generated on the GPU from a per-rank seed (inputs
     # resident in HBM before timing).  HBM layout: shard i of block b at
-    # (b*k + i) * pitch with pitch = S rounded up to 4 KiB -- for S = 524,288
-    # this IS the reference's block buffer (shards contiguous at i*S); for
-    # S = 1,677,722 (RS(10,4) 16 MiB) it is the page-aligned pitched layout
-    # (1,679,360 B per shard slot, 0.1 % padding).
+    # (b*k + i) * pitch with pitch = S rounded up to 4 KiB, plus one 4 KiB page
+    # when that is a multiple of 64 KiB: S = 524,288 (RS(8,3) 4 MiB) gets
+    # 528,384-byte slots (0.8 % padding) instead of the reference's contiguous
+    # block buffer, whose 2^19 shard stride starts every shard of a tile on the
+    # same HBM channel; S = 1,677,722 (RS(10,4) 16 MiB) gets the page-aligned
+    # 1,679,360-byte slots (0.1 %) and no page.
     a = max(16, args.pitch_align)
     pitch = (S + a - 1) // a * a
+    pitch += (4096 if pitch % 65536 == 0 else 0) if args.pitch_pad < 0 else args.pitch_pad
     g = torch.Generator(device=dev)
     g.manual_seed(SEED + rank)
     bufs = []

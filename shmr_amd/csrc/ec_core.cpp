@@ -51,11 +51,10 @@ std::atomic<int> g_alias_devices{0};   // tools build: alias device IDs (see ec_
 // that lift RS(8,3) from 5 to 6 waves/SIMD), RS(4,2) 78 % vs 77 %, RS(10,4)
 // 71 % vs 70 %, reconstruct RS(8,3) 72 % vs 71 %; deeper rings (5, 9) and
 // occupancy caps lose.  With depth 2, NT loads + NT stores win everywhere;
-// encodes with 4 rows per launch (RS(10,4)) use U = 2.  Encodes with k < 8
-// (short-lived workgroups) issue their first data loads ahead of the plan
-// staging ("early": RS(4,2) 83 % vs 80 %; neutral at k = 8, -2 % on decode,
-// re-measured with segment launches: RS(8,3) 71.1 vs 72.6 %, RS(10,4) 75.1 vs
-// 76.6 %).  Decodes with temporal stores lose 5-8 points (RS(8,3) 64.8 vs
+// launches of 4 rows use U = 2.  Encodes with k <= 8 (short-lived
+// workgroups) issue their first data loads ahead of the plan staging
+// ("early": RS(4,2) 83 % vs 80 %; -2 % on decode, re-measured with segment
+// launches: RS(8,3) 71.1 vs 72.6 %, RS(10,4) 75.1 vs 76.6 %).  Decodes with temporal stores lose 5-8 points (RS(8,3) 64.8 vs
 // 73.3 %, RS(10,4) 70.7 vs 75.9 %), although a copy-only 8-in/1-out probe
 // preferred them (tools/membench.hip).
 // Scalar-loaded tables ("spre", 7-8 waves/SIMD) lose 3-6 % everywhere.
@@ -91,11 +90,14 @@ kern::Variant variant_policy(OpClass op, unsigned k, unsigned rows, bool host_ma
     v.nt_store = true;
     v.nt_load = !host_mapped;
     v.depth = 2;
-    // early prologue for small k; for 4-row encodes (RS(10,4)) early plus the
-    // per-dword math order (fewer live VGPRs at U = 2): +0.5 - 1.0 point in
-    // three interleaved A/Bs (profiles/r02/tune_encode104_early_serial*.txt);
-    // serial loses on RS(8,3) encode (profiles/r02/tune_encode83_early_serial.txt)
-    v.early = op == kEncode && (k < 8 || rows >= 4) && !host_mapped;
+    // early prologue for k <= 8 (RS(8,3) with de-aliased shard slots +1.2 -
+    // 1.4 points, RS(8,1) / RS(8,2) +2.4, RS(4,2) +1.7 - 2.6; RS(8,3) on the
+    // contiguous 2^19-stride layout -0.3 - 0.6: profiles/r02/pad/); for
+    // 4-row encodes (RS(10,4)) early plus the per-dword math order (fewer live
+    // VGPRs at U = 2): +0 - 1.0 point in interleaved A/Bs
+    // (profiles/r02/tune_encode104_early_serial*.txt); serial loses on RS(8,3)
+    // encode (profiles/r02/tune_encode83_early_serial.txt)
+    v.early = op == kEncode && (k <= 8 || rows >= 4) && !host_mapped;
     v.serial = op == kEncode && rows >= 4 && !host_mapped;
     v.fuse_tail = true;   // only where len % tile != 0 (RS(10,4): -5.5 % encode, -5.8 % decode time)
     return v;

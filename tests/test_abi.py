@@ -206,7 +206,8 @@ def test_tuning_api():
     assert "nt_load=1" in shmr_amd.describe_variant(True, 8, 1)
     assert "depth=2" in shmr_amd.describe_variant(True, 8, 1)
     assert "early=1" in shmr_amd.describe_variant(False, 4, 2)
-    assert "early=0" in shmr_amd.describe_variant(False, 8, 3)
+    assert "early=1" in shmr_amd.describe_variant(False, 8, 3)
+    assert "early=0" in shmr_amd.describe_variant(False, 10, 3)
     assert "early=0" in shmr_amd.describe_variant(True, 4, 2)
     assert "fuse_tail=1" in shmr_amd.describe_variant(False, 10, 4)
     assert "fuse_tail=1" in shmr_amd.describe_variant(True, 10, 2)

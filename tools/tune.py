@@ -69,7 +69,7 @@ def main():
         def run():
             rs.encode_batch_dev(data, parity, shard_len=S)
     else:
-        pitch = (S + 255) // 256 * 256
+        pitch = (S + 255) // 256 * 256 + a.pad
         shards = torch.zeros((B, k + p, pitch), dtype=torch.uint8, device=dev)
         shards[:, :k, :S] = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=dev, generator=g)
         present = np.ones((B, k + p), np.uint8)
