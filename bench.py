@@ -346,6 +346,10 @@ def run(args):
             "tuning": tuning,
             "memory": "physically contiguous VRAM (shmr_ec_device_alloc)" if args.contig else "torch caching allocator (hipMalloc)",
             "shard_pitch_bytes": pitch,
+            "shard_layout": ("contiguous shards (the reference's block buffer)" if pitch == S else
+                             f"shard slots of {pitch} B for {S} B shards"
+                             + (" (one 4 KiB page past the 4 KiB-aligned size: power-of-two strides alias HBM "
+                                "channels, DESIGN.md section 4)" if pitch - S >= 4096 else " (4 KiB-aligned)")),
         },
         "roofline": {
             "bound": "hbm",
