@@ -896,6 +896,8 @@ hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStr
     X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial | (5 << kOccShift)) \
     X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | (5 << kOccShift)) \
     X(2, kNtLoad | kNtStore | kDepth2 | kFuse | (5 << kOccShift)) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kEarly) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kEarly) \
     X(1, kDiagXor | kNtLoad | kNtStore | kDepth2) \
     X(2, kDiagXor | kNtLoad | kNtStore | kDepth2) \
     X(1, kDiagXor | kNtLoad | kNtStore | kDepth2 | kFuse) \
