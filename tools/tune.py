@@ -45,6 +45,7 @@ def main():
                     help="';'-separated knob sets applied on top of the defaults (prefix-free keys)")
     ap.add_argument("--json", default="")
     ap.add_argument("--pad", type=int, default=0, help="extra bytes per shard pitch (de-alias 2^n strides)")
+    ap.add_argument("--bpad", type=int, default=0, help="encode: extra bytes per block pitch")
     ap.add_argument("--diag", action="store_true", help="also time the XOR-only ceiling kernel")
     ap.add_argument("--ref", action="store_true", help="also time torch copy / xor references")
     ap.add_argument("--same-pattern", action="store_true", help="decode: every block loses the same shards")
@@ -62,8 +63,14 @@ def main():
     g.manual_seed(1)
     if er == 0:
         P = (S + 255) // 256 * 256 + a.pad
-        data = torch.randint(0, 256, (B, k, P), dtype=torch.uint8, device=dev, generator=g)
-        parity = torch.empty((B, p, P), dtype=torch.uint8, device=dev)
+        if a.bpad:   # extra bytes per block pitch (block stride != k * shard pitch)
+            flat = torch.randint(0, 256, (B * (k * P + a.bpad),), dtype=torch.uint8, device=dev, generator=g)
+            data = flat.as_strided((B, k, P), (k * P + a.bpad, P, 1))
+            parity = torch.empty((B * (p * P + a.bpad),), dtype=torch.uint8, device=dev).as_strided(
+                (B, p, P), (p * P + a.bpad, P, 1))
+        else:
+            data = torch.randint(0, 256, (B, k, P), dtype=torch.uint8, device=dev, generator=g)
+            parity = torch.empty((B, p, P), dtype=torch.uint8, device=dev)
         algo = B * (k + p) * S
 
         def run():
