@@ -79,8 +79,8 @@ def parse():
     ap.add_argument("--pitch-pad", type=int, default=-1,
                     help="bytes added to every shard slot after alignment; -1 (auto): one 4 KiB page when the "
                          "aligned pitch is a multiple of 64 KiB (power-of-two shard sizes: RS(8,3) 4 MiB, RS(4,2) "
-                         "1 MiB), whose shards would otherwise all start on the same HBM channel; 0 = the "
-                         "reference's contiguous block buffer for those sizes (DESIGN.md section 4)")
+                         "1 MiB: +1.7-1.8 points of HBM peak); 0 = the reference's contiguous block buffer for "
+                         "those sizes (DESIGN.md section 4)")
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher rehearsal without a GPU: ranks join the process group, exchange their "
                          "identities and rank 0 prints one JSON line (tests/test_bench_launch.py)")
@@ -218,9 +218,9 @@ def run(args):
     # (b*k + i) * pitch with pitch = S rounded up to 4 KiB, plus one 4 KiB page
     # when that is a multiple of 64 KiB: S = 524,288 (RS(8,3) 4 MiB) gets
     # 528,384-byte slots (0.8 % padding) instead of the reference's contiguous
-    # block buffer, whose 2^19 shard stride starts every shard of a tile on the
-    # same HBM channel; S = 1,677,722 (RS(10,4) 16 MiB) gets the page-aligned
-    # 1,679,360-byte slots (0.1 %) and no page.
+    # block buffer, whose 2^19 shard stride measured 1.8 points of HBM peak
+    # slower; S = 1,677,722 (RS(10,4) 16 MiB) gets the
+    # page-aligned 1,679,360-byte slots (0.1 %) and no page.
     a = max(16, args.pitch_align)
     pitch = (S + a - 1) // a * a
     pitch += (4096 if pitch % 65536 == 0 else 0) if args.pitch_pad < 0 else args.pitch_pad
@@ -348,8 +348,8 @@ def run(args):
             "shard_pitch_bytes": pitch,
             "shard_layout": ("contiguous shards (the reference's block buffer)" if pitch == S else
                              f"shard slots of {pitch} B for {S} B shards"
-                             + (" (one 4 KiB page past the 4 KiB-aligned size: power-of-two strides alias HBM "
-                                "channels, DESIGN.md section 4)" if pitch - S >= 4096 else " (4 KiB-aligned)")),
+                             + (" (one 4 KiB page past the 4 KiB-aligned size for a power-of-two stride, "
+                                "DESIGN.md section 4)" if pitch - S >= 4096 else " (4 KiB-aligned)")),
         },
         "roofline": {
             "bound": "hbm",

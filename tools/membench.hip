@@ -6,7 +6,8 @@
 //
 //   hipcc -O3 --offload-arch=gfx950 tools/membench.hip -o tools/_bin/membench
 //   membench [shard_bytes=524288] [blocks=512] [iters=20]
-//   env: MEMBENCH_ALLOC=contig (physically contiguous VRAM), MEMBENCH_ONLY=83
+//   env: MEMBENCH_ALLOC=contig (physically contiguous VRAM), MEMBENCH_ONLY=83,
+//        MEMBENCH_PITCH=<bytes> (shard slot > S: padded layout, bench.py --pitch-pad)
 //
 // Prints one JSON line per (pattern, variant): TB/s of algorithmic bytes
 // (K + R) * S * B and the fraction of the 8 TB/s HBM peak.
@@ -46,6 +47,7 @@ template <int K, int R, int U, int F>
 __global__ __launch_bounds__(256) void kin_rout(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                 uint64_t S, uint64_t tiles_per_block, uint32_t ntiles,
                                                 uint32_t* sink) {
+    // S here is the shard slot (pitch); tiles_per_block covers the shard length
     uint32_t tile = blockIdx.x;
     if constexpr (F & kRemap) {
         // XCD-contiguous: dispatch puts blockIdx i on XCD i % 8; give XCD x the
@@ -88,13 +90,15 @@ __global__ __launch_bounds__(256) void kin_rout(const uint8_t* __restrict__ in, 
 template <int K, int R, int U, int F>
 void run(const char* name, const uint8_t* in, uint8_t* out, uint64_t S, uint64_t B, uint32_t* sink, int iters) {
     const uint64_t tpb = S / (4096ull * U);
+    const char* pe = std::getenv("MEMBENCH_PITCH");
+    const uint64_t P = pe ? std::strtoull(pe, nullptr, 10) : S;   // shard slot
     const uint32_t grid = uint32_t(tpb * B);
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    for (int w = 0; w < 10; ++w) kin_rout<K, R, U, F><<<grid, 256>>>(in, out, S, tpb, grid, sink);
+    for (int w = 0; w < 10; ++w) kin_rout<K, R, U, F><<<grid, 256>>>(in, out, P, tpb, grid, sink);
     CK(hipEventRecord(e0));
-    for (int i = 0; i < iters; ++i) kin_rout<K, R, U, F><<<grid, 256>>>(in, out, S, tpb, grid, sink);
+    for (int i = 0; i < iters; ++i) kin_rout<K, R, U, F><<<grid, 256>>>(in, out, P, tpb, grid, sink);
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
     float ms = 0;
@@ -102,8 +106,9 @@ void run(const char* name, const uint8_t* in, uint8_t* out, uint64_t S, uint64_t
     ms /= iters;
     const double tbps = double(B) * (K + R) * S / (ms * 1e-3) / 1e12;
     std::printf("{\"pattern\": \"%din%dout\", \"variant\": \"%s\", \"U\": %d, \"ntl\": %d, \"nts\": %d, \"remap\": %d, "
-                "\"ms\": %.4f, \"TBps\": %.3f, \"frac\": %.4f}\n",
-                K, R, name, U, (F & kNtL) ? 1 : 0, (F & kNtS) ? 1 : 0, (F & kRemap) ? 1 : 0, ms, tbps, tbps / 8.0);
+                "\"pitch\": %llu, \"ms\": %.4f, \"TBps\": %.3f, \"frac\": %.4f}\n",
+                K, R, name, U, (F & kNtL) ? 1 : 0, (F & kNtS) ? 1 : 0, (F & kRemap) ? 1 : 0, (unsigned long long)P, ms,
+                tbps, tbps / 8.0);
     CK(hipEventDestroy(e0));
     CK(hipEventDestroy(e1));
 }
@@ -129,23 +134,29 @@ int main(int argc, char** argv) {
     }
     uint8_t *in, *out;
     uint32_t* sink;
+    const char* pe = std::getenv("MEMBENCH_PITCH");
+    const uint64_t P = pe ? std::strtoull(pe, nullptr, 10) : S;
+    if (P < S) {
+        std::fprintf(stderr, "MEMBENCH_PITCH must be >= S\n");
+        return 2;
+    }
     // MEMBENCH_ALLOC=contig: physically contiguous VRAM (hipDeviceMallocContiguous),
     // to separate page-translation effects from the access pattern's own ceiling.
     const char* alloc = std::getenv("MEMBENCH_ALLOC");
     const bool contig = alloc && std::strcmp(alloc, "contig") == 0;
     if (contig) {
-        CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&in), B * 10 * S, hipDeviceMallocContiguous));
-        CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&out), B * 4 * S, hipDeviceMallocContiguous));
+        CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&in), B * 10 * P, hipDeviceMallocContiguous));
+        CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&out), B * 4 * P, hipDeviceMallocContiguous));
     } else {
-        CK(hipMalloc(&in, B * 10 * S));
-        CK(hipMalloc(&out, B * 4 * S));
+        CK(hipMalloc(&in, B * 10 * P));
+        CK(hipMalloc(&out, B * 4 * P));
     }
     const char* only = std::getenv("MEMBENCH_ONLY");   // "83": the RS(8,3) encode pattern only
     CK(hipMalloc(&sink, 4));
-    CK(hipMemset(in, 0x5a, B * 10 * S));
-    CK(hipMemset(out, 0, B * 4 * S));
+    CK(hipMemset(in, 0x5a, B * 10 * P));
+    CK(hipMemset(out, 0, B * 4 * P));
     for (int i = 0; i < 300; ++i)   // clock ramp
-        kin_rout<8, 3, 1, 3><<<uint32_t(S / 4096 * B), 256>>>(in, out, S, S / 4096, uint32_t(S / 4096 * B), sink);
+        kin_rout<8, 3, 1, 3><<<uint32_t(S / 4096 * B), 256>>>(in, out, P, S / 4096, uint32_t(S / 4096 * B), sink);
     CK(hipDeviceSynchronize());
     for (int rep = 0; rep < 2; ++rep) {
         pattern<8, 3>(in, out, S, B, sink, iters);
