@@ -181,10 +181,6 @@ int shmr_ec_describe_variant(int decode, uint32_t data_shards, uint32_t rows, ch
         const size_t n = std::strlen(buf);
         if (kv.first && n + 1 < len) std::snprintf(buf + n, len - n, "%s", kv.second);
     }
-    if (v.split > 0) {
-        const size_t n = std::strlen(buf);
-        if (n + 1 < len) std::snprintf(buf + n, len - n, " split=%d", v.split);
-    }
     return SHMR_EC_OK;
 }
 

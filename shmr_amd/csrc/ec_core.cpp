@@ -37,7 +37,6 @@ struct Tuning {
     std::atomic<int> fuse_tail{kAuto};
     std::atomic<int> glds{kAuto};
     std::atomic<int> serial{kAuto};
-    std::atomic<int> split{kAuto};
 };
 Tuning g_tune[2];   // [kEncode], [kDecode]
 std::atomic<int> g_bounce_kib{kBounceKibDefault};
@@ -167,7 +166,7 @@ int set_tuning(const char* key, int value) {
             {"chunks", kAuto}, {"nt_load", kAuto}, {"nt_store", kAuto}, {"scalar_tabs", 0}, {"occ8", 0},
             {"grid", -1},      {"diag", 0},        {"threads", 256},    {"depth", kAuto},   {"wgs_per_cu", kAuto},
             {"occ", kAuto},    {"early", kAuto},   {"spre", kAuto},     {"fuse_tail", kAuto},
-            {"glds", kAuto},   {"serial", kAuto},  {"split", kAuto}};
+            {"glds", kAuto},   {"serial", kAuto}};
         const auto it = kDefaults.find(k);
         return (it != kDefaults.end() && it->second == value) ? SHMR_EC_OK : SHMR_EC_INVALID_ARGUMENT;
     }
@@ -212,9 +211,6 @@ int set_tuning(const char* key, int value) {
             T.glds = value == kAuto ? kAuto : (value != 0);
         } else if (k == "serial") {
             T.serial = value == kAuto ? kAuto : (value != 0);
-        } else if (k == "split") {
-            if (value < 0 && value != kAuto) return SHMR_EC_INVALID_ARGUMENT;
-            T.split = value;
         } else {
             return SHMR_EC_INVALID_ARGUMENT;
         }
@@ -248,7 +244,6 @@ int get_tuning(const char* key) {
     if (k == "fuse_tail") return T.fuse_tail;
     if (k == "glds") return T.glds;
     if (k == "serial") return T.serial;
-    if (k == "split") return T.split;
     return SHMR_EC_INVALID_ARGUMENT;
 }
 
@@ -272,7 +267,6 @@ kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_m
     if (T.fuse_tail.load() != kAuto) v.fuse_tail = T.fuse_tail.load() != 0;
     if (T.glds.load() != kAuto) v.glds = T.glds.load() != 0;
     if (T.serial.load() != kAuto) v.serial = T.serial.load() != 0;
-    if (T.split.load() != kAuto) v.split = T.split.load();
     if (v.glds) v.early = v.spre = v.scalar_tabs = false;   // the LDS-DMA ring is a form of the plain tile
     return v;
 }
@@ -303,7 +297,6 @@ kern::Variant launch_variant(OpClass op, unsigned k, unsigned rows, bool host_ma
     v.segs = segs;
     if (ptrs) {
         v.early = v.spre = v.scalar_tabs = v.glds = false;   // only the plain LDS-staged tile reads pointer tables
-        v.split = 0;                                           // (a split drain is a form of the early tile)
         if (g_tune[op].serial.load() == kAuto) v.serial = false;   // the policy's serial goes with early
         kern::Variant lean = v;
         lean.fuse_tail = false;
@@ -462,25 +455,15 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
             fused = kern::variant_compiled(fv);
         }
         var.fuse_tail = fused;
-        if (var.split > 0 && !(var.u == 2 && var.early && kern::variant_compiled(var))) var.split = 0;
         if (full) {
             a.col_base = 0;
             a.tiles_per_block = uint32_t(full);
             a.lead_tails = fused ? nblk : 0;
             a.ntiles = nblk * full + a.lead_tails;
-            if (var.split > 0) {   // the last `split` full tiles run as halves (ApplyArgs::split_from)
-                // only full tiles split (lead_tails <= split_from), and split_from > 0
-                // (0 means no split)
-                const uint64_t ns =
-                    std::min<uint64_t>(uint64_t(var.split), nblk * full - (a.lead_tails == 0 ? 1 : 0));
-                a.split_from = a.ntiles - ns;
-                a.ntiles += ns;
-            }
             const hipError_t e = kern::launch_apply(a, rows, var, 0, cap, stream);
             if (e == hipErrorInvalidValue) return SHMR_EC_INVALID_ARGUMENT;   // variant not compiled
             if (e != hipSuccess) return SHMR_EC_DEVICE_ERROR;
             a.lead_tails = 0;
-            a.split_from = 0;
         }
         if (len % tb && !fused) {
             const uint64_t tb1 = kern::tile_bytes(1);

@@ -66,9 +66,6 @@ constexpr int kGlds = 1 << 21;
 // before the first XOR (48 live temporaries at R = 4), trading ILP inside a
 // wave for registers (more waves per SIMD).
 constexpr int kSerial = 1 << 22;
-// Split drain (U = 2, early-prologue tiles): the last full tiles of the grid
-// run as 4 KiB halves (ApplyArgs::split_from).
-constexpr int kSplit = 1 << 23;
 
 template <int MODE, int F>
 constexpr bool has_ptrs() {
@@ -678,18 +675,7 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
         const uint64_t tb = uint64_t(TH) * 16 * U;
         bool first = true;
         for (uint64_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
-            // split drain: grid tile split_from + 2i + h = half h of full tile split_from + i
-            bool half = false;
-            uint64_t hoff = 0, ft = tile;
-            if constexpr ((F & kSplit) != 0 && MODE == 0 && U == 2) {
-                if (a.split_from && tile >= a.split_from) {
-                    const uint64_t d = tile - a.split_from;
-                    hoff = (d & 1) * uint64_t(TH) * 16;
-                    ft = a.split_from + (d >> 1);
-                    half = true;
-                }
-            }
-            const TileRef tr = tile_ref<F>(a, ft);
+            const TileRef tr = tile_ref<F>(a, tile);
             const uint64_t j = tr.j, cc = tr.cc;
             uint64_t blk;
             const uint8_t* plan = a.plan;
@@ -717,8 +703,6 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
                 }
             } else if ((F & kFuse) != 0 && MODE == 0 && tr.tail) {
                 early_tile<R, U, 1, F>(a, plan, smem, first, ib, ob, col);
-            } else if ((F & kSplit) != 0 && MODE == 0 && U == 2 && half) {
-                early_tile<R, 1, MODE, F>(a, plan, smem, first, ib, ob, col + hoff);
             } else {
                 early_tile<R, U, MODE, F>(a, plan, smem, first, ib, ob, col);
             }
@@ -932,11 +916,7 @@ hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStr
     X(1, kNtLoad | kNtStore | kGlds | kSegs) \
     X(1, kNtLoad | kNtStore | kGlds | kDepth5 | kSegs) \
     X(1, kNtLoad | kNtStore | kGlds | kSegs | kFuse) \
-    X(1, kNtLoad | kNtStore | kGlds | kDepth5 | kSegs | kFuse) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSplit) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSplit) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial | kSplit) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial | kSplit)
+    X(1, kNtLoad | kNtStore | kGlds | kDepth5 | kSegs | kFuse)
 #define SHMR_VARIANTS(X) SHMR_VARIANTS_PRODUCT(X) SHMR_VARIANTS_TOOLS(X)
 #else
 #define SHMR_VARIANTS(X) SHMR_VARIANTS_PRODUCT(X)
@@ -948,7 +928,7 @@ int variant_flags(const Variant& v) {
            (v.threads == 512 ? kTh512 : 0) | (v.depth == 5 ? kDepth5 : 0) | (v.depth == 9 ? kDepth9 : 0) |
            (v.depth == 2 ? kDepth2 : 0) | (v.depth == 1 ? kDepth1 : 0) | ((v.occ & 15) << kOccShift) |
            (v.early ? kEarly : 0) | (v.spre ? kSPre : 0) | (v.fuse_tail ? kFuse : 0) | (v.ptrs ? kPtrs : 0) |
-           (v.segs ? kSegs : 0) | (v.glds ? kGlds : 0) | (v.serial ? kSerial : 0) | (v.split > 0 ? kSplit : 0);
+           (v.segs ? kSegs : 0) | (v.glds ? kGlds : 0) | (v.serial ? kSerial : 0);
 }
 
 template <int R>

@@ -68,12 +68,6 @@ struct ApplyArgs {
     // run bounds-checked; tile lead_tails + t is full tile t.  Leading, so the
     // latency-bound partial tiles start first and finish under the full ones.
     uint64_t lead_tails;
-    // Split drain (kernels compiled with the split flag, U = 2): grid tiles
-    // from split_from on are halves of full tiles -- grid tile split_from + 2i + h
-    // is half h (4 KiB of columns) of full tile split_from + i -- so the
-    // workgroups dispatched last are half as long and the launch drains sooner.
-    // 0: no split.
-    uint64_t split_from;
     // Segment launches (nseg > 0; plan / plan_table / blk_list unused): block
     // j of the launch is found in segs[0 .. nseg) (ascending start, segs[0].start = 0).
     uint32_t nseg;
@@ -99,7 +93,6 @@ struct Variant {
     bool segs = false;       // full-tile kernel that takes segment launches (set by launch_set)
     bool glds = false;       // input ring in LDS filled by LDS-DMA (depth = slots; full tiles only)
     bool serial = false;     // GF math one dword at a time (fewer live registers, more waves)
-    int split = 0;           // > 0: the last `split` full U = 2 tiles run as two 4 KiB halves (ApplyArgs::split_from)
 };
 
 // rows in [1, kMaxRowsPerLaunch].  mode 0: full tiles, every shard base
