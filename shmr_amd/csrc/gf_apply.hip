@@ -916,7 +916,11 @@ hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStr
     X(1, kNtLoad | kNtStore | kGlds | kSegs) \
     X(1, kNtLoad | kNtStore | kGlds | kDepth5 | kSegs) \
     X(1, kNtLoad | kNtStore | kGlds | kSegs | kFuse) \
-    X(1, kNtLoad | kNtStore | kGlds | kDepth5 | kSegs | kFuse)
+    X(1, kNtLoad | kNtStore | kGlds | kDepth5 | kSegs | kFuse) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSPre | kFuse) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSPre | kFuse | kSerial) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSPre | kFuse) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSPre | kFuse | kSerial)
 #define SHMR_VARIANTS(X) SHMR_VARIANTS_PRODUCT(X) SHMR_VARIANTS_TOOLS(X)
 #else
 #define SHMR_VARIANTS(X) SHMR_VARIANTS_PRODUCT(X)

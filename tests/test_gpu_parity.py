@@ -207,7 +207,12 @@ VARIANTS = [dict(BASE, **v) for v in (
     dict(nt_load=1, nt_store=1, depth=2, early=1, serial=1), dict(nt_load=1, nt_store=1, depth=5, serial=1),
     dict(nt_load=1, nt_store=1, depth=2, early=1, fuse_tail=1, serial=1),
     dict(chunks=2, nt_load=1, nt_store=1, depth=2, early=1, serial=1),
-    dict(chunks=2, nt_load=1, nt_store=1, depth=2, early=1, fuse_tail=1, serial=1))]
+    dict(chunks=2, nt_load=1, nt_store=1, depth=2, early=1, fuse_tail=1, serial=1),
+    # scalar-loaded tables with fused tails (tools/ab_spre.sh)
+    dict(chunks=2, nt_load=1, nt_store=1, depth=2, spre=1, fuse_tail=1),
+    dict(chunks=2, nt_load=1, nt_store=1, depth=2, spre=1, fuse_tail=1, serial=1),
+    dict(nt_load=1, nt_store=1, depth=2, spre=1, fuse_tail=1),
+    dict(nt_load=1, nt_store=1, depth=2, spre=1, fuse_tail=1, serial=1, wgs_per_cu=6))]
 
 
 @pytest.mark.parametrize("knobs", VARIANTS, ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items() if BASE[k] != v) or "base")
