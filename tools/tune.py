@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--json", default="")
     ap.add_argument("--pad", type=int, default=0, help="extra bytes per shard pitch (de-alias 2^n strides)")
     ap.add_argument("--bpad", type=int, default=0, help="encode: extra bytes per block pitch")
+    ap.add_argument("--ppad", type=int, default=None,
+                    help="encode: parity shard pitch = S rounded to 256 B plus this (default: --pad, as the data)")
     ap.add_argument("--diag", action="store_true", help="also time the XOR-only ceiling kernel")
     ap.add_argument("--ref", action="store_true", help="also time torch copy / xor references")
     ap.add_argument("--same-pattern", action="store_true", help="decode: every block loses the same shards")
@@ -70,7 +72,8 @@ def main():
                 (B, p, P), (p * P + a.bpad, P, 1))
         else:
             data = torch.randint(0, 256, (B, k, P), dtype=torch.uint8, device=dev, generator=g)
-            parity = torch.empty((B, p, P), dtype=torch.uint8, device=dev)
+            PP = P if a.ppad is None else (S + 255) // 256 * 256 + a.ppad
+            parity = torch.empty((B, p, PP), dtype=torch.uint8, device=dev)
         algo = B * (k + p) * S
 
         def run():
