@@ -439,11 +439,25 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
         a.shard_ptrs = L.d_ptrs;
         a.total = L.total;
         if (!aligned) {
+            // Device-resident shards off 16-byte alignment (the reference's
+            // contiguous block buffer, shard i at i * S): full 4 KiB tiles in
+            // the realigning vector kernel (mode 3), the rest byte-granular.
+            // Mapped host shards stay byte-granular: their loads cross PCIe,
+            // where mode 3's second (overlapping) load would be paid again.
             const uint64_t tb1 = kern::tile_bytes(1);
-            a.col_base = 0;
-            a.tiles_per_block = uint32_t((len + tb1 - 1) / tb1);
-            a.ntiles = nblk * a.tiles_per_block;
-            SHMR_HIP_TRY(kern::launch_apply(a, rows, tail, 2, cap, stream));
+            const uint64_t full1 = ptrs ? 0 : len / tb1;
+            if (full1) {
+                a.col_base = 0;
+                a.tiles_per_block = uint32_t(full1);
+                a.ntiles = nblk * full1;
+                SHMR_HIP_TRY(kern::launch_apply(a, rows, tail, 3, cap, stream));
+            }
+            if (len > full1 * tb1) {
+                a.col_base = full1 * tb1;
+                a.tiles_per_block = uint32_t((len - full1 * tb1 + tb1 - 1) / tb1);
+                a.ntiles = nblk * a.tiles_per_block;
+                SHMR_HIP_TRY(kern::launch_apply(a, rows, tail, 2, cap, stream));
+            }
             continue;
         }
         const uint64_t full = len / tb;

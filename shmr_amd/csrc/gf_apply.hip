@@ -158,8 +158,28 @@ __device__ __forceinline__ void store_bytes(uint8_t* p, u32x4 v, int64_t n) {
         if (b < n) p[b] = uint8_t(w[b >> 2] >> (8 * (b & 3)));
 }
 
+// Bytes [s, s + 16) of the 32-byte window lo:hi, s in [0, 16) wave-uniform
+// (the switch is a scalar branch; v_alignbyte_b32 takes the byte shift).
+__device__ __forceinline__ u32x4 funnel16(const u32x4& lo, const u32x4& hi, uint32_t s) {
+    const uint32_t r = s & 3u;
+    auto ab = [r](uint32_t h, uint32_t l) { return __builtin_amdgcn_alignbyte(h, l, r); };
+    switch (s >> 2) {
+        case 0: return u32x4{ab(lo.y, lo.x), ab(lo.z, lo.y), ab(lo.w, lo.z), ab(hi.x, lo.w)};
+        case 1: return u32x4{ab(lo.z, lo.y), ab(lo.w, lo.z), ab(hi.x, lo.w), ab(hi.y, hi.x)};
+        case 2: return u32x4{ab(lo.w, lo.z), ab(hi.x, lo.w), ab(hi.y, hi.x), ab(hi.z, hi.y)};
+        default: return u32x4{ab(hi.x, lo.w), ab(hi.y, hi.x), ab(hi.z, hi.y), ab(hi.w, hi.z)};
+    }
+}
+
 // MODE 0: full tile, aligned vector path.  MODE 1: partial tail tile (bounds
-// per lane), aligned.  MODE 2: arbitrary alignment, byte-granular.
+// per lane), aligned.  MODE 2: arbitrary alignment, byte-granular.  MODE 3:
+// full tile over shards that are not 16-byte aligned (the reference's
+// contiguous block buffer with shards at i * S, e.g. RS(10,4) 16 MiB:
+// S = 1,677,722): 16-byte aligned vector loads realigned in registers (the
+// register ring of do_tile), and stores realigned across lanes (st_shifted).
+// A shard's misalignment is uniform over the tile (lanes' columns are
+// multiples of 16): it is read into a scalar register, so every branch on it
+// is a scalar branch.
 template <int MODE, int F>
 __device__ __forceinline__ u32x4 ld(const uint8_t* base, uint64_t col, uint64_t len) {
     if constexpr (MODE == 0) {
@@ -172,10 +192,44 @@ __device__ __forceinline__ u32x4 ld(const uint8_t* base, uint64_t col, uint64_t 
     }
 }
 
+// MODE 3 store of one wave's contiguous 1 KiB run (lane L owns bytes
+// [p_L, p_L + 16), p_L = p_0 + 16 L, p_0 misaligned by mo): lane L >= 1 writes
+// the aligned chunk at p_L - mo, made of the last mo bytes of lane L-1's
+// value and the first 16 - mo of its own; lane 0 writes its first 16 - mo
+// bytes and lane 63 its last mo bytes with byte stores.  Every lane of the
+// wave must call it (ds_bpermute).
+template <int F>
+__device__ __forceinline__ void st_shifted(uint8_t* p, u32x4 v) {
+    const uint32_t mo = __builtin_amdgcn_readfirstlane(uint32_t(uintptr_t(p)) & 15u);
+    if (mo == 0) {
+        store16<F>(p, v);
+        return;
+    }
+    const uint32_t lane = threadIdx.x & 63u;
+    const int src = int(((lane + 63u) & 63u) << 2);   // lane - 1
+    const u32x4 prev{uint32_t(__builtin_amdgcn_ds_bpermute(src, int(v.x))),
+                     uint32_t(__builtin_amdgcn_ds_bpermute(src, int(v.y))),
+                     uint32_t(__builtin_amdgcn_ds_bpermute(src, int(v.z))),
+                     uint32_t(__builtin_amdgcn_ds_bpermute(src, int(v.w)))};
+    if (lane != 0) store16<F>(p - mo, funnel16(prev, v, 16u - mo));
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    if (lane == 0) {
+#pragma unroll
+        for (uint32_t b = 0; b < 16; ++b)
+            if (b < 16u - mo) p[b] = uint8_t(w[b >> 2] >> (8 * (b & 3)));
+    } else if (lane == 63) {
+#pragma unroll
+        for (uint32_t b = 0; b < 16; ++b)
+            if (b >= 16u - mo) p[b] = uint8_t(w[b >> 2] >> (8 * (b & 3)));
+    }
+}
+
 template <int MODE, int F>
 __device__ __forceinline__ void st(uint8_t* base, uint64_t col, uint64_t len, u32x4 v) {
     if constexpr (MODE == 0) {
         store16<F>(base + col, v);
+    } else if constexpr (MODE == 3) {
+        st_shifted<F>(base + col, v);
     } else if constexpr (MODE == 1) {
         if (col + 16 <= len) store16<F>(base + col, v);
         else store_bytes(base + col, v, int64_t(len) - int64_t(col));
@@ -343,6 +397,48 @@ __device__ __forceinline__ void do_tile(const ApplyArgs& a, const Ctx& c, const 
                 st<MODE, F>(o, col0 + (uint64_t(u) * TH + tid) * 16, len,
                             u32x4{acc[u][r][0], acc[u][r][1], acc[u][r][2], acc[u][r][3]});
         }
+        return;
+    }
+
+    if constexpr (MODE == 3) {
+        // Misaligned shards: each ring slot holds the two aligned 16-byte
+        // loads that cover the lane's 16 bytes and the shard's misalignment;
+        // the realignment runs when the slot is consumed, so the look-ahead
+        // loads stay in flight as in the aligned ring.  Both loads are 16-byte
+        // aligned and each holds a byte the lane needs (with m == 0 the second
+        // repeats the first), so neither leaves the shard's pages.
+        static_assert(U == 1, "mode 3 tiles are 4 KiB");
+        constexpr int NB = 2;
+        u32x4 rlo[NB], rhi[NB];
+        uint32_t rm[NB];
+        auto load3 = [&](u32x4& lo, u32x4& hi, uint32_t& m, uint32_t t) {
+            const uint32_t tt = t < k ? t : k - 1;
+            const uint8_t* base = ib + in_off<F>(a, c, tt) + col0;
+            m = __builtin_amdgcn_readfirstlane(uint32_t(uintptr_t(base)) & 15u);
+            const uint8_t* q = base - m + uint64_t(tid) * 16;
+            lo = load16<F>(q);
+            hi = load16<F>(q + (m ? 16 : 0));
+        };
+        load3(rlo[0], rhi[0], rm[0], 0);
+        __builtin_amdgcn_sched_barrier(0);
+        for (uint32_t t = 0; t < k; t += NB) {
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+                const int nx = (i + 1) % NB;
+                load3(rlo[nx], rhi[nx], rm[nx], t + i + 1);
+                __builtin_amdgcn_sched_barrier(0);
+                if (t + i < k) {
+                    Tab tb[R];
+                    read_tabs<R, F>(a, c, t + i, tb);
+                    mac<R, F>(acc[0], funnel16(rlo[i], rhi[i], rm[i]), tb);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            st_shifted<F>(ob + out_off<F>(a, c, r) + col0 + uint64_t(tid) * 16,
+                          u32x4{acc[0][r][0], acc[0][r][1], acc[0][r][2], acc[0][r][3]});
         return;
     }
 
@@ -950,6 +1046,7 @@ hipError_t dispatch(const ApplyArgs& a, const Variant& v, int mode, int grid_cap
     switch (mode) {
         case 0: return dispatch_full<R>(a, v, grid_cap, s);
         case 1: return launch_one<R, 1, 1, 0>(a, v, grid_cap, s);
+        case 3: return launch_one<R, 1, 3, kNtLoad | kNtStore | kDepth2>(a, v, grid_cap, s);
         default: return launch_one<R, 1, 2, 0>(a, v, grid_cap, s);
     }
 }

@@ -98,7 +98,9 @@ struct Variant {
 // rows in [1, kMaxRowsPerLaunch].  mode 0: full tiles, every shard base
 // (base + b*bpitch + idx*spitch) 16-byte aligned (variant v); mode 1: one
 // partial tail tile per block (aligned, U = 1); mode 2: any alignment,
-// byte-granular (U = 1; the variant only affects mode 0).
+// byte-granular (U = 1); mode 3: full 4 KiB tiles at any alignment, vector
+// loads and stores realigned in registers (U = 1).  The variant only affects
+// mode 0.
 // grid_cap: -1 one workgroup per tile; 0 balanced persistent grid sized by
 // occupancy; > 0 persistent grid capped at grid_cap.
 // Whether the full-tile kernel for variant v is compiled into the library.

@@ -604,3 +604,48 @@ def test_device_buffer_view_keeps_buffer_alive(gpu):
     assert ref() is None
     with pytest.raises(ValueError):
         shmr_amd.DeviceBuffer(1024, contiguous=False).tensor((2, 1024))
+
+
+# ------------------------------------------------ misaligned (contiguous) layouts
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,p,L,B,off", [
+    (10, 4, 1677722, 3, 0),      # RS(10,4) 16 MiB: the reference's block buffer, shard i at i * S
+    (8, 3, 524288 + 4096 + 5, 4, 3),   # odd pitch and a misaligned base
+    (5, 2, 4096 * 3 + 1, 5, 7),  # 3 full realigned tiles + a 1-byte tail per shard
+    (4, 4, 4096 * 2, 2, 9),      # tile-multiple shards, every base misaligned
+])
+def test_contiguous_layout_realigned(gpu, k, p, L, B, off):
+    """Shards packed at i * L inside each [k+p] * L block buffer (and the batch
+    shifted by `off` bytes) are not 16-byte aligned: full 4 KiB tiles run the
+    realigning vector kernel, the remainder byte-granular.  Encode into the
+    buffer's parity slots, then rebuild two erased shards per block in place,
+    all against the oracle; bytes outside the shards stay untouched."""
+    import torch
+    t = k + p
+    rng = np.random.default_rng(L + B + off)
+    host = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+    flat = torch.full((off + B * t * L + 64,), 0x5A, dtype=torch.uint8, device=gpu)
+    for b in range(B):
+        for i in range(k):
+            s0 = off + (b * t + i) * L
+            flat[s0:s0 + L] = torch.from_numpy(host[b, i]).to(gpu)
+    blocks = flat[off:off + B * t * L].view(B, t, L)
+    rs = shmr_amd.ReedSolomon(k, p)
+    rs.encode_batch_dev(blocks[:, :k], blocks[:, k:], shard_len=L, data_shard_pitch=L, parity_shard_pitch=L)
+    torch.cuda.synchronize()
+    got = blocks.cpu().numpy()
+    for b in range(B):
+        ref = oracle_parity(k, p, [host[b, i].copy() for i in range(k)])
+        for r in range(p):
+            assert np.array_equal(got[b, k + r], ref[r]), ("encode", b, r)
+    full = got.copy()
+    present = np.ones((B, t), np.uint8)
+    for b in range(B):
+        for e in ((b % t), ((b + 3) % t)):
+            present[b, e] = 0
+            blocks[b, e] = 0
+    rs.reconstruct_batch_dev(blocks, present, shard_len=L)
+    torch.cuda.synchronize()
+    assert np.array_equal(blocks.cpu().numpy(), full)
+    edge = flat.cpu().numpy()
+    assert (edge[:off] == 0x5A).all() and (edge[off + B * t * L:] == 0x5A).all(), "wrote outside the batch"
