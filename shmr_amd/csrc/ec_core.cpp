@@ -44,6 +44,10 @@ std::atomic<int> g_mirror_zc{1};
 std::atomic<int> g_ptrs_direct{kPtrsDirectDefault};
 std::atomic<int> g_sync_spin{kSyncSpinDefault};
 std::atomic<int> g_alias_devices{0};   // tools build: alias device IDs (see ec_core.hpp)
+// Misaligned device-resident shards: kAuto = the vector kernels (modes 0 / 1)
+// where the device passed probe_unaligned_vector, else the realigning kernel
+// (mode 3); 0 = always mode 3, 1 = always modes 0 / 1 (tools build only).
+std::atomic<int> g_uvec{kAuto};
 
 // Measured (tools/tune.py, interleaved A/B in one process): a register ring
 // of depth 2 (one shard of loads in flight per wave) beats depth 3 on every
@@ -145,6 +149,15 @@ int set_tuning(const char* key, int value) {
         g_sync_spin = value == kAuto ? kSyncSpinDefault : value;
         return SHMR_EC_OK;
     }
+    if (k == "uvec") {   // not per op class; kAuto only in the product build
+#ifdef SHMR_EC_TOOLS
+        if (value != kAuto && value != 0 && value != 1) return SHMR_EC_INVALID_ARGUMENT;
+        g_uvec = value;
+        return SHMR_EC_OK;
+#else
+        return value == kAuto ? SHMR_EC_OK : SHMR_EC_INVALID_ARGUMENT;
+#endif
+    }
     if (k == "alias_devices") {   // not per op class; tools build only (see ec_core.hpp)
         const int v = value == kAuto ? 0 : value;
 #ifdef SHMR_EC_TOOLS
@@ -228,6 +241,7 @@ int get_tuning(const char* key) {
     if (k == "ptrs_direct") return g_ptrs_direct;
     if (k == "sync_spin_us") return g_sync_spin;
     if (k == "alias_devices") return g_alias_devices;
+    if (k == "uvec") return g_uvec;
     if (k == "chunks") return T.u;
     if (k == "nt_load") return T.nt_load;
     if (k == "nt_store") return T.nt_store;
@@ -272,6 +286,23 @@ kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_m
 }
 
 int grid_mode(OpClass op) { return g_tune[op].grid.load(); }
+
+// Whether misaligned device-resident shards may take the vector kernels: the
+// knob, or (auto) the device's probe result, run once per physical device.
+bool unaligned_vector(int dev) {
+    const int knob = g_uvec.load();
+    if (knob != kAuto) return knob != 0;
+    static std::mutex mu;
+    static auto* verdict = new std::map<int, bool>;   // leaked: outlives static teardown
+    std::lock_guard<std::mutex> lock(mu);
+    const int phys = physical_device(dev);
+    auto it = verdict->find(phys);
+    if (it != verdict->end()) return it->second;
+    bool ok = false;
+    if (kern::probe_unaligned_vector(&ok) != hipSuccess) ok = false;
+    (*verdict)[phys] = ok;
+    return ok;
+}
 
 uint64_t bounce_limit() { return uint64_t(g_bounce_kib.load()) << 10; }
 
@@ -386,7 +417,10 @@ int plan_on_device(Plan& plan, int dev, const uint8_t** out) {
 // Launch sets.  Rows go in groups of <= 4 per launch; each group is one
 // full-tile launch (the tuned variant) plus, when len is not a multiple of the
 // tile, one launch over the remaining U=1 tiles (the last partial, byte-exact
-// bounds).  Unaligned layouts take the byte-granular kernel.
+// bounds).  Misaligned device-resident layouts take the same kernels where
+// the device serves unaligned vector access (unaligned_vector), else the
+// realigning kernel for full 4 KiB tiles plus the byte-granular one for the
+// rest; misaligned mapped host shards take the byte-granular kernel.
 // ===========================================================================
 int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_t len, hipStream_t stream,
                OpClass op) {
@@ -404,10 +438,16 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
     kern::Variant tail;   // tail / unaligned launches: U = 1, plain loads
     const int cap = grid_mode(op);
     const bool ptrs = L.d_ptrs != nullptr;
+    // Misaligned device-resident shards (the reference's contiguous block
+    // buffer, shard i at i * S) take the same vector kernels as aligned ones
+    // where the device serves unaligned 16-byte accesses (verified once per
+    // device; every access still covers only the lane's own bytes), else the
+    // realigning kernel below.
     const bool aligned = ptrs ? L.ptrs_aligned
-                              : aligned16(uintptr_t(L.in_base)) && aligned16(uintptr_t(L.out_base)) &&
-                                    aligned16(L.in_bpitch) && aligned16(L.in_spitch) && aligned16(L.out_bpitch) &&
-                                    aligned16(L.out_spitch);
+                              : (aligned16(uintptr_t(L.in_base)) && aligned16(uintptr_t(L.out_base)) &&
+                                 aligned16(L.in_bpitch) && aligned16(L.in_spitch) && aligned16(L.out_bpitch) &&
+                                 aligned16(L.out_spitch)) ||
+                                    unaligned_vector(dev);
     for (uint32_t row0 = 0; row0 < plan.m; row0 += kern::kMaxRowsPerLaunch) {
         const uint32_t rows = std::min<uint32_t>(kern::kMaxRowsPerLaunch, plan.m - row0);
         count_device(dev, kDevLaunches);

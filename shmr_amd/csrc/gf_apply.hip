@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstring>
 
 #include "gf_apply.hpp"
 
@@ -1060,6 +1061,45 @@ bool variant_compiled(const Variant& v) {
     SHMR_VARIANTS(SHMR_F)
 #undef SHMR_F
     return false;
+}
+
+namespace {
+// 16-byte vector loads and stores at addresses off 16-byte alignment, with the
+// plain and the nontemporal instructions the kernels use (see
+// probe_unaligned_vector).  Lane-dependent addresses keep them vector memory
+// instructions (a wave-uniform address from a read-only pointer may become a
+// scalar load, which ignores the low address bits).
+constexpr int kProbeLanes = 64, kProbeBytes = kProbeLanes * 16 + 64;
+__global__ void unaligned_probe_kernel(const uint8_t* in, uint8_t* out) {
+    const uint32_t l = threadIdx.x;
+    store16<0>(out + 5 + 16 * l, load16<0>(in + 3 + 16 * l));
+    store16<kNtStore>(out + kProbeBytes + 7 + 16 * l, load16<kNtLoad>(in + kProbeBytes + 9 + 16 * l));
+}
+}  // namespace
+
+hipError_t probe_unaligned_vector(bool* ok) {
+    *ok = false;
+    constexpr int N = 2 * kProbeBytes;
+    uint8_t h_in[N], h_out[N], want[N];
+    for (int i = 0; i < N; ++i) h_in[i] = uint8_t(i * 37 + 11), want[i] = 0xA5;
+    for (int i = 0; i < kProbeLanes * 16; ++i) {
+        want[5 + i] = h_in[3 + i];
+        want[kProbeBytes + 7 + i] = h_in[kProbeBytes + 9 + i];
+    }
+    uint8_t *d_in = nullptr, *d_out = nullptr;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&d_in), N);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d_out), N);
+    if (e == hipSuccess) e = hipMemcpy(d_in, h_in, N, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(d_out, 0xA5, N);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(unaligned_probe_kernel, dim3(1), dim3(kProbeLanes), 0, nullptr, d_in, d_out);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(h_out, d_out, N, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) *ok = std::memcmp(h_out, want, N) == 0;
+    if (d_in) (void)hipFree(d_in);
+    if (d_out) (void)hipFree(d_out);
+    return e;
 }
 
 hipError_t launch_apply(const ApplyArgs& a, unsigned rows, const Variant& v, int mode, int grid_cap,

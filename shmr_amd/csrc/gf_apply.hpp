@@ -100,7 +100,8 @@ struct Variant {
 // partial tail tile per block (aligned, U = 1); mode 2: any alignment,
 // byte-granular (U = 1); mode 3: full 4 KiB tiles at any alignment, vector
 // loads and stores realigned in registers (U = 1).  The variant only affects
-// mode 0.
+// mode 0.  Modes 0 and 1 also run on misaligned shards where the device's
+// unaligned vector access was verified (probe_unaligned_vector).
 // grid_cap: -1 one workgroup per tile; 0 balanced persistent grid sized by
 // occupancy; > 0 persistent grid capped at grid_cap.
 // Whether the full-tile kernel for variant v is compiled into the library.
@@ -108,6 +109,12 @@ bool variant_compiled(const Variant& v);
 
 hipError_t launch_apply(const ApplyArgs& a, unsigned rows, const Variant& v, int mode, int grid_cap,
                         hipStream_t stream);
+
+// Runs a one-lane kernel on the current device that loads and stores 16 bytes
+// at addresses off 16-byte alignment (plain and nontemporal) and sets *ok if
+// the bytes arrived where they belong: the memory system's unaligned access
+// mode serves the vector kernels on misaligned shards (ec_core launch_set).
+hipError_t probe_unaligned_vector(bool* ok);
 
 }  // namespace kern
 }  // namespace shmr

@@ -608,18 +608,34 @@ def test_device_buffer_view_keeps_buffer_alive(gpu):
 
 # ------------------------------------------------ misaligned (contiguous) layouts
 @pytest.mark.gpu
+@pytest.mark.parametrize("path", ["auto", "realign", "vector"])
 @pytest.mark.parametrize("k,p,L,B,off", [
     (10, 4, 1677722, 3, 0),      # RS(10,4) 16 MiB: the reference's block buffer, shard i at i * S
     (8, 3, 524288 + 4096 + 5, 4, 3),   # odd pitch and a misaligned base
-    (5, 2, 4096 * 3 + 1, 5, 7),  # 3 full realigned tiles + a 1-byte tail per shard
+    (5, 2, 4096 * 3 + 1, 5, 7),  # 3 full tiles + a 1-byte tail per shard
     (4, 4, 4096 * 2, 2, 9),      # tile-multiple shards, every base misaligned
+    (10, 4, 8192 * 3 + 2458, 2, 1),   # 4-row encode policy (8 KiB tiles, fused tails) off alignment
 ])
-def test_contiguous_layout_realigned(gpu, k, p, L, B, off):
+def test_contiguous_layout_realigned(gpu, path, k, p, L, B, off):
     """Shards packed at i * L inside each [k+p] * L block buffer (and the batch
-    shifted by `off` bytes) are not 16-byte aligned: full 4 KiB tiles run the
-    realigning vector kernel, the remainder byte-granular.  Encode into the
-    buffer's parity slots, then rebuild two erased shards per block in place,
-    all against the oracle; bytes outside the shards stay untouched."""
+    shifted by `off` bytes) are not 16-byte aligned.  "auto": the product
+    policy (the vector kernels on a device that passed the unaligned-access
+    probe); tools build "realign" (knob uvec=0): the realigning kernel for full
+    4 KiB tiles, the remainder byte-granular; "vector" (uvec=1): the vector
+    kernels unconditionally.  Encode into the buffer's parity slots, then
+    rebuild two erased shards per block in place, all against the oracle;
+    bytes outside the shards stay untouched."""
+    if path == "auto":
+        return _contiguous_layout_check(gpu, k, p, L, B, off)
+    with _native.tools():
+        shmr_amd.set_tuning(uvec=0 if path == "realign" else 1)
+        try:
+            _contiguous_layout_check(gpu, k, p, L, B, off)
+        finally:
+            shmr_amd.set_tuning(uvec=-2)
+
+
+def _contiguous_layout_check(gpu, k, p, L, B, off):
     import torch
     t = k + p
     rng = np.random.default_rng(L + B + off)
