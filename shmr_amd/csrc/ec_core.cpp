@@ -299,7 +299,12 @@ bool unaligned_vector(int dev) {
     auto it = verdict->find(phys);
     if (it != verdict->end()) return it->second;
     bool ok = false;
-    if (kern::probe_unaligned_vector(&ok) != hipSuccess) ok = false;
+    // A probe that could not run (e.g. inside a stream capture) decides only
+    // this launch (realigning kernel) and is tried again on the next one.
+    if (kern::probe_unaligned_vector(&ok) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
     (*verdict)[phys] = ok;
     return ok;
 }

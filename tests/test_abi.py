@@ -190,10 +190,10 @@ def test_tuning_api():
     assert _native.lib().shmr_ec_is_tools_build() == 0
     assert b"product" in _native.lib().shmr_ec_version()
     for key, default in (("encode.chunks", -2), ("chunks", -2), ("grid", -1), ("threads", 256), ("diag", 0),
-                         ("decode.depth", -2), ("occ8", 0)):
+                         ("decode.depth", -2), ("occ8", 0), ("uvec", -2)):
         shmr_amd.set_tuning(**{key: default})
     for key, value in (("encode.chunks", 2), ("diag", 1), ("decode.diag", 1), ("depth", 3), ("grid", 0),
-                       ("threads", 512), ("spre", 1), ("occ8", 1)):
+                       ("threads", 512), ("spre", 1), ("occ8", 1), ("uvec", 0), ("uvec", 1)):
         with pytest.raises(shmr_amd.Error) as e:
             shmr_amd.set_tuning(**{key: value})
         assert e.value.name == "InvalidArgument", key
