@@ -75,7 +75,8 @@ def parse():
                          "reference fans blocks out with rayon, mod.rs:93-96)")
     ap.add_argument("--pitch-align", type=int, default=4096,
                     help="device shard pitch = S rounded up to this many bytes (DESIGN.md section 4: 4 KiB "
-                         "measured +0.7-1.0 point of HBM peak over 256 B for RS(10,4)'s S = 1,677,722)")
+                         "measured +0.7-1.0 point of HBM peak over 256 B for RS(10,4)'s S = 1,677,722); 1 = the "
+                         "reference's packing, shard i at i * S (off 16-byte alignment for RS(10,4))")
     ap.add_argument("--pitch-pad", type=int, default=-1,
                     help="bytes added to every shard slot after alignment; -1 (auto): one 4 KiB page when the "
                          "aligned pitch is a multiple of 64 KiB (power-of-two shard sizes: RS(8,3) 4 MiB, RS(4,2) "
@@ -221,7 +222,7 @@ def run(args):
     # block buffer, whose 2^19 shard stride measured 1.8 points of HBM peak
     # slower; S = 1,677,722 (RS(10,4) 16 MiB) gets the
     # page-aligned 1,679,360-byte slots (0.1 %) and no page.
-    a = max(16, args.pitch_align)
+    a = max(1, args.pitch_align)          # 1: pitch = S, the reference's packing (any alignment)
     pitch = (S + a - 1) // a * a
     pitch += (4096 if pitch % 65536 == 0 else 0) if args.pitch_pad < 0 else args.pitch_pad
     g = torch.Generator(device=dev)
@@ -364,6 +365,9 @@ def run(args):
         "cpu_baseline": None,
     }
     traffic, source = load_traffic(args.config, B, out["library"]["build_id"], tuning)
+    if (args.pitch_align, args.pitch_pad) != (4096, -1):
+        # the PMC records were taken on the default shard slots
+        traffic, source = None, dict(source, status="not profiled: non-default shard layout")
     out["roofline"]["traffic"] = traffic
     out["roofline"]["traffic_source"] = source
     if codec:
