@@ -226,7 +226,7 @@ int shmr_ec_set_device(shmr_ec_t* rs, int device);
  * a kernel knob can only be set to its default (anything else returns
  * SHMR_EC_INVALID_ARGUMENT); the tools build (libshmr_ec_tools.so) takes:
  * "chunks" (16-B chunks per lane per tile: 1, 2, 4), "nt_load", "nt_store"
- * (nontemporal 0/1), "scalar_tabs" (0/1), "occ8" (0/1), "grid" (-1 one
+ * (nontemporal 0/1), "occ8" (0/1), "grid" (-1 one
  * workgroup per tile, 0 balanced persistent grid, >0 capped persistent
  * grid), "threads" (lanes per workgroup: 128, 256, 512), "depth" (register
  * ring depth = shards of loads in flight + 1: 1, 2, 3, 5, 9), "wgs_per_cu"

@@ -171,9 +171,9 @@ int shmr_ec_describe_variant(int decode, uint32_t data_shards, uint32_t rows, ch
     lean.fuse_tail = false;
     const bool compiled = shmr::kern::variant_compiled(lean) && (!v.fuse_tail || shmr::kern::variant_compiled(v));
     std::snprintf(buf, len,
-                  "chunks=%d nt_load=%d nt_store=%d scalar_tabs=%d occ8=%d threads=%d grid=%d diag=%d depth=%d "
+                  "chunks=%d nt_load=%d nt_store=%d occ8=%d threads=%d grid=%d diag=%d depth=%d "
                   "wgs_per_cu=%d occ=%d early=%d spre=%d fuse_tail=%d compiled=%d",
-                  v.u, int(v.nt_load), int(v.nt_store), int(v.scalar_tabs), int(v.occ8), v.threads,
+                  v.u, int(v.nt_load), int(v.nt_store), int(v.occ8), v.threads,
                   core::grid_mode(op), int(v.diag), v.depth, v.wgs_per_cu, v.occ, int(v.early), int(v.spre), int(v.fuse_tail),
                   int(compiled));
     // appended only when set: records keyed by the string stay valid

@@ -24,7 +24,6 @@ struct Tuning {
     std::atomic<int> u{kAuto};
     std::atomic<int> nt_load{kAuto};
     std::atomic<int> nt_store{kAuto};
-    std::atomic<int> scalar_tabs{0};
     std::atomic<int> occ8{0};
     std::atomic<int> grid{-1};     // -1: one workgroup per tile
     std::atomic<int> diag{0};
@@ -176,7 +175,7 @@ int set_tuning(const char* key, int value) {
     // In particular "diag" (XOR-only, wrong results) is refused.
     {
         static const std::map<std::string, int> kDefaults = {
-            {"chunks", kAuto}, {"nt_load", kAuto}, {"nt_store", kAuto}, {"scalar_tabs", 0}, {"occ8", 0},
+            {"chunks", kAuto}, {"nt_load", kAuto}, {"nt_store", kAuto}, {"occ8", 0},
             {"grid", -1},      {"diag", 0},        {"threads", 256},    {"depth", kAuto},   {"wgs_per_cu", kAuto},
             {"occ", kAuto},    {"early", kAuto},   {"spre", kAuto},     {"fuse_tail", kAuto},
             {"glds", kAuto},   {"serial", kAuto}};
@@ -193,8 +192,6 @@ int set_tuning(const char* key, int value) {
             T.nt_load = value == kAuto ? kAuto : (value != 0);
         } else if (k == "nt_store") {
             T.nt_store = value == kAuto ? kAuto : (value != 0);
-        } else if (k == "scalar_tabs") {
-            T.scalar_tabs = value != 0;
         } else if (k == "occ8") {
             T.occ8 = value != 0;
         } else if (k == "grid") {
@@ -245,7 +242,6 @@ int get_tuning(const char* key) {
     if (k == "chunks") return T.u;
     if (k == "nt_load") return T.nt_load;
     if (k == "nt_store") return T.nt_store;
-    if (k == "scalar_tabs") return T.scalar_tabs;
     if (k == "occ8") return T.occ8;
     if (k == "grid") return T.grid;
     if (k == "diag") return T.diag;
@@ -267,7 +263,6 @@ kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_m
     if (T.u.load() != kAuto) v.u = T.u.load();
     if (T.nt_load.load() != kAuto) v.nt_load = T.nt_load.load() != 0;
     if (T.nt_store.load() != kAuto) v.nt_store = T.nt_store.load() != 0;
-    v.scalar_tabs = T.scalar_tabs.load() != 0;
     v.occ8 = T.occ8.load() != 0;
 #ifdef SHMR_EC_TOOLS
     v.diag = T.diag.load() != 0;
@@ -281,7 +276,7 @@ kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_m
     if (T.fuse_tail.load() != kAuto) v.fuse_tail = T.fuse_tail.load() != 0;
     if (T.glds.load() != kAuto) v.glds = T.glds.load() != 0;
     if (T.serial.load() != kAuto) v.serial = T.serial.load() != 0;
-    if (v.glds) v.early = v.spre = v.scalar_tabs = false;   // the LDS-DMA ring is a form of the plain tile
+    if (v.glds) v.early = v.spre = false;   // the LDS-DMA ring is a form of the plain tile
     return v;
 }
 
@@ -332,7 +327,7 @@ kern::Variant launch_variant(OpClass op, unsigned k, unsigned rows, bool host_ma
     v.ptrs = ptrs;
     v.segs = segs;
     if (ptrs) {
-        v.early = v.spre = v.scalar_tabs = v.glds = false;   // only the plain LDS-staged tile reads pointer tables
+        v.early = v.spre = v.glds = false;   // only the plain LDS-staged tile reads pointer tables
         if (g_tune[op].serial.load() == kAuto) v.serial = false;   // the policy's serial goes with early
         kern::Variant lean = v;
         lean.fuse_tail = false;

@@ -59,7 +59,7 @@ struct ApplyArgs {
     // are then 0): shard i of block b is at address shard_ptrs[b * total + i]
     // -- e.g. Block-Cache buffers in mapped (pinned) host memory, which the
     // kernel reads and writes across PCIe without a staging copy.  Only the
-    // plain LDS-staged tile supports it (no early / spre / scalar_tabs).
+    // plain LDS-staged tile supports it (no early / spre).
     const uint64_t* shard_ptrs;
     uint32_t total;
     // Fused tails (kernels compiled with the fused-tail flag): the first
@@ -74,12 +74,12 @@ struct ApplyArgs {
     Seg segs[kMaxSegs];
 };
 
-// Compiled-in kernel variant for full tiles (see gf_apply.hip dispatch_full).
+// Compiled-in kernel variant for full tiles (see gf_apply.hip dispatch_full;
+// measurement-only variants: gf_apply_tools.hip, tools build).
 struct Variant {
     int u = 1;               // 16-byte chunks per lane per shard (1, 2, 4)
     bool nt_load = false;    // nontemporal loads
     bool nt_store = false;   // nontemporal stores
-    bool scalar_tabs = false;// coefficient tables via scalar loads instead of LDS
     bool occ8 = false;       // __launch_bounds__ for 8 waves / SIMD
     bool diag = false;       // diagnostics: XOR-only (wrong results)
     int threads = kThreads;  // lanes per workgroup (128, 256, 512)
@@ -93,6 +93,7 @@ struct Variant {
     bool segs = false;       // full-tile kernel that takes segment launches (set by launch_set)
     bool glds = false;       // input ring in LDS filled by LDS-DMA (depth = slots; full tiles only)
     bool serial = false;     // GF math one dword at a time (fewer live registers, more waves)
+    bool sc1_store = false;  // stores with the sc1 cache policy instead of nontemporal
 };
 
 // rows in [1, kMaxRowsPerLaunch].  mode 0: full tiles, every shard base
@@ -109,6 +110,14 @@ bool variant_compiled(const Variant& v);
 
 hipError_t launch_apply(const ApplyArgs& a, unsigned rows, const Variant& v, int mode, int grid_cap,
                         hipStream_t stream);
+
+#ifdef SHMR_EC_TOOLS
+// Full-tile measurement variants (gf_apply_tools.hip, tools build only):
+// launch_apply / variant_compiled fall through to these for variants the
+// product list does not carry.
+hipError_t launch_full_tools(const ApplyArgs& a, unsigned rows, const Variant& v, int grid_cap, hipStream_t stream);
+bool variant_compiled_tools(const Variant& v);
+#endif
 
 // Runs a one-lane kernel on the current device that loads and stores 16 bytes
 // at addresses off 16-byte alignment (plain and nontemporal) and sets *ok if

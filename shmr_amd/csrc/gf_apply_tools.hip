@@ -1,0 +1,288 @@
+// Measurement-only variants of the gfx950 GF(2^8) matrix-apply kernel,
+// linked into the tools build (libshmr_ec_tools.so, -DSHMR_EC_TOOLS) only.
+// Each was measured against the product policy ("Kernel
+// decisions at a glance") and kept as the record of that measurement:
+//  * the LDS-DMA input ring (glds_tile): -1.2 to -9.6 points;
+//  * scalar-loaded tables and offsets, no LDS (spre_tile): -1.0 to -6.5;
+//  * the XOR-only diagnostic twin (diag_mac; WRONG results by design), the
+//    ceiling of the kernel's own access pattern;
+//  * ring depths 1/3/5/9, 128/512-lane workgroups, occupancy targets and the
+//    other knob combinations of the instantiation list below.
+#include <hip/hip_runtime.h>
+
+#include "gf_tile.hpp"
+
+namespace shmr {
+namespace kern {
+
+namespace {
+
+template <int R>
+__device__ __forceinline__ void diag_mac(uint32_t (&acc)[R][4], const u32x4& d, const Tab (&tb)[R]) {
+    const uint32_t w[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r][j] ^= w[j] + tb[r].t2;
+}
+
+// LDS ring: slot s holds shard (t mod NB)'s U x 16 B per lane, lane-linear per
+// wave (LDS-DMA writes wave base + lane * 16).  Each lane reads back only the
+// bytes its own wave's DMA wrote, so the covering vmcnt orders the ds_read (no
+// barrier); the slot a DMA refills was last read one step earlier, and those
+// reads have returned (their values were used).
+template <int R, int U, int F>
+__device__ __forceinline__ void glds_tile(const ApplyArgs& a, const Ctx& c, const uint8_t* ib, uint8_t* ob, uint64_t col0) {
+    constexpr int TH = threads_of<F>();
+    constexpr int NB = depth_of<F>();
+    constexpr int AUX = (F & kNtLoad) ? 2 : 0;   // nt
+    const uint32_t k = a.k;
+    const uint64_t len = a.len;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t wave_base = (tid & ~63u) * 16;
+    uint32_t acc[U][R][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[u][r][j] = 0u;
+    auto gload = [&](int slot, uint32_t t) {
+        const uint32_t tt = t < k ? t : k - 1;
+        const uint8_t* base = ib + c.s_in_off[tt] + col0 + uint64_t(tid) * 16;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            __builtin_amdgcn_global_load_lds(
+                (__attribute__((address_space(1))) void*)(uintptr_t)(base + uint64_t(u) * TH * 16),
+                (__attribute__((address_space(3))) void*)(c.ring + (slot * U + u) * TH * 16 + wave_base), 16, 0, AUX);
+    };
+    auto consume_lds = [&](int slot, uint32_t t) {
+        Tab tb[R];
+        read_tabs<R>(c, t, tb);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(c.ring + ((slot * U + u) * TH + tid) * 16);
+            mac<R, F>(acc[u], v, tb);
+        }
+    };
+    // vmcnt(N) with expcnt / lgkmcnt left alone (gfx9 encoding)
+    constexpr int VM = (NB - 1) * U;
+    constexpr int WAIT = (VM & 15) | ((VM >> 4) << 14) | (7 << 4) | (15 << 8);
+#pragma unroll
+    for (int i = 0; i < NB - 1; ++i) gload(i, i);
+    __builtin_amdgcn_sched_barrier(0);
+    for (uint32_t t = 0; t < k; t += NB) {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            gload((i + NB - 1) % NB, t + i + NB - 1);
+            __builtin_amdgcn_s_waitcnt(WAIT);   // shard t+i has landed in slot i
+            __builtin_amdgcn_sched_barrier(0);
+            if (t + i < k) consume_lds(i, t + i);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): no DMA into LDS outlives the tile
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        uint8_t* o = ob + c.s_out_off[r];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            st<0, F>(o, col0 + (uint64_t(u) * TH + tid) * 16, len,
+                     u32x4{acc[u][r][0], acc[u][r][1], acc[u][r][2], acc[u][r][3]});
+    }
+}
+
+// ---- scalar-table tile (flag kSPre) --------------------------------------
+// No LDS: shard offsets (in_idx) and the coefficient tables are wave-uniform,
+// so they come from the plan image by scalar loads (constant address space)
+// into SGPRs; only the table words v_perm cannot take from an SGPR are copied
+// to VGPRs.  Per step: issue the data load for shard t+NB-1 (its offset was
+// fetched during the previous step), the scalar loads of shard t's tables and
+// of the next offset, then multiply shard t.
+template <int R>
+__device__ __forceinline__ void s_tabs(const ApplyArgs& a, const uint8_t* plan, uint32_t t, Tab (&tb)[R]) {
+    const cu32* e0 = as_const<cu32>(plan + a.tab_off) + (size_t(t) * a.m + a.row0) * 8;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const cu32* e = e0 + r * 8;
+        tb[r] = Tab{e[0], e[1], e[2], e[3], e[4]};
+    }
+}
+
+template <int R, int U, int MODE, int F, bool IDENT>
+__device__ __forceinline__ void spre_tile(const ApplyArgs& a, const uint8_t* plan, const uint8_t* ib, uint8_t* ob, uint64_t col0) {
+    constexpr int TH = threads_of<F>();
+    constexpr int NB = depth_of<F>();
+    const uint32_t k = a.k;
+    const uint64_t len = a.len;
+    const uint32_t tid = threadIdx.x;
+    const uint16_t* in_idx = reinterpret_cast<const uint16_t*>(plan + 8);
+    auto in_off = [&](uint32_t t) {
+        const uint32_t tt = t < k ? t : k - 1;
+        if constexpr (IDENT) return uint64_t(tt) * a.in_spitch;   // pure scalar arithmetic
+        else return uint64_t(plan_u16(in_idx, tt)) * a.in_spitch;
+    };
+    uint32_t acc[U][R][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[u][r][j] = 0u;
+    auto load = [&](u32x4 (&buf)[U], uint64_t off) {
+        const uint8_t* base = ib + off;
+#pragma unroll
+        for (int u = 0; u < U; ++u) buf[u] = ld<MODE, F>(base, col0 + (uint64_t(u) * TH + tid) * 16, len);
+    };
+    u32x4 ring[NB][U];
+#pragma unroll
+    for (int i = 0; i < NB - 1; ++i) load(ring[i], in_off(i));
+    uint64_t next_off = in_off(NB - 1);
+    __builtin_amdgcn_sched_barrier(0);
+    for (uint32_t t = 0; t < k; t += NB) {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            load(ring[(i + NB - 1) % NB], next_off);   // shard t+i+NB-1
+            __builtin_amdgcn_sched_barrier(0);
+            next_off = in_off(t + i + NB);
+            // Unconditional multiply (a branch here lets the compiler sink
+            // the look-ahead load into it, collapsing the ring): past the
+            // last shard the tables are zeroed, so the product is 0.
+            {
+                const bool live = t + i < k;
+                Tab tb[R];
+                s_tabs<R>(a, plan, live ? t + i : k - 1, tb);
+                const uint32_t msk = live ? ~0u : 0u;
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    tb[r] = Tab{tb[r].t0lo & msk, tb[r].t0hi & msk, tb[r].t1lo & msk, tb[r].t1hi & msk, tb[r].t2 & msk};
+#pragma unroll
+                for (int u = 0; u < U; ++u) mac<R, F>(acc[u], ring[i][u], tb);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        uint8_t* o = ob + uint64_t(plan_u16(in_idx, k + a.row0 + r) - a.out_bias) * a.out_spitch;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            st<MODE, F>(o, col0 + (uint64_t(u) * TH + tid) * 16, len,
+                        u32x4{acc[u][r][0], acc[u][r][1], acc[u][r][2], acc[u][r][3]});
+    }
+}
+
+#define SHMR_VARIANTS_TOOLS(X) \
+    X(1, 0) \
+    X(1, kNtLoad) \
+    X(1, kNtStore) \
+    X(1, kNtLoad | kNtStore) \
+    X(1, kOcc8 | kNtLoad | kNtStore) \
+    X(1, kDiagXor) \
+    X(1, kDiagXor | kNtLoad | kNtStore) \
+    X(2, 0) \
+    X(2, kNtLoad | kNtStore) \
+    X(4, kNtLoad | kNtStore) \
+    X(1, kNtLoad | kNtStore | kTh128) \
+    X(1, kNtLoad | kNtStore | kTh512) \
+    X(1, kNtStore | kTh512) \
+    X(2, kNtLoad | kNtStore | kTh128) \
+    X(1, kNtLoad | kNtStore | kDepth5) \
+    X(1, kNtLoad | kNtStore | kDepth9) \
+    X(1, kNtLoad | kDepth5) \
+    X(1, kNtLoad | kDepth9) \
+    X(1, kNtLoad | kNtStore | kDepth1) \
+    X(1, kNtLoad | kDepth2) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kTh512) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kTh128) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kOcc8) \
+    X(1, kNtLoad | kNtStore | kDepth2 | (6 << kOccShift)) \
+    X(1, kNtLoad | kNtStore | kDepth2 | (7 << kOccShift)) \
+    X(1, kNtLoad | kNtStore | (6 << kOccShift)) \
+    X(1, kNtLoad | kNtStore | (7 << kOccShift)) \
+    X(2, kNtLoad | kNtStore | kDepth2 | (6 << kOccShift)) \
+    X(1, kNtLoad | kNtStore | kEarly) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | (6 << kOccShift)) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSPre) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSPre) \
+    X(1, kNtLoad | kNtStore | kSPre) \
+    X(1, kNtLoad | kNtStore | kSegs) \
+    X(1, kNtLoad | kNtStore | kSegs | kFuse) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kTh512) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kTh128) \
+    X(2, kNtLoad | kNtStore | kFuse) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kTh128) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kFuse | kTh512) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSerial) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSerial) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kFuse | kSerial) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kSerial) \
+    X(1, kNtLoad | kNtStore | kSerial) \
+    X(1, kNtLoad | kNtStore | kFuse | kSerial) \
+    X(1, kNtLoad | kNtStore | kDepth5 | kSerial) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kSerial) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kSerial) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial | (5 << kOccShift)) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | (5 << kOccShift)) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | (5 << kOccShift)) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kEarly) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kEarly) \
+    X(1, kDiagXor | kNtLoad | kNtStore | kDepth2) \
+    X(2, kDiagXor | kNtLoad | kNtStore | kDepth2) \
+    X(1, kDiagXor | kNtLoad | kNtStore | kDepth2 | kFuse) \
+    X(2, kDiagXor | kNtLoad | kNtStore | kDepth2 | kFuse) \
+    X(1, kDiagXor | kNtLoad | kNtStore | kDepth2 | kSegs) \
+    X(1, kNtLoad | kNtStore | kGlds) \
+    X(1, kNtLoad | kNtStore | kGlds | kDepth5) \
+    X(1, kNtLoad | kNtStore | kGlds | kDepth9) \
+    X(2, kNtLoad | kNtStore | kGlds) \
+    X(2, kNtLoad | kNtStore | kGlds | kDepth5) \
+    X(1, kNtLoad | kNtStore | kGlds | kFuse) \
+    X(1, kNtLoad | kNtStore | kGlds | kDepth5 | kFuse) \
+    X(1, kNtLoad | kNtStore | kGlds | kDepth9 | kFuse) \
+    X(2, kNtLoad | kNtStore | kGlds | kFuse) \
+    X(2, kNtLoad | kNtStore | kGlds | kDepth5 | kFuse) \
+    X(1, kNtLoad | kNtStore | kGlds | kSegs) \
+    X(1, kNtLoad | kNtStore | kGlds | kDepth5 | kSegs) \
+    X(1, kNtLoad | kNtStore | kGlds | kSegs | kFuse) \
+    X(1, kNtLoad | kNtStore | kGlds | kDepth5 | kSegs | kFuse) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSPre | kFuse) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSPre | kFuse | kSerial) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSPre | kFuse) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSPre | kFuse | kSerial)
+
+template <int R>
+hipError_t dispatch_tools(const ApplyArgs& a, const Variant& v, int grid_cap, hipStream_t s) {
+    const int f = variant_flags(v);
+#define SHMR_F(UU, FL) \
+    if (v.u == UU && f == (FL)) return launch_one<R, UU, 0, FL>(a, v, grid_cap, s);
+    SHMR_VARIANTS_TOOLS(SHMR_F)
+#undef SHMR_F
+    return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+hipError_t launch_full_tools(const ApplyArgs& a, unsigned rows, const Variant& v, int grid_cap, hipStream_t stream) {
+    switch (rows) {
+        case 1: return dispatch_tools<1>(a, v, grid_cap, stream);
+        case 2: return dispatch_tools<2>(a, v, grid_cap, stream);
+        case 3: return dispatch_tools<3>(a, v, grid_cap, stream);
+        case 4: return dispatch_tools<4>(a, v, grid_cap, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+bool variant_compiled_tools(const Variant& v) {
+    const int f = variant_flags(v);
+#define SHMR_F(UU, FL) \
+    if (v.u == UU && f == (FL)) return true;
+    SHMR_VARIANTS_TOOLS(SHMR_F)
+#undef SHMR_F
+    return false;
+}
+
+}  // namespace kern
+}  // namespace shmr

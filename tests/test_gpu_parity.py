@@ -130,7 +130,7 @@ def test_reconstruct_all_patterns_10_4(gpu):
 
 
 # --------------------------------------------------------------- device batch API
-KNOBS = ("chunks", "nt_load", "nt_store", "scalar_tabs", "occ8", "grid", "threads", "depth", "wgs_per_cu", "occ", "early", "spre",
+KNOBS = ("chunks", "nt_load", "nt_store", "occ8", "grid", "threads", "depth", "wgs_per_cu", "occ", "early", "spre",
          "fuse_tail", "glds", "serial")
 
 
@@ -174,11 +174,11 @@ def test_encode_batch_dev(gpu, k, p, L, B):
     _dev_encode_check(gpu, k, p, L, B, pitch=(L + 255) // 256 * 256)
 
 
-BASE = dict(chunks=1, nt_load=0, nt_store=0, scalar_tabs=0, occ8=0, grid=-1, threads=256, depth=3, wgs_per_cu=0, occ=0, early=0, spre=0,
+BASE = dict(chunks=1, nt_load=0, nt_store=0, occ8=0, grid=-1, threads=256, depth=3, wgs_per_cu=0, occ=0, early=0, spre=0,
             fuse_tail=0, glds=0, serial=0)
 VARIANTS = [dict(BASE, **v) for v in (
     {}, dict(nt_load=1), dict(nt_store=1), dict(nt_load=1, nt_store=1),
-    dict(scalar_tabs=1, nt_load=1, nt_store=1), dict(occ8=1, nt_load=1, nt_store=1),
+    dict(occ8=1, nt_load=1, nt_store=1),
     dict(chunks=2), dict(chunks=2, nt_load=1, nt_store=1), dict(chunks=4, nt_load=1, nt_store=1),
     dict(grid=0), dict(chunks=2, grid=0), dict(chunks=4, grid=7, nt_load=1, nt_store=1),
     dict(nt_load=1, nt_store=1, threads=128), dict(nt_load=1, nt_store=1, threads=512),

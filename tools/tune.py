@@ -40,7 +40,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--variants", default="chunks=1;nt_load=1;nt_store=1;nt_load=1,nt_store=1;"
-                    "scalar_tabs=1,nt_load=1,nt_store=1;occ8=1,nt_load=1,nt_store=1;chunks=2;"
+                    "occ8=1,nt_load=1,nt_store=1;chunks=2;"
                     "chunks=2,nt_load=1,nt_store=1;chunks=4,nt_load=1,nt_store=1;grid=0;nt_load=1,nt_store=1,grid=0",
                     help="';'-separated knob sets applied on top of the defaults (prefix-free keys)")
     ap.add_argument("--json", default="")
@@ -95,7 +95,7 @@ def main():
 
         def run():
             rs.reconstruct_batch_dev(shards, present, shard_len=S)
-    base = {"chunks": 1, "nt_load": 0, "nt_store": 0, "scalar_tabs": 0, "occ8": 0, "grid": -1, "diag": 0, "depth": 3, "wgs_per_cu": 0, "occ": 0, "early": 0, "spre": 0,
+    base = {"chunks": 1, "nt_load": 0, "nt_store": 0, "occ8": 0, "grid": -1, "diag": 0, "depth": 3, "wgs_per_cu": 0, "occ": 0, "early": 0, "spre": 0,
             "threads": 256, "fuse_tail": 0, "glds": 0, "serial": 0, "uvec": -2}
     variants = []
     for spec in a.variants.split(";"):
