@@ -76,12 +76,18 @@ def parse():
     ap.add_argument("--pitch-align", type=int, default=4096,
                     help="device shard pitch = S rounded up to this many bytes (DESIGN.md section 4: 4 KiB "
                          "measured +0.7-1.0 point of HBM peak over 256 B for RS(10,4)'s S = 1,677,722); 1 = the "
-                         "reference's packing, shard i at i * S (off 16-byte alignment for RS(10,4))")
+                         "reference's packing, shard i at i * S (off 16-byte alignment for RS(10,4)); implies "
+                         "--pitch-pad 0 unless the pad is given")
     ap.add_argument("--pitch-pad", type=int, default=-1,
                     help="bytes added to every shard slot after alignment; -1 (auto): one 4 KiB page when the "
                          "aligned pitch is a multiple of 64 KiB (power-of-two shard sizes: RS(8,3) 4 MiB, RS(4,2) "
-                         "1 MiB: +1.7-1.8 points of HBM peak); 0 = the reference's contiguous block buffer for "
-                         "those sizes (DESIGN.md section 4)")
+                         "1 MiB: +1.7-1.8 points of HBM peak), none with --pitch-align 1; 0 = the reference's "
+                         "contiguous block buffer for those sizes (DESIGN.md section 4)")
+    ap.add_argument("--rebuild-out", default="inplace", choices=["inplace", "compact"],
+                    help="decode configs: rebuild the erased shards in place in their block's slots, or into a "
+                         "separate compact [blocks][erasures][pitch] output -- the crate's semantics, every None "
+                         "shard rebuilt into a fresh buffer (reference src/vfs/block.rs:556-565; "
+                         "shmr_ec_reconstruct_batch_dev_out)")
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher rehearsal without a GPU: ranks join the process group, exchange their "
                          "identities and rank 0 prints one JSON line (tests/test_bench_launch.py)")
@@ -209,7 +215,8 @@ def run(args):
         erasures = -erasures
     op = "encode" if erasures is None else "decode"
     rows = p if erasures is None else erasures
-    tuning = shmr_amd.describe_variant(op == "decode", k, rows)
+    compact = erasures is not None and args.rebuild_out == "compact"
+    tuning = shmr_amd.describe_variant(0 if op == "encode" else 2 if compact else 1, k, rows)
     if codec:
         tuning = f"encode: {shmr_amd.describe_variant(False, k, p)}; reconstruct: {tuning}"
     rs = shmr_amd.ReedSolomon(k, p)
@@ -224,7 +231,10 @@ def run(args):
     # page-aligned 1,679,360-byte slots (0.1 %) and no page.
     a = max(1, args.pitch_align)          # 1: pitch = S, the reference's packing (any alignment)
     pitch = (S + a - 1) // a * a
-    pitch += (4096 if pitch % 65536 == 0 else 0) if args.pitch_pad < 0 else args.pitch_pad
+    pad = args.pitch_pad
+    if pad < 0:
+        pad = 0 if a == 1 else (4096 if pitch % 65536 == 0 else 0)
+    pitch += pad
     g = torch.Generator(device=dev)
     g.manual_seed(SEED + rank)
     bufs = []
@@ -259,6 +269,20 @@ def run(args):
         else:
             present[np.arange(B), gb % 10] = 0                     # config 4: {b%10, (b+3)%10}
             present[np.arange(B), (gb + 3) % 10] = 0
+        rebuilt = None
+        if compact:
+            # rebuilt shards into their own [B][erasures][pitch] array; the
+            # erased slots of the block buffer are zeroed and never read
+            rebuilt = vram((B, erasures, pitch))
+            rebuilt.zero_()
+            originals = shards[torch.from_numpy(present == 0).to(dev)][:, :S].clone().view(B, erasures, S)
+            shards[torch.from_numpy(present == 0).to(dev)] = 0
+
+        def rebuild():
+            if compact:
+                rs.reconstruct_batch_dev_out(shards, present, rebuilt, shard_len=S)
+            else:
+                rs.reconstruct_batch_dev(shards, present, shard_len=S)
 
         if codec:
             # encode, then rebuild the erased shards in place: two launches per
@@ -268,11 +292,10 @@ def run(args):
             def step():
                 rs.encode_batch_dev(shards[:, :k], shards[:, k:], shard_len=S,
                                     data_shard_pitch=pitch, parity_shard_pitch=pitch)
-                rs.reconstruct_batch_dev(shards, present, shard_len=S)
+                rebuild()
             algo_bytes_per_block = (k + p) * S + (k + erasures) * S
         else:
-            def step():
-                rs.reconstruct_batch_dev(shards, present, shard_len=S)
+            step = rebuild
             algo_bytes_per_block = (k + erasures) * S
         payload_bytes_per_block = k * S
     torch.cuda.synchronize(dev)
@@ -347,6 +370,9 @@ def run(args):
             "tuning": tuning,
             "memory": "physically contiguous VRAM (shmr_ec_device_alloc)" if args.contig else "torch caching allocator (hipMalloc)",
             "shard_pitch_bytes": pitch,
+            "rebuild_out": (None if erasures is None else
+                            "compact [blocks][erasures][pitch] output (crate semantics: a fresh buffer per None "
+                            "shard)" if compact else "in place, in the erased shards' own slots"),
             "shard_layout": ("contiguous shards (the reference's block buffer)" if pitch == S else
                              f"shard slots of {pitch} B for {S} B shards"
                              + (" (one 4 KiB page past the 4 KiB-aligned size for a power-of-two stride, "
@@ -364,10 +390,7 @@ def run(args):
         },
         "cpu_baseline": None,
     }
-    traffic, source = load_traffic(args.config, B, out["library"]["build_id"], tuning)
-    if (args.pitch_align, args.pitch_pad) != (4096, -1):
-        # the PMC records were taken on the default shard slots
-        traffic, source = None, dict(source, status="not profiled: non-default shard layout")
+    traffic, source = load_traffic(traffic_key(args), B, out["library"]["build_id"], tuning)
     out["roofline"]["traffic"] = traffic
     out["roofline"]["traffic_source"] = source
     if codec:
@@ -378,19 +401,31 @@ def run(args):
         # the timed steps ran over already-consistent blocks: wipe the parity,
         # encode, wipe the erased shards, rebuild them, and check every shard
         # against the originals
+        erased = torch.from_numpy(present == 0).to(dev)
         shards[:, k:] = 0
         rs.encode_batch_dev(shards[:, :k], shards[:, k:], shard_len=S,
                             data_shard_pitch=pitch, parity_shard_pitch=pitch)
-        shards[torch.from_numpy(present == 0).to(dev)] = 0
-        rs.reconstruct_batch_dev(shards, present, shard_len=S)
-        torch.cuda.synchronize(dev)
-        out["roofline"]["round_trip_bit_exact"] = bool(torch.equal(shards[:, :, :S], reference))
+        if compact:
+            # the encode rewrote the erased parity slots: clear them again
+            shards[erased] = 0
+            rebuilt.zero_()
+            rebuild()
+            torch.cuda.synchronize(dev)
+            ok = bool(torch.equal(rebuilt[:, :, :S], originals)) and bool(
+                torch.equal(shards[~erased][:, :S], reference[~erased]))
+        else:
+            shards[erased] = 0
+            rebuild()
+            torch.cuda.synchronize(dev)
+            ok = bool(torch.equal(shards[:, :, :S], reference))
+        out["roofline"]["round_trip_bit_exact"] = ok
         del reference
     if rank == 0 and world == 1 and not args.no_cpu:
         if codec:
             enc = cpu_baseline(k, p, S, block_bytes, shards[:, :k], shards[:, k:], args.cpu_seconds / 2,
                                args.cpu_threads)
-            dec = cpu_baseline_decode(k, p, S, shards, present, args.cpu_seconds / 2, args.cpu_threads)
+            dec = cpu_baseline_decode(k, p, S, shards, present, args.cpu_seconds / 2, args.cpu_threads,
+                                      rebuilt)
             rate = 1.0 / (1.0 / enc["value"] + 1.0 / dec["value"])
             out["cpu_baseline"] = {
                 "value": round(rate, 3), "unit": "GiB/s", "cores": enc["cores"], "kind": "port",
@@ -405,11 +440,29 @@ def run(args):
         elif erasures is None:
             out["cpu_baseline"] = cpu_baseline(k, p, S, block_bytes, data, parity, args.cpu_seconds, args.cpu_threads)
         else:
-            out["cpu_baseline"] = cpu_baseline_decode(k, p, S, shards, present, args.cpu_seconds, args.cpu_threads)
+            out["cpu_baseline"] = cpu_baseline_decode(k, p, S, shards, present, args.cpu_seconds, args.cpu_threads,
+                                                      rebuilt)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def traffic_key(args) -> str:
+    """Key of the PMC record for this run's configuration and layout: the
+    config name, plus "+packed" for the reference's packing (--pitch-align 1),
+    "+contig" for --pitch-pad 0 on a power-of-two shard, "+compact" for a
+    compact rebuild output."""
+    key = args.config
+    if args.pitch_align == 1:
+        key += "+packed"
+    elif args.pitch_pad == 0:
+        key += "+contig"
+    elif (args.pitch_align, args.pitch_pad) != (4096, -1):
+        key += f"+pitch{args.pitch_align}_{args.pitch_pad}"
+    if args.rebuild_out == "compact" and CONFIGS[args.config][3] is not None:
+        key += "+compact"
+    return key
 
 
 def load_traffic(config: str, B: int, build_id: str, variant: str):
@@ -543,17 +596,23 @@ def cpu_baseline(k, p, S, block_bytes, data_t, parity_t, budget_s, threads=0):
     }
 
 
-def cpu_baseline_decode(k, p, S, shards_t, present, budget_s, threads=0):
+def cpu_baseline_decode(k, p, S, shards_t, present, budget_s, threads=0, rebuilt_t=None):
     """CPU restatement of the crate's reconstruct (first k present shards,
     inverted sub-matrix, SIMD mul_slice loop; oracle/, "port"), one block per
     thread; bounded sample of the same decode workload.  The GPU's rebuilt
-    shards of the sampled blocks are checked bit-for-bit against it."""
+    shards of the sampled blocks (in place, or rows of the compact output
+    `rebuilt_t`) are checked bit-for-bit against it."""
     from oracle import c_oracle   # cpu_baseline leg: oracle allowed here only
     cores = cpu_threads(threads)
     t = k + p
     nb = min(shards_t.shape[0], max(1, (1 << 30) // (t * S), 4 * cores))
     gpu = np.ascontiguousarray(shards_t[:nb, :, :S].cpu().numpy())
     pr = np.ascontiguousarray(present[:nb], dtype=np.uint8)
+    if rebuilt_t is not None:   # compact output: row j = the j-th erased shard of the block
+        rows = rebuilt_t[:nb, :, :S].cpu().numpy()
+        for b in range(nb):
+            for j, i in enumerate(np.flatnonzero(pr[b] == 0)):
+                gpu[b, i] = rows[b, j]
     work = gpu.copy()
     work[pr == 0] = 0
     reps, secs = 0, 0.0

@@ -126,11 +126,24 @@ int shmr_ec_reconstruct(shmr_ec_t* rs, uint8_t* const* shards, const size_t* sha
 
 /* ---- device-resident batched entry points ------------------------------ *
  * All pointers are device pointers on `device`; `stream` is a hipStream_t
- * (NULL = the null stream).  Calls are asynchronous w.r.t. the host: they
- * enqueue kernels on `stream` and return.  Block b's shard i lives at
- *     base + b * block_pitch + i * shard_pitch.
- * 16-byte aligned bases/pitches take the vector path; anything else is
- * handled byte-granularly (correct, slower). */
+ * (NULL = the null stream).  Block b's shard i lives at
+ *     base + b * block_pitch + i * shard_pitch,
+ * at any byte alignment (the reference's packed block buffer, shard i at
+ * i * S, included).
+ *
+ * Stream-ordered: after the device's one-time initialisation (the first call
+ * that touches the device, or shmr_ec_device_init) these calls make no
+ * blocking HIP call -- they enqueue kernels (and, for an erasure pattern not
+ * seen before on the device, one hipMemcpyAsync of its coefficient plan from
+ * a permanent pinned slot) on `stream` and return.  They can be captured into
+ * a HIP graph (e.g. torch.cuda.graph) once the device is initialised; a
+ * capture that would need the initialisation returns INVALID_ARGUMENT with
+ * nothing enqueued.  SHMR_EC_DEV_BLOCKING_CALLS counts the exceptions. */
+
+/* One-time per-device initialisation (probe of the memory system's unaligned
+ * access mode on a private stream, the plan arena in pinned and device
+ * memory).  Optional: the first device call does it implicitly.  Blocking. */
+int shmr_ec_device_init(int device);
 
 /* Encode nblocks blocks: data shard i of block b at
  * d_data + b*data_block_pitch + i*data_shard_pitch; parity shard r at
@@ -147,6 +160,24 @@ int shmr_ec_encode_batch_dev(shmr_ec_t* rs, const uint8_t* d_data, size_t data_s
 int shmr_ec_reconstruct_batch_dev(shmr_ec_t* rs, uint8_t* d_shards, size_t shard_pitch,
                                   size_t block_pitch, const uint8_t* present, size_t nblocks,
                                   size_t shard_len, int data_only, int device, void* stream);
+
+/* Reconstruct with the crate's memory semantics: every absent shard is
+ * rebuilt into a buffer of its own (reed_solomon_erasure allocates
+ * vec![0; len] for each None, called at src/vfs/block.rs:556-565; load_block
+ * then concatenates them, :567-576), not into the block's slot.  Present
+ * shards of block b are read in place at d_shards + b*block_pitch +
+ * i*shard_pitch (absent slots are neither read nor written); block b's
+ * rebuilt shards, in ascending shard index, are written to
+ *     d_out + b*out_block_pitch + j*out_shard_pitch,  j = 0 .. rebuilt-1
+ * (data_only != 0: the absent data shards only).  d_out must hold the largest
+ * rebuilt count of the batch per block and must not overlap a present shard.
+ * Blocks with every shard present write nothing.  Validation and errors as
+ * shmr_ec_reconstruct_batch_dev. */
+int shmr_ec_reconstruct_batch_dev_out(shmr_ec_t* rs, const uint8_t* d_shards, size_t shard_pitch,
+                                      size_t block_pitch, const uint8_t* present, size_t nblocks,
+                                      size_t shard_len, int data_only, uint8_t* d_out,
+                                      size_t out_shard_pitch, size_t out_block_pitch, int device,
+                                      void* stream);
 
 /* ---- host-buffer batches over one or more GPUs ---------------------------- *
  * Blocks held in HOST memory (the Block Cache / shard file buffers), whole
@@ -240,17 +271,20 @@ int shmr_ec_set_device(shmr_ec_t* rs, int device);
  * head of the full-tile launch instead of in a second launch), "glds" (0/1:
  * input ring in LDS filled by global_load_lds_dwordx4, depth = ring slots),
  * "serial" (0/1: GF math ordered one dword at a time, fewer VGPRs; auto:
- * encodes of 4 output rows), "diag"
+ * encodes of 4 output rows), "sc1_store" (0/1: stores with the sc1 cache
+ * policy instead of nontemporal; auto: reconstructs into a compact output),
+ * "diag"
  * (0/1: XOR-only diagnostic kernel, WRONG results, for ceiling measurements).
  * Prefix "encode." or "decode." to set one operation class only.
  * "chunks", "nt_load", "nt_store", "depth", "wgs_per_cu", "occ", "early",
- * "spre", "fuse_tail", "glds" and "serial" default to -2 (auto): the per-shape policy; any other value pins
+ * "spre", "fuse_tail", "glds", "serial" and "sc1_store" default to -2 (auto): the per-shape policy; any other value pins
  * the knob, and setting -2 returns it to the policy. */
 int shmr_ec_set_tuning(const char* key, int value);
 int shmr_ec_get_tuning(const char* key);
 
 /* Writes the kernel variant that a launch of `rows` output rows over
- * `data_shards` inputs would use (encode: decode=0, reconstruct: decode=1). */
+ * `data_shards` inputs would use (encode: decode=0, reconstruct in place:
+ * decode=1, reconstruct into a compact output: decode=2). */
 int shmr_ec_describe_variant(int decode, uint32_t data_shards, uint32_t rows, char* buf, size_t len);
 
 /* Decode-matrix LRU statistics of the (data, parity) codec (crate cache
@@ -279,7 +313,10 @@ enum {
     SHMR_EC_DEV_PLAN_IMAGES = 3,          /* coefficient plans uploaded to this device */
     SHMR_EC_DEV_UPLOAD_RINGS = 4,         /* pinned upload rings created for this device */
     SHMR_EC_DEV_STAGING_STREAMS = 5,      /* staging / pipeline streams created for this device */
-    SHMR_EC_DEV_COUNTERS = 6
+    SHMR_EC_DEV_BLOCKING_CALLS = 6,       /* blocking HIP calls the library made on its own: device
+                                             init, plan-arena growth, upload-ring creation and waits
+                                             for a ring slot (not the host-buffer calls' final sync) */
+    SHMR_EC_DEV_COUNTERS = 7
 };
 int shmr_ec_device_stats(int device, uint64_t* out, size_t n);
 

@@ -6,6 +6,6 @@ of GF(2^8) arithmetic runs in hand-written gfx950 HIP kernels
 (``shmr_amd/csrc/gf_apply.hip``).  No CPU compute fallback exists.
 """
 from .reed_solomon import (DeviceBuffer, Error, PinnedBuffer, ReedSolomon, calculate_shard_size, describe_variant, device_count,  # noqa: F401
-                           device_stats, get_tuning, host_register, host_unregister, path_stats, set_tuning)
+                           device_init, device_stats, get_tuning, host_register, host_unregister, path_stats, set_tuning)
 
 __version__ = "0.1.0"

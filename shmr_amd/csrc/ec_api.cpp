@@ -165,8 +165,10 @@ int shmr_ec_get_tuning(const char* key) {
 
 int shmr_ec_describe_variant(int decode, uint32_t data_shards, uint32_t rows, char* buf, size_t len) {
     if (!buf || len == 0 || rows == 0) return SHMR_EC_INVALID_ARGUMENT;
+    if (decode < 0 || decode > 2) return SHMR_EC_INVALID_ARGUMENT;
     const core::OpClass op = decode ? core::kDecode : core::kEncode;
-    const auto v = core::resolve_variant(op, data_shards, std::min<uint32_t>(rows, shmr::kern::kMaxRowsPerLaunch));
+    const auto v = core::resolve_variant(op, data_shards, std::min<uint32_t>(rows, shmr::kern::kMaxRowsPerLaunch),
+                                         false, decode == 2);
     auto lean = v;   // the full-tile kernel without fused tails must always exist
     lean.fuse_tail = false;
     const bool compiled = shmr::kern::variant_compiled(lean) && (!v.fuse_tail || shmr::kern::variant_compiled(v));
@@ -177,7 +179,8 @@ int shmr_ec_describe_variant(int decode, uint32_t data_shards, uint32_t rows, ch
                   core::grid_mode(op), int(v.diag), v.depth, v.wgs_per_cu, v.occ, int(v.early), int(v.spre), int(v.fuse_tail),
                   int(compiled));
     // appended only when set: records keyed by the string stay valid
-    for (const auto& kv : {std::make_pair(v.glds, " glds=1"), std::make_pair(v.serial, " serial=1")}) {
+    for (const auto& kv : {std::make_pair(v.glds, " glds=1"), std::make_pair(v.serial, " serial=1"),
+                           std::make_pair(v.sc1_store, " sc1_store=1")}) {
         const size_t n = std::strlen(buf);
         if (kv.first && n + 1 < len) std::snprintf(buf + n, len - n, "%s", kv.second);
     }
@@ -192,6 +195,14 @@ int shmr_ec_cache_stats(const shmr_ec_t* rs, uint64_t* hits, uint64_t* misses) {
 }
 
 int shmr_ec_device_count(void) { return core::device_count(); }
+
+int shmr_ec_device_init(int device) {
+    return guarded([&]() -> int {
+        const int rc = core::check_device(device);
+        if (rc) return rc;
+        return core::device_init(device, nullptr);
+    });
+}
 
 int shmr_ec_device_stats(int device, uint64_t* out, size_t n) {
     if (!out || device < 0) return SHMR_EC_INVALID_ARGUMENT;
@@ -458,6 +469,29 @@ int shmr_ec_reconstruct_batch_dev(shmr_ec_t* rs, uint8_t* d_shards, size_t shard
         if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
         return core::reconstruct_on_device(c, device, d_shards, shard_pitch, block_pitch, present, nblocks, shard_len,
                                            data_only != 0, static_cast<hipStream_t>(stream));
+    });
+}
+
+int shmr_ec_reconstruct_batch_dev_out(shmr_ec_t* rs, const uint8_t* d_shards, size_t shard_pitch, size_t block_pitch,
+                                      const uint8_t* present, size_t nblocks, size_t shard_len, int data_only,
+                                      uint8_t* d_out, size_t out_shard_pitch, size_t out_block_pitch, int device,
+                                      void* stream) {
+    return guarded([&]() -> int {
+        if (!rs || !present) return SHMR_EC_INVALID_ARGUMENT;
+        if (nblocks == 0) return SHMR_EC_OK;
+        if (shard_len == 0) return SHMR_EC_EMPTY_SHARD;
+        if (!d_shards || !d_out) return SHMR_EC_INVALID_ARGUMENT;
+        Codec& c = *rs->codec;
+        int rc = core::validate_presence(c, present, nblocks);   // no launch on a bad batch
+        if (rc) return rc;
+        rc = core::check_device(device);
+        if (rc) return rc;
+        core::DeviceScope scope(device);
+        if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
+        core::Layout L{d_shards, d_out, block_pitch, shard_pitch, out_block_pitch, out_shard_pitch, 0};
+        L.compact = true;
+        return core::reconstruct_on_device(c, device, L, present, nblocks, shard_len, data_only != 0,
+                                           static_cast<hipStream_t>(stream));
     });
 }
 

@@ -36,6 +36,7 @@ struct Tuning {
     std::atomic<int> fuse_tail{kAuto};
     std::atomic<int> glds{kAuto};
     std::atomic<int> serial{kAuto};
+    std::atomic<int> sc1_store{kAuto};
 };
 Tuning g_tune[2];   // [kEncode], [kDecode]
 std::atomic<int> g_bounce_kib{kBounceKibDefault};
@@ -83,7 +84,13 @@ std::atomic<int> g_uvec{kAuto};
 // +1.4 to +1.7 points of HBM peak on two boxes (73.9-74.7 vs 72.6-73.0 %;
 // caps of 6, 5, 4 lose; profiles/r02/ab_occ*_decode83.txt).  Neutral for
 // RS(10,4) 2-row decodes and RS(8,3) encodes, so only there.
-kern::Variant variant_policy(OpClass op, unsigned k, unsigned rows, bool host_mapped) {
+//
+// Reconstructs into a compact output (shmr_ec_reconstruct_batch_dev_out: the
+// rebuilt shards of a block written densely to a separate array, the crate's
+// fresh-allocation semantics) store with the sc1 policy instead of
+// nontemporal: the XOR replica of the 8-in / 1-out pattern ran 81 vs 76 % of
+// peak into a separate buffer (tools/cachepol.hip, profiles/r01/cachepol.jsonl).
+kern::Variant variant_policy(OpClass op, unsigned k, unsigned rows, bool host_mapped, bool compact = false) {
     kern::Variant v;
     if (op == kDecode && rows == 1 && !host_mapped) v.wgs_per_cu = 7;
     // U = 2 (8 KiB tiles) for 4-row launches, encode and reconstruct alike: a
@@ -103,6 +110,10 @@ kern::Variant variant_policy(OpClass op, unsigned k, unsigned rows, bool host_ma
     v.early = op == kEncode && (k <= 8 || rows >= 4) && !host_mapped;
     v.serial = op == kEncode && rows >= 4 && !host_mapped;
     v.fuse_tail = true;   // only where len % tile != 0 (RS(10,4): -5.5 % encode, -5.8 % decode time)
+    if (compact && op == kDecode && !host_mapped) {
+        v.sc1_store = true;
+        v.nt_store = false;
+    }
     return v;
 }
 
@@ -178,7 +189,7 @@ int set_tuning(const char* key, int value) {
             {"chunks", kAuto}, {"nt_load", kAuto}, {"nt_store", kAuto}, {"occ8", 0},
             {"grid", -1},      {"diag", 0},        {"threads", 256},    {"depth", kAuto},   {"wgs_per_cu", kAuto},
             {"occ", kAuto},    {"early", kAuto},   {"spre", kAuto},     {"fuse_tail", kAuto},
-            {"glds", kAuto},   {"serial", kAuto}};
+            {"glds", kAuto},   {"serial", kAuto},   {"sc1_store", kAuto}};
         const auto it = kDefaults.find(k);
         return (it != kDefaults.end() && it->second == value) ? SHMR_EC_OK : SHMR_EC_INVALID_ARGUMENT;
     }
@@ -221,6 +232,8 @@ int set_tuning(const char* key, int value) {
             T.glds = value == kAuto ? kAuto : (value != 0);
         } else if (k == "serial") {
             T.serial = value == kAuto ? kAuto : (value != 0);
+        } else if (k == "sc1_store") {
+            T.sc1_store = value == kAuto ? kAuto : (value != 0);
         } else {
             return SHMR_EC_INVALID_ARGUMENT;
         }
@@ -254,12 +267,13 @@ int get_tuning(const char* key) {
     if (k == "fuse_tail") return T.fuse_tail;
     if (k == "glds") return T.glds;
     if (k == "serial") return T.serial;
+    if (k == "sc1_store") return T.sc1_store;
     return SHMR_EC_INVALID_ARGUMENT;
 }
 
-kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_mapped) {
+kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_mapped, bool compact) {
     const Tuning& T = g_tune[op];
-    kern::Variant v = variant_policy(op, k, rows, host_mapped);
+    kern::Variant v = variant_policy(op, k, rows, host_mapped, compact);
     if (T.u.load() != kAuto) v.u = T.u.load();
     if (T.nt_load.load() != kAuto) v.nt_load = T.nt_load.load() != 0;
     if (T.nt_store.load() != kAuto) v.nt_store = T.nt_store.load() != 0;
@@ -276,33 +290,13 @@ kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_m
     if (T.fuse_tail.load() != kAuto) v.fuse_tail = T.fuse_tail.load() != 0;
     if (T.glds.load() != kAuto) v.glds = T.glds.load() != 0;
     if (T.serial.load() != kAuto) v.serial = T.serial.load() != 0;
+    if (T.sc1_store.load() != kAuto) v.sc1_store = T.sc1_store.load() != 0;
+    if (v.sc1_store) v.nt_store = false;   // one store policy per kernel
     if (v.glds) v.early = v.spre = false;   // the LDS-DMA ring is a form of the plain tile
     return v;
 }
 
 int grid_mode(OpClass op) { return g_tune[op].grid.load(); }
-
-// Whether misaligned device-resident shards may take the vector kernels: the
-// knob, or (auto) the device's probe result, run once per physical device.
-bool unaligned_vector(int dev) {
-    const int knob = g_uvec.load();
-    if (knob != kAuto) return knob != 0;
-    static std::mutex mu;
-    static auto* verdict = new std::map<int, bool>;   // leaked: outlives static teardown
-    std::lock_guard<std::mutex> lock(mu);
-    const int phys = physical_device(dev);
-    auto it = verdict->find(phys);
-    if (it != verdict->end()) return it->second;
-    bool ok = false;
-    // A probe that could not run (e.g. inside a stream capture) decides only
-    // this launch (realigning kernel) and is tried again on the next one.
-    if (kern::probe_unaligned_vector(&ok) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    (*verdict)[phys] = ok;
-    return ok;
-}
 
 uint64_t bounce_limit() { return uint64_t(g_bounce_kib.load()) << 10; }
 
@@ -322,8 +316,9 @@ hipError_t sync_stream(hipStream_t stream) {
     return hipStreamSynchronize(stream);
 }
 
-kern::Variant launch_variant(OpClass op, unsigned k, unsigned rows, bool host_mapped, bool ptrs, bool segs) {
-    kern::Variant v = resolve_variant(op, k, rows, host_mapped);
+kern::Variant launch_variant(OpClass op, unsigned k, unsigned rows, bool host_mapped, bool ptrs, bool segs,
+                             bool compact) {
+    kern::Variant v = resolve_variant(op, k, rows, host_mapped, compact && !ptrs);
     v.ptrs = ptrs;
     v.segs = segs;
     if (ptrs) {
@@ -340,9 +335,9 @@ kern::Variant launch_variant(OpClass op, unsigned k, unsigned rows, bool host_ma
     return v;
 }
 
-bool segs_supported(OpClass op, unsigned k, bool host_mapped, bool ptrs) {
+bool segs_supported(OpClass op, unsigned k, bool host_mapped, bool ptrs, bool compact) {
     for (unsigned rows : {1u, kern::kMaxRowsPerLaunch}) {
-        kern::Variant v = launch_variant(op, k, rows, host_mapped, ptrs, true);
+        kern::Variant v = launch_variant(op, k, rows, host_mapped, ptrs, true, compact);
         v.fuse_tail = false;
         if (!kern::variant_compiled(v)) return false;
     }
@@ -393,23 +388,207 @@ uint32_t plan_tab_off(unsigned k, unsigned m) {
     return uint32_t((8 + 2 * size_t(k) + 2 * size_t(m) + 31) & ~size_t(31));
 }
 
-int plan_on_device(Plan& plan, int dev, const uint8_t** out) {
-    std::lock_guard<std::mutex> lock(plan.dev_mu);
-    auto it = plan.dev_image.find(dev);
-    if (it != plan.dev_image.end()) {
-        *out = static_cast<const uint8_t*>(it->second);
-        return SHMR_EC_OK;
+// ---- per-device state: unaligned-access verdict and the plan arena ----------
+namespace {
+constexpr size_t kArenaChunk = size_t(4) << 20;   // ~3,000 RS(10,4) plan images
+constexpr size_t kArenaAlign = 256;
+
+struct ArenaChunk {
+    uint8_t* host = nullptr;   // pinned
+    uint8_t* dev = nullptr;
+    size_t cap = 0, used = 0;
+};
+
+struct DeviceState {
+    int dev = -1;
+    bool uvec = false;             // probe verdict of the physical GPU
+    hipStream_t priv = nullptr;    // private stream of init-time work
+    std::mutex mu;                 // guards chunks
+    std::vector<ArenaChunk> chunks;
+};
+
+std::mutex g_state_mu;                          // serialises device_init
+std::atomic<DeviceState*> g_state[kMaxDevIds];  // leaked: in-flight kernels read the arenas
+std::map<int, bool>* g_probe_verdict = new std::map<int, bool>;   // physical GPU -> verdict
+
+DeviceState* state_of(int dev) {
+    return (dev >= 0 && dev < kMaxDevIds) ? g_state[dev].load(std::memory_order_acquire) : nullptr;
+}
+
+// Blocking: pinned + device allocation.  Caller holds ds.mu (or owns ds).
+int add_chunk(DeviceState& ds, size_t bytes) {
+    ArenaChunk c;
+    c.cap = std::max(round_up(bytes, kArenaAlign), kArenaChunk);
+    count_device(ds.dev, kDevBlockingCalls, 2);
+    if (hipHostMalloc(reinterpret_cast<void**>(&c.host), c.cap, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return SHMR_EC_OUT_OF_MEMORY;
     }
-    std::vector<uint8_t> img = plan.image();
-    void* d = nullptr;
-    if (hipMalloc(&d, img.size()) != hipSuccess) return SHMR_EC_OUT_OF_MEMORY;
-    if (hipMemcpy(d, img.data(), img.size(), hipMemcpyHostToDevice) != hipSuccess) {
-        (void)hipFree(d);
+    if (hipMalloc(reinterpret_cast<void**>(&c.dev), c.cap) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipHostFree(c.host);
+        return SHMR_EC_OUT_OF_MEMORY;
+    }
+    ds.chunks.push_back(c);
+    return SHMR_EC_OK;
+}
+}  // namespace
+
+bool stream_capturing(hipStream_t stream) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &st) != hipSuccess) {
+        (void)hipGetLastError();
+        return true;   // unknown: take the capture-safe path
+    }
+    return st != hipStreamCaptureStatusNone;
+}
+
+int device_init(int dev, hipStream_t caller) {
+    if (dev < 0 || dev >= kMaxDevIds) return SHMR_EC_INVALID_ARGUMENT;
+    if (state_of(dev)) return SHMR_EC_OK;
+    std::lock_guard<std::mutex> lock(g_state_mu);
+    if (state_of(dev)) return SHMR_EC_OK;
+    // Init allocates and synchronises: inside a capture it would invalidate
+    // the caller's graph, so it is refused there (nothing enqueued).
+    if (caller && stream_capturing(caller)) return SHMR_EC_INVALID_ARGUMENT;
+    DeviceScope scope(dev);
+    if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
+    auto* ds = new DeviceState;
+    ds->dev = dev;
+    count_device(dev, kDevBlockingCalls);
+    if (hipStreamCreateWithFlags(&ds->priv, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        delete ds;
         return SHMR_EC_DEVICE_ERROR;
     }
-    plan.dev_image[dev] = d;
-    count_device(dev, kDevPlanImages);
-    *out = static_cast<const uint8_t*>(d);
+    int rc = add_chunk(*ds, kArenaChunk);
+    if (rc) {
+        (void)hipStreamDestroy(ds->priv);
+        delete ds;
+        return rc;
+    }
+    // the probe's scratch: the head of the first chunk
+    ArenaChunk& c = ds->chunks.back();
+    c.used = round_up(kern::kProbeScratchBytes, kArenaAlign);
+    const int phys = physical_device(dev);
+    auto it = g_probe_verdict->find(phys);
+    if (it == g_probe_verdict->end()) {
+        bool ok = false;
+        count_device(dev, kDevBlockingCalls);
+        if (kern::probe_unaligned_vector(&ok, c.dev, c.host, ds->priv) != hipSuccess) {
+            (void)hipGetLastError();
+            ok = false;   // the realigning kernel serves misaligned shards
+        }
+        it = g_probe_verdict->emplace(phys, ok).first;
+    }
+    ds->uvec = it->second;
+    g_state[dev].store(ds, std::memory_order_release);
+    return SHMR_EC_OK;
+}
+
+bool unaligned_vector(int dev) {
+    const int knob = g_uvec.load();
+    if (knob != kAuto) return knob != 0;
+    const DeviceState* ds = state_of(dev);
+    return ds && ds->uvec;
+}
+
+int arena_alloc(int dev, size_t bytes, bool capturing, uint8_t** host, uint8_t** devp) {
+    DeviceState* ds = state_of(dev);
+    if (!ds) return SHMR_EC_INVALID_ARGUMENT;
+    bytes = round_up(bytes ? bytes : 1, kArenaAlign);
+    std::lock_guard<std::mutex> lock(ds->mu);
+    if (ds->chunks.back().used + bytes > ds->chunks.back().cap) {
+        if (capturing) return SHMR_EC_OUT_OF_MEMORY;   // growth would allocate inside the capture
+        DeviceScope scope(dev);
+        if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
+        const int rc = add_chunk(*ds, bytes);
+        if (rc) return rc;
+    }
+    ArenaChunk& c = ds->chunks.back();
+    *host = c.host + c.used;
+    *devp = c.dev + c.used;
+    c.used += bytes;
+    return SHMR_EC_OK;
+}
+
+// ---- plan images ---------------------------------------------------------------
+namespace {
+// One plan image on one device ID: a permanent pinned copy and its device
+// twin in the arena.  The upload runs on the stream of the first use
+// (kPending, `ready` recorded behind it) until observed complete (kDone); an
+// upload recorded inside a capture (kCaptured) happens only when the graph
+// runs, so the next use outside a capture uploads again.
+struct PlanDev {
+    uint8_t* host = nullptr;
+    uint8_t* dev = nullptr;
+    size_t bytes = 0;
+    enum State { kCaptured, kPending, kDone } state = kCaptured;
+    hipStream_t stream = nullptr;
+    hipEvent_t ready = nullptr;
+};
+
+int upload_plan(PlanDev& pd, hipStream_t stream, bool capturing) {
+    if (hipMemcpyAsync(pd.dev, pd.host, pd.bytes, hipMemcpyHostToDevice, stream) != hipSuccess) {
+        (void)hipGetLastError();
+        return SHMR_EC_DEVICE_ERROR;
+    }
+    if (capturing) return SHMR_EC_OK;   // a graph node: same bytes on every replay
+    if (!pd.ready && hipEventCreateWithFlags(&pd.ready, hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        return SHMR_EC_DEVICE_ERROR;
+    }
+    if (hipEventRecord(pd.ready, stream) != hipSuccess) {
+        (void)hipGetLastError();
+        return SHMR_EC_DEVICE_ERROR;
+    }
+    pd.state = PlanDev::kPending;
+    pd.stream = stream;
+    return SHMR_EC_OK;
+}
+}  // namespace
+
+int plan_on_device(Plan& plan, int dev, hipStream_t stream, bool compact, const uint8_t** out) {
+    const bool cap = stream_capturing(stream);
+    std::lock_guard<std::mutex> lock(plan.dev_mu);
+    void*& slot = plan.dev_image[dev * 2 + (compact ? 1 : 0)];
+    auto* pd = static_cast<PlanDev*>(slot);
+    if (!pd) {
+        const std::vector<uint8_t> img = plan.image(compact);
+        uint8_t *h = nullptr, *d = nullptr;
+        const int rc = arena_alloc(dev, img.size(), cap, &h, &d);
+        if (rc) return rc;
+        std::memcpy(h, img.data(), img.size());
+        pd = new PlanDev;
+        pd->host = h;
+        pd->dev = d;
+        pd->bytes = img.size();
+        slot = pd;
+        count_device(dev, kDevPlanImages);
+        const int rc2 = upload_plan(*pd, stream, cap);
+        if (rc2) return rc2;
+    } else if (pd->state == PlanDev::kPending && !cap) {
+        const hipError_t q = hipEventQuery(pd->ready);
+        if (q == hipSuccess) {
+            pd->state = PlanDev::kDone;
+        } else if (q == hipErrorNotReady) {
+            (void)hipGetLastError();
+            // still in flight on another stream: order this stream after it
+            if (pd->stream != stream && hipStreamWaitEvent(stream, pd->ready, 0) != hipSuccess) {
+                (void)hipGetLastError();
+                return SHMR_EC_DEVICE_ERROR;
+            }
+        } else {
+            (void)hipGetLastError();
+            return SHMR_EC_DEVICE_ERROR;
+        }
+    } else if (pd->state != PlanDev::kDone) {
+        // captured-only upload, or capturing now before the eager upload is
+        // known complete: (re)upload on this stream -- identical bytes
+        const int rc = upload_plan(*pd, stream, cap);
+        if (rc) return rc;
+    }
+    *out = pd->dev;
     return SHMR_EC_OK;
 }
 
@@ -426,10 +605,12 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
                OpClass op) {
     const uint64_t nblk = bs.n;
     if (nblk == 0 || plan.m == 0) return SHMR_EC_OK;
+    int rc = device_init(dev, stream);
+    if (rc) return rc;
     const uint8_t* dplan = nullptr;
     const uint32_t tab_off = plan_tab_off(plan.k, plan.m);
     if (!bs.d_plans && !bs.segs) {
-        int rc = plan_on_device(plan, dev, &dplan);
+        rc = plan_on_device(plan, dev, stream, L.compact, &dplan);
         if (rc) return rc;
     }
     if (bs.nseg > kern::kMaxSegs) return SHMR_EC_INVALID_ARGUMENT;
@@ -441,17 +622,18 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
     // Misaligned device-resident shards (the reference's contiguous block
     // buffer, shard i at i * S) take the same vector kernels as aligned ones
     // where the device serves unaligned 16-byte accesses (verified once per
-    // device; every access still covers only the lane's own bytes), else the
-    // realigning kernel below.
+    // device at init; every access still covers only the lane's own bytes),
+    // else the realigning kernel below.  Mapped host shards never do: the
+    // probe covered device memory only.
     const bool aligned = ptrs ? L.ptrs_aligned
                               : (aligned16(uintptr_t(L.in_base)) && aligned16(uintptr_t(L.out_base)) &&
                                  aligned16(L.in_bpitch) && aligned16(L.in_spitch) && aligned16(L.out_bpitch) &&
                                  aligned16(L.out_spitch)) ||
-                                    unaligned_vector(dev);
+                                    (!L.host_mapped && unaligned_vector(dev));
     for (uint32_t row0 = 0; row0 < plan.m; row0 += kern::kMaxRowsPerLaunch) {
         const uint32_t rows = std::min<uint32_t>(kern::kMaxRowsPerLaunch, plan.m - row0);
         count_device(dev, kDevLaunches);
-        kern::Variant var = launch_variant(op, plan.k, rows, L.host_mapped, ptrs, bs.segs != nullptr);
+        kern::Variant var = launch_variant(op, plan.k, rows, L.host_mapped, ptrs, bs.segs != nullptr, L.compact);
         const uint64_t tb = kern::tile_bytes(var.u, var.threads);
         kern::ApplyArgs a{};
         a.in_base = L.in_base;
@@ -485,7 +667,7 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
             // Mapped host shards stay byte-granular: their loads cross PCIe,
             // where mode 3's second (overlapping) load would be paid again.
             const uint64_t tb1 = kern::tile_bytes(1);
-            const uint64_t full1 = ptrs ? 0 : len / tb1;
+            const uint64_t full1 = (ptrs || L.host_mapped) ? 0 : len / tb1;
             if (full1) {
                 a.col_base = 0;
                 a.tiles_per_block = uint32_t(full1);
@@ -557,6 +739,8 @@ int reconstruct_on_device(Codec& c, int dev, uint8_t* d_shards, uint64_t shard_p
 int reconstruct_on_device(Codec& c, int dev, const Layout& L, const uint8_t* present, uint64_t nblocks, uint64_t len,
                           bool data_only, hipStream_t stream) {
     const unsigned k = c.k(), t = k + c.p();
+    int rc = device_init(dev, stream);
+    if (rc) return rc;
     std::map<std::vector<uint8_t>, std::vector<uint64_t>> groups;   // pattern -> blocks
     for (uint64_t b = 0; b < nblocks; ++b) {
         const uint8_t* pr = present + b * t;
@@ -590,7 +774,6 @@ int reconstruct_on_device(Codec& c, int dev, const Layout& L, const uint8_t* pre
             grp.plan_idx.push_back(pi);
         }
     }
-    int rc = SHMR_EC_OK;
     for (auto& kv : by_m) {
         Group& grp = kv.second;
         // A single pattern over an arithmetic block sequence needs no upload.
@@ -613,7 +796,7 @@ int reconstruct_on_device(Codec& c, int dev, const Layout& L, const uint8_t* pre
         // no dependent table loads in the kernel prologue.
         {
             std::vector<kern::Seg> segs;
-            bool fits = segs_supported(kDecode, c.k(), L.host_mapped, L.d_ptrs != nullptr);
+            bool fits = segs_supported(kDecode, c.k(), L.host_mapped, L.d_ptrs != nullptr, L.compact);
             for (size_t i = 0; i < grp.blocks.size() && fits;) {
                 size_t e = i + 1;
                 const uint32_t st = e < grp.blocks.size() ? grp.blocks[e] - grp.blocks[i] : 1;
@@ -636,7 +819,7 @@ int reconstruct_on_device(Codec& c, int dev, const Layout& L, const uint8_t* pre
             if (fits) {
                 for (auto& sg : segs) {
                     const uint8_t* dp = nullptr;
-                    rc = plan_on_device(*grp.plans[sg.pad_], dev, &dp);
+                    rc = plan_on_device(*grp.plans[sg.pad_], dev, stream, L.compact, &dp);
                     if (rc) return rc;
                     sg.plan = dp;
                     sg.pad_ = 0;
@@ -653,12 +836,39 @@ int reconstruct_on_device(Codec& c, int dev, const Layout& L, const uint8_t* pre
         if (grp.plans.size() > 65535) return SHMR_EC_INVALID_ARGUMENT;
         std::vector<const uint8_t*> dplans(grp.plans.size());
         for (size_t i = 0; i < grp.plans.size(); ++i) {
-            rc = plan_on_device(*grp.plans[i], dev, &dplans[i]);
+            rc = plan_on_device(*grp.plans[i], dev, stream, L.compact, &dplans[i]);
             if (rc) return rc;
+        }
+        const size_t ptab_bytes = (dplans.size() * sizeof(void*) + 15) & ~size_t(15);
+        if (stream_capturing(stream)) {
+            // Inside a capture the tables must outlive every replay: one
+            // permanent arena block per captured call (never reused).
+            const size_t n = grp.blocks.size();
+            const size_t list_off = ptab_bytes;
+            const size_t pidx_off = (list_off + n * sizeof(uint32_t) + 15) & ~size_t(15);
+            const size_t total = pidx_off + n * sizeof(uint16_t);
+            uint8_t *h = nullptr, *d = nullptr;
+            rc = arena_alloc(dev, total, true, &h, &d);
+            if (rc) return rc;
+            std::memcpy(h, dplans.data(), dplans.size() * sizeof(void*));
+            std::memcpy(h + list_off, grp.blocks.data(), n * sizeof(uint32_t));
+            std::memcpy(h + pidx_off, grp.plan_idx.data(), n * sizeof(uint16_t));
+            if (hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, stream) != hipSuccess) {
+                (void)hipGetLastError();
+                return SHMR_EC_DEVICE_ERROR;
+            }
+            BlockSet bs;
+            bs.n = n;
+            bs.d_plans = reinterpret_cast<const uint8_t* const*>(d);
+            bs.d_list = reinterpret_cast<const uint32_t*>(d + list_off);
+            bs.d_plan_idx = reinterpret_cast<const uint16_t*>(d + pidx_off);
+            rc = launch_set(*grp.plans[0], dev, L, bs, len, stream, kDecode);
+            if (rc) return rc;
+            continue;
         }
         UploadRing* ring = UploadRing::for_device(dev, &rc);
         if (!ring) return rc;
-        const size_t table_bytes = (dplans.size() * sizeof(void*) + 15) & ~size_t(15);
+        const size_t table_bytes = ptab_bytes;
         if (table_bytes + 64 > UploadRing::kSlotBytes) return SHMR_EC_INVALID_ARGUMENT;
         const size_t per_chunk = (UploadRing::kSlotBytes - table_bytes - 32) / (sizeof(uint32_t) + sizeof(uint16_t));
         for (size_t c0 = 0; c0 < grp.blocks.size(); c0 += per_chunk) {
@@ -698,6 +908,7 @@ UploadRing* UploadRing::for_device(int dev, int* rc, Kind kind) {
     auto& r = (*rings)[{dev, int(kind)}];
     if (!r) {
         auto* ring = new UploadRing;
+        ring->dev_id_ = dev;
         // on failure nothing is kept: the next call retries from scratch
         auto give_up = [&](int code) -> UploadRing* {
             for (int i = 0; i < kSlots; ++i)
@@ -708,6 +919,7 @@ UploadRing* UploadRing::for_device(int dev, int* rc, Kind kind) {
             *rc = code;
             return nullptr;
         };
+        count_device(dev, kDevBlockingCalls, 2);
         if (hipHostMalloc(reinterpret_cast<void**>(&ring->host_), kSlots * kSlotBytes, hipHostMallocDefault) !=
                 hipSuccess ||
             hipMalloc(reinterpret_cast<void**>(&ring->dev_), kSlots * kSlotBytes) != hipSuccess)
@@ -735,9 +947,18 @@ int UploadRing::acquire(uint8_t** host, uint8_t** dev, int* slot) {
             next_ = (i + 1) % kSlots;
             const bool armed = armed_[i];
             lock.unlock();
-            if (armed && hipEventSynchronize(ev_[i]) != hipSuccess) {
-                release_now(i);
-                return SHMR_EC_DEVICE_ERROR;
+            if (armed) {
+                hipError_t q = hipEventQuery(ev_[i]);
+                if (q == hipErrorNotReady) {   // the slot's last reader is still queued
+                    (void)hipGetLastError();
+                    count_device(dev_id_, kDevBlockingCalls);
+                    q = hipEventSynchronize(ev_[i]);
+                }
+                if (q != hipSuccess) {
+                    (void)hipGetLastError();
+                    release_now(i);
+                    return SHMR_EC_DEVICE_ERROR;
+                }
             }
             *host = host_ + size_t(i) * kSlotBytes;
             *dev = dev_ + size_t(i) * kSlotBytes;

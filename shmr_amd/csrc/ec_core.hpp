@@ -36,12 +36,15 @@ constexpr int kAuto = -2;
 
 int set_tuning(const char* key, int value);
 int get_tuning(const char* key);
-kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_mapped = false);
+// compact: a reconstruct that writes its rebuilt shards to a separate compact
+// output (shmr_ec_reconstruct_batch_dev_out) rather than into their slots.
+kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_mapped = false, bool compact = false);
 // The full-tile variant a launch uses: resolve_variant plus the launch form
 // (shard-pointer tables, segment table), which selects its own instantiation.
-kern::Variant launch_variant(OpClass op, unsigned k, unsigned rows, bool host_mapped, bool ptrs, bool segs);
+kern::Variant launch_variant(OpClass op, unsigned k, unsigned rows, bool host_mapped, bool ptrs, bool segs,
+                             bool compact = false);
 // Whether segment launches are compiled for this op's current tuning.
-bool segs_supported(OpClass op, unsigned k, bool host_mapped, bool ptrs);
+bool segs_supported(OpClass op, unsigned k, bool host_mapped, bool ptrs, bool compact = false);
 int grid_mode(OpClass op);
 // Largest block ((k+p) * shard bytes) a pageable single-block call bounces
 // through a mapped buffer instead of per-shard DMA copies (knob "bounce_kib").
@@ -79,6 +82,7 @@ enum DevCounter {
     kDevPlanImages,
     kDevUploadRings,
     kDevStagingStreams,
+    kDevBlockingCalls,
     kDevCounters
 };
 void count_device(int dev, DevCounter c, uint64_t n = 1);
@@ -100,10 +104,31 @@ private:
     bool ok_ = false;
 };
 
-// Device image of a plan, uploaded once per device (synchronously, on first
-// use) and kept for the codec's lifetime.
-int plan_on_device(Plan& plan, int dev, const uint8_t** out);
+// ---- per-device state --------------------------------------------------------
+// Created once per device ID, by the first call that touches the device or by
+// shmr_ec_device_init, synchronously and on a private stream (never the
+// caller's): the unaligned-access probe of the physical GPU, and the first
+// chunk of the plan arena (pinned host + device memory).  Afterwards the
+// device-resident entry points make no blocking HIP call: a plan image is
+// written once into a permanent pinned slot and uploaded with hipMemcpyAsync
+// on the caller's stream, so a graph capture records the upload and a replay
+// re-copies the same bytes.  Inside a stream capture the state must already
+// exist (SHMR_EC_INVALID_ARGUMENT otherwise: nothing is enqueued).
+int device_init(int dev, hipStream_t caller = nullptr);
+// Whether misaligned device-resident shards may take the vector kernels (the
+// probe's verdict for the device, or the tools knob "uvec").  Needs the state.
+bool unaligned_vector(int dev);
+// Whether `stream` is being captured into a graph (queries nothing else).
+bool stream_capturing(hipStream_t stream);
+
+// Device image of a plan (compact: the compact-output form, Plan::image),
+// written to the device's arena on first use and uploaded on `stream`; later
+// uses on another stream wait for that upload (an event, no host block).
+int plan_on_device(Plan& plan, int dev, hipStream_t stream, bool compact, const uint8_t** out);
 uint32_t plan_tab_off(unsigned k, unsigned m);
+// Permanent device memory from the device's plan arena (plus its pinned host
+// twin): multi-plan tables of captured launches, which a replay re-reads.
+int arena_alloc(int dev, size_t bytes, bool capturing, uint8_t** host, uint8_t** devp);
 
 // ---- launches -----------------------------------------------------------------
 struct Layout {
@@ -119,6 +144,9 @@ struct Layout {
     uint32_t total = 0;
     bool ptrs_aligned = false;
     bool host_mapped = false;
+    // Reconstruct into a compact output: rebuilt shard j (index order) of block
+    // b at out_base + b * out_bpitch + j * out_spitch (compact plan images).
+    bool compact = false;
 };
 
 // Blocks covered by one launch set: {first + j * stride} or, with d_list, the
@@ -149,7 +177,7 @@ int reconstruct_on_device(Codec& c, int dev, uint8_t* d_shards, uint64_t shard_p
                           const uint8_t* present, uint64_t nblocks, uint64_t len, bool data_only,
                           hipStream_t stream);
 
-// Same over any layout (e.g. a shard-pointer table).
+// Same over any layout (e.g. a shard-pointer table, or a compact output).
 int reconstruct_on_device(Codec& c, int dev, const Layout& L, const uint8_t* present, uint64_t nblocks, uint64_t len,
                           bool data_only, hipStream_t stream);
 
@@ -181,6 +209,7 @@ public:
 
 private:
     void release_now(int slot);
+    int dev_id_ = 0;
     bool host_unified_ = false;
     uint8_t* host_ = nullptr;
     uint8_t* dev_ = nullptr;

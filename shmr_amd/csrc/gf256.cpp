@@ -4,7 +4,6 @@
 #include <algorithm>
 #include <cstring>
 
-#include <hip/hip_runtime.h>
 
 namespace shmr {
 namespace gf {
@@ -119,7 +118,7 @@ PermTab perm_table(uint8_t c) {
     return t;
 }
 
-std::vector<uint8_t> Plan::image() const {
+std::vector<uint8_t> Plan::image(bool compact) const {
     // header: u32 k, u32 m, u16 in_idx[k], u16 out_idx[m], pad to 32 B
     size_t hdr = 8 + 2 * size_t(k) + 2 * size_t(m);
     hdr = (hdr + 31) & ~size_t(31);
@@ -127,7 +126,10 @@ std::vector<uint8_t> Plan::image() const {
     uint32_t km[2] = {k, m};
     std::memcpy(img.data(), km, 8);
     std::memcpy(img.data() + 8, in_idx.data(), 2 * size_t(k));
-    std::memcpy(img.data() + 8 + 2 * size_t(k), out_idx.data(), 2 * size_t(m));
+    std::vector<uint16_t> oi = out_idx;
+    if (compact)
+        for (unsigned j = 0; j < m; ++j) oi[j] = uint16_t(j);
+    std::memcpy(img.data() + 8 + 2 * size_t(k), oi.data(), 2 * size_t(m));
     PermTab* tabs = reinterpret_cast<PermTab*>(img.data() + hdr);
     for (unsigned t = 0; t < k; ++t)
         for (unsigned r = 0; r < m; ++r) tabs[size_t(t) * m + r] = perm_table(rows.at(r, t));
@@ -145,22 +147,9 @@ Codec::Codec(unsigned k, unsigned p) : k_(k), p_(p), matrix_(build_matrix(k, k +
     encode_plan_ = plan;
 }
 
-Codec::~Codec() {
-    auto release = [](Plan& pl) {
-        for (auto& kv : pl.dev_image) {
-            // kv.first is the caller's device ID (an alias ID maps to a physical GPU)
-            int prev = 0, n = 0;
-            const int phys = (hipGetDeviceCount(&n) == hipSuccess && n > 0 && kv.first >= n) ? kv.first % n : kv.first;
-            if (hipGetDevice(&prev) == hipSuccess && hipSetDevice(phys) == hipSuccess) {
-                (void)hipFree(kv.second);
-                (void)hipSetDevice(prev);
-            }
-        }
-        pl.dev_image.clear();
-    };
-    if (encode_plan_) release(*encode_plan_);
-    for (auto& kv : plans_) release(*kv.second);
-}
+// Device plan images live in the per-device arenas of ec_core (process
+// lifetime: a kernel may still read them when the last handle goes).
+Codec::~Codec() = default;
 
 std::shared_ptr<const Matrix> Codec::data_decode_matrix(const std::vector<uint16_t>& valid,
                                                         const std::vector<uint16_t>& invalid) {

@@ -73,13 +73,16 @@ struct Plan {
     std::vector<uint16_t> in_idx;   // size k
     std::vector<uint16_t> out_idx;  // size m
     Matrix rows;                    // m x k
-    // Device image (one per device): [u32 k][u32 m][u16 in_idx[k]][u16 out_idx[m]]
-    // padded to 32 B, then PermTab[k][m] (input-major so one shard's rows are
-    // contiguous for the kernel).
-    std::vector<uint8_t> image() const;
+    // Device image: [u32 k][u32 m][u16 in_idx[k]][u16 out_idx[m]] padded to
+    // 32 B, then PermTab[k][m] (input-major so one shard's rows are contiguous
+    // for the kernel).  compact: out_idx[j] = j, i.e. output j goes to slot j
+    // of a separate output array (the rebuilt shards in index order) instead
+    // of its shard's own slot.
+    std::vector<uint8_t> image(bool compact = false) const;
+    // Per (device ID, compact) the core's upload record (ec_core PlanDev,
+    // arena memory that lives as long as the process: in-flight kernels).
     std::mutex dev_mu;
-    std::map<int, void*> dev_image; // device id -> device pointer (never freed
-                                    // while the codec lives: in-flight kernels)
+    std::map<int, void*> dev_image;
 };
 
 // One codec per (k, p): matrix, encode plan and the crate's decode-matrix LRU.

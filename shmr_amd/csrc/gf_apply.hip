@@ -70,7 +70,15 @@ namespace {
     X(2, kNtStore | kDepth2 | kPtrs | kSegs) \
     X(2, kNtStore | kDepth2 | kPtrs | kSegs | kFuse) \
     X(1, kNtLoad | kNtStore | kDepth2 | kPtrs) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kPtrs)
+    X(2, kNtLoad | kNtStore | kDepth2 | kPtrs) \
+    X(1, kNtLoad | kSc1Store | kDepth2) \
+    X(2, kNtLoad | kSc1Store | kDepth2) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kFuse) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kFuse) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse)
 
 template <int R>
 hipError_t dispatch_full(const ApplyArgs& a, const Variant& v, int grid_cap, hipStream_t s) {
@@ -125,28 +133,29 @@ __global__ void unaligned_probe_kernel(const uint8_t* in, uint8_t* out) {
 }
 }  // namespace
 
-hipError_t probe_unaligned_vector(bool* ok) {
+hipError_t probe_unaligned_vector(bool* ok, uint8_t* d_scratch, uint8_t* h_scratch, hipStream_t stream) {
     *ok = false;
     constexpr int N = 2 * kProbeBytes;
-    uint8_t h_in[N], h_out[N], want[N];
+    static_assert(2 * N <= kProbeScratchBytes, "probe scratch");
+    uint8_t* h_in = h_scratch;
+    uint8_t* h_out = h_scratch + N;
+    uint8_t want[N];
     for (int i = 0; i < N; ++i) h_in[i] = uint8_t(i * 37 + 11), want[i] = 0xA5;
     for (int i = 0; i < kProbeLanes * 16; ++i) {
         want[5 + i] = h_in[3 + i];
         want[kProbeBytes + 7 + i] = h_in[kProbeBytes + 9 + i];
     }
-    uint8_t *d_in = nullptr, *d_out = nullptr;
-    hipError_t e = hipMalloc(reinterpret_cast<void**>(&d_in), N);
-    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d_out), N);
-    if (e == hipSuccess) e = hipMemcpy(d_in, h_in, N, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemset(d_out, 0xA5, N);
+    uint8_t* d_in = d_scratch;
+    uint8_t* d_out = d_scratch + N;
+    hipError_t e = hipMemcpyAsync(d_in, h_in, N, hipMemcpyHostToDevice, stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d_out, 0xA5, N, stream);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(unaligned_probe_kernel, dim3(1), dim3(kProbeLanes), 0, nullptr, d_in, d_out);
+        hipLaunchKernelGGL(unaligned_probe_kernel, dim3(1), dim3(kProbeLanes), 0, stream, d_in, d_out);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipMemcpy(h_out, d_out, N, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpyAsync(h_out, d_out, N, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
     if (e == hipSuccess) *ok = std::memcmp(h_out, want, N) == 0;
-    if (d_in) (void)hipFree(d_in);
-    if (d_out) (void)hipFree(d_out);
     return e;
 }
 

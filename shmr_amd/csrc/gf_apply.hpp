@@ -119,11 +119,14 @@ hipError_t launch_full_tools(const ApplyArgs& a, unsigned rows, const Variant& v
 bool variant_compiled_tools(const Variant& v);
 #endif
 
-// Runs a one-lane kernel on the current device that loads and stores 16 bytes
-// at addresses off 16-byte alignment (plain and nontemporal) and sets *ok if
-// the bytes arrived where they belong: the memory system's unaligned access
-// mode serves the vector kernels on misaligned shards (ec_core launch_set).
-hipError_t probe_unaligned_vector(bool* ok);
+// Runs a one-wave kernel on `stream` (current device) that loads and stores 16
+// bytes at addresses off 16-byte alignment (plain and nontemporal), waits for
+// it, and sets *ok if the bytes arrived where they belong: the memory
+// system's unaligned access mode serves the vector kernels on misaligned
+// shards (ec_core launch_set).  Scratch: kProbeScratchBytes of device memory
+// and of pinned host memory.
+constexpr int kProbeScratchBytes = 4 * (64 * 16 + 64);
+hipError_t probe_unaligned_vector(bool* ok, uint8_t* d_scratch, uint8_t* h_scratch, hipStream_t stream);
 
 }  // namespace kern
 }  // namespace shmr

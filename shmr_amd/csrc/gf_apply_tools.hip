@@ -251,7 +251,12 @@ __device__ __forceinline__ void spre_tile(const ApplyArgs& a, const uint8_t* pla
     X(2, kNtLoad | kNtStore | kDepth2 | kSPre | kFuse) \
     X(2, kNtLoad | kNtStore | kDepth2 | kSPre | kFuse | kSerial) \
     X(1, kNtLoad | kNtStore | kDepth2 | kSPre | kFuse) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kSPre | kFuse | kSerial)
+    X(1, kNtLoad | kNtStore | kDepth2 | kSPre | kFuse | kSerial) \
+    X(1, kNtLoad | kDepth2 | kFuse) \
+    X(1, kNtLoad | kDepth2 | kSegs) \
+    X(1, kNtLoad | kDepth2 | kSegs | kFuse) \
+    X(2, kNtLoad | kDepth2) \
+    X(2, kNtLoad | kDepth2 | kSegs)
 
 template <int R>
 hipError_t dispatch_tools(const ApplyArgs& a, const Variant& v, int grid_cap, hipStream_t s) {

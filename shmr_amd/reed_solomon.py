@@ -20,7 +20,7 @@ import numpy as np
 from ._native import _u8p, lib
 
 __all__ = ["Error", "ReedSolomon", "calculate_shard_size", "device_count", "set_tuning", "get_tuning", "describe_variant",
-           "PinnedBuffer", "host_register", "host_unregister", "path_stats"]
+           "PinnedBuffer", "host_register", "host_unregister", "path_stats", "device_init"]
 
 
 class Error(Exception):
@@ -56,8 +56,10 @@ def get_tuning(key: str) -> int:
     return int(lib().shmr_ec_get_tuning(key.encode()))
 
 
-def describe_variant(decode: bool, data_shards: int, rows: int) -> str:
-    """The kernel variant a launch of this shape uses (after the auto policy)."""
+def describe_variant(decode, data_shards: int, rows: int) -> str:
+    """The kernel variant a launch of this shape uses (after the auto policy).
+    decode: 0/False encode, 1/True reconstruct in place, 2 reconstruct into a
+    compact output (reconstruct_batch_dev_out)."""
     buf = ctypes.create_string_buffer(256)
     _check(lib().shmr_ec_describe_variant(int(decode), data_shards, rows, buf, 256))
     return buf.value.decode()
@@ -262,6 +264,42 @@ class ReedSolomon:
         _check(self._L.shmr_ec_reconstruct_batch_dev(self._h, ctypes.c_void_p(shards.data_ptr()), shards.stride(1),
                                                    shards.stride(0), _ptr(pr), B, L, int(data_only), dev, stream))
 
+    def reconstruct_batch_dev_out(self, shards, present: np.ndarray, out, shard_len: Optional[int] = None,
+                                  data_only: bool = False, device: Optional[int] = None) -> None:
+        """Rebuild the absent shards of every block into a separate compact
+        output -- the crate's semantics, where each ``None`` shard becomes a
+        fresh buffer (reference src/vfs/block.rs:556-565).
+
+        shards: uint8 [B, total, pitch] on the GPU (present shards are read in
+        place; absent slots are neither read nor written); present: host
+        [B, total] flags; out: uint8 [B, n_out, pitch'] on the GPU, where
+        out[b, j] receives block b's j-th rebuilt shard in ascending shard
+        index (absent data shards only with ``data_only``)."""
+        if shards.dim() != 3:
+            raise TypeError("shards must be a [blocks, total, bytes] tensor")
+        B, t, k = shards.shape[0], self.total_shard_count(), self.data_shard_count()
+        L = shard_len if shard_len is not None else shards.stride(1)
+        self._check_batch_tensor(shards, t, shards.stride(1), L)
+        pr = np.ascontiguousarray(present, dtype=np.uint8)
+        if pr.size != B * t:
+            raise ValueError(f"present must hold {B} x {t} flags")
+        pr = pr.reshape(B, t)
+        absent = pr == 0
+        if data_only:
+            absent[:, k:] = False
+        rebuilt = np.where(pr.all(axis=1), 0, absent.sum(axis=1)) if B else np.zeros(0, np.int64)
+        need = int(rebuilt.max()) if B else 0
+        if out.dim() != 3 or out.shape[0] != B:
+            raise TypeError("out must be a [blocks, rebuilt shards, bytes] tensor with one row per block")
+        if need:
+            self._check_batch_tensor(out[:, :need] if out.shape[1] >= need else out, need, out.stride(1), L)
+        self._check_addressable(shards, out)
+        dev, stream = self._stream_and_device(shards)
+        dev = dev if device is None else int(device)
+        _check(self._L.shmr_ec_reconstruct_batch_dev_out(
+            self._h, ctypes.c_void_p(shards.data_ptr()), shards.stride(1), shards.stride(0), _ptr(pr), B, L,
+            int(data_only), ctypes.c_void_p(out.data_ptr()), out.stride(1), out.stride(0), dev, stream))
+
     def _host_ptrs(self, blocks):
         t = self.total_shard_count()
         if isinstance(blocks, np.ndarray):
@@ -404,7 +442,14 @@ def path_stats():
 
 
 DEVICE_COUNTERS = ("blocks_encoded", "blocks_reconstructed", "launches", "plan_images", "upload_rings",
-                   "staging_streams")
+                   "staging_streams", "blocking_calls")
+
+
+def device_init(device: int = 0) -> None:
+    """One-time per-device initialisation (shmr_ec_device_init): after it the
+    device-resident entry points make no blocking HIP call and can be
+    captured into a graph."""
+    _check(lib().shmr_ec_device_init(int(device)))
 
 
 def device_stats(device: int) -> dict:

@@ -211,6 +211,13 @@ def test_tuning_api():
     assert "early=0" in shmr_amd.describe_variant(True, 4, 2)
     assert "fuse_tail=1" in shmr_amd.describe_variant(False, 10, 4)
     assert "fuse_tail=1" in shmr_amd.describe_variant(True, 10, 2)
+    # reconstructs into a compact output store with sc1 (decode=2)
+    assert "sc1_store=1" in shmr_amd.describe_variant(2, 8, 1)
+    assert "nt_store=0" in shmr_amd.describe_variant(2, 8, 1)
+    assert "sc1_store" not in shmr_amd.describe_variant(True, 8, 1)
+    shmr_amd.set_tuning(sc1_store=-2)
+    with pytest.raises(shmr_amd.Error):
+        shmr_amd.set_tuning(sc1_store=0)
     saved = shmr_amd.get_tuning("bounce_kib")
     try:
         shmr_amd.set_tuning(bounce_kib=0)
@@ -233,7 +240,7 @@ def test_tuning_api():
 
 def test_auto_policy_variants_are_compiled():
     """Every shape the auto policy can pick maps to a compiled kernel."""
-    for decode in (False, True):
+    for decode in (0, 1, 2):
         for k in range(1, 33):
             for rows in range(1, 5):
                 d = shmr_amd.describe_variant(decode, k, rows)
@@ -263,7 +270,9 @@ def test_tools_build_is_separate():
     libshmr_ec_tools.so; objects keep the library they were created with."""
     with _native.tools() as T:
         assert T.shmr_ec_is_tools_build() == 1 and b"tools" in T.shmr_ec_version()
-        assert T.shmr_ec_build_id() == _native.lib().shmr_ec_build_id()   # same kernel sources
+        # the tools ID hashes the product kernel TU and the tools-only TU
+        assert re.fullmatch(rb"[0-9a-f]{12}", T.shmr_ec_build_id())
+        assert T.shmr_ec_build_id() != _native._load("product").shmr_ec_build_id()
         saved = shmr_amd.get_tuning("encode.chunks")
         try:
             shmr_amd.set_tuning(**{"encode.chunks": 2})
@@ -362,8 +371,10 @@ def test_product_library_has_no_diagnostic_kernel():
     tools = _kernel_flags(_native._PATHS["tools"])
     assert product and not any(f & KDIAG for f in product)
     assert any(f & KDIAG for f in tools)
-    # every product full-tile kernel (MODE 0) is a depth-2 ring with nontemporal stores
-    assert all(f & KDEPTH2 and f & 2 for f in product if f != 0)
+    # every product full-tile kernel (MODE 0) is a depth-2 ring with nontemporal
+    # stores, or sc1 stores (reconstructs into a compact output)
+    KSC1 = 1 << 23
+    assert all(f & KDEPTH2 and (f & 2 or f & KSC1) for f in product if f != 0)
     assert product < tools
 
 
@@ -384,10 +395,12 @@ def test_device_list_and_stats_api():
         assert L.shmr_ec_reconstruct_blocks_host(h, ptrs, pr.ctypes.data_as(_native._u8p), 1, 4096, 0, d, n) == -100
     assert L.shmr_ec_set_device(h, -1) == -100
     L.shmr_ec_free(h)
-    out = (ctypes.c_uint64 * 6)(*([7] * 6))
-    assert L.shmr_ec_device_stats(-1, out, 6) == -100
-    assert L.shmr_ec_device_stats(0, None, 6) == -100
-    assert L.shmr_ec_device_stats(0, out, 6) == 0 and list(out) == [0] * 6
+    out = (ctypes.c_uint64 * 7)(*([7] * 7))
+    assert L.shmr_ec_device_stats(-1, out, 7) == -100
+    assert L.shmr_ec_device_stats(0, None, 7) == -100
+    assert L.shmr_ec_device_stats(0, out, 7) == 0 and list(out) == [0] * 7
+    assert L.shmr_ec_device_init(0) == -101          # NoDevice (no GPU here)
+    assert L.shmr_ec_device_init(-1) in (-100, -101)
     assert shmr_amd.device_stats(3) == {k: 0 for k in shmr_amd.reed_solomon.DEVICE_COUNTERS}
     assert L.shmr_ec_set_tuning(b"alias_devices", 1) == -100
     assert L.shmr_ec_set_tuning(b"alias_devices", 0) == 0

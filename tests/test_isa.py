@@ -1,0 +1,103 @@
+"""The product code object's memory instructions (CPU-only: disassembles the
+gfx950 code object embedded in libshmr_ec.so with the ROCm LLVM tools).
+
+Misaligned device-resident shards (the reference's packed block buffer, shard
+i at i * S, src/vfs/block.rs:408-419) run the same vector kernels as aligned
+ones.  Their 16-byte accesses go through an under-aligned vector type (well-
+defined C++ at any address); this pins that the compiler still lowers every
+full-tile kernel's data path to global_load_dwordx4 / global_store_dwordx4 --
+no byte-granular or split accesses -- and that the sc1 policy reaches the
+compact-output kernels' stores.
+"""
+import os
+import re
+import subprocess
+
+import pytest
+
+from shmr_amd import _native
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+def _disasm(lib_path, tmp_path):
+    objcopy, bundler, objdump = (os.path.join(LLVM, n) for n in ("llvm-objcopy", "clang-offload-bundler",
+                                                                  "llvm-objdump"))
+    if not all(os.path.exists(x) for x in (objcopy, bundler, objdump)):
+        pytest.skip("ROCm LLVM tools not available")
+    fb, co = str(tmp_path / "lib.fatbin"), str(tmp_path / "lib.co")
+    subprocess.check_call([objcopy, f"--dump-section=.hip_fatbin={fb}", lib_path, str(tmp_path / "discard")])
+    subprocess.check_call([bundler, "--unbundle", "--type=o", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950",
+                           f"--input={fb}", f"--output={co}"])
+    text = subprocess.check_output([objdump, "-d", co], text=True)
+    kernels, cur = {}, None
+    for line in text.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(.*)>:", line)
+        if m:
+            cur = m.group(1)
+            kernels[cur] = []
+        elif cur and line.startswith("\t"):
+            ins = line.split("//")[0].strip()
+            if ins:
+                kernels[cur].append(ins)
+    return kernels
+
+
+@pytest.fixture(scope="module")
+def product_kernels(tmp_path_factory):
+    return _disasm(_native._PATHS["product"], tmp_path_factory.mktemp("isa"))
+
+
+def _apply_kernels(kernels):
+    out = {}
+    for name, body in kernels.items():
+        m = re.search(r"gf_apply_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E", name)
+        if m:
+            out[tuple(int(x) for x in m.groups())] = body
+    return out
+
+
+KFUSE, KPTRS, KSC1, KNTSTORE = 1 << 18, 1 << 19, 1 << 23, 2
+
+
+def test_full_tile_kernels_use_dwordx4(product_kernels):
+    """Every full-tile (MODE 0) kernel without the bounds-checked tail form
+    moves shard data only with 16-byte vector loads and stores."""
+    kern = _apply_kernels(product_kernels)
+    full = {key: body for key, body in kern.items() if key[2] == 0 and not key[3] & KFUSE}
+    assert len(full) >= 40, len(full)
+    for (R, U, mode, F), body in full.items():
+        ops = [i.split()[0] for i in body]
+        assert "global_load_dwordx4" in ops, (R, U, F)
+        assert "global_store_dwordx4" in ops, (R, U, F)
+        # no byte accesses at all; 16-bit loads only read the plan's u16 shard
+        # indices (stage_plan), never shard data
+        narrow = [o for o in ops if re.fullmatch(r"(global|flat|buffer)_(load_(ubyte|sbyte)|store_(byte|short))\w*", o)]
+        assert not narrow, ((R, U, F), narrow[:4])
+        # data stores: R outputs x U chunks per lane, all 16-byte
+        stores = [o for o in ops if o.startswith("global_store")]
+        assert set(stores) == {"global_store_dwordx4"}, ((R, U, F), set(stores))
+
+
+def test_store_cache_policy(product_kernels):
+    """sc1 kernels (compact rebuilt-shard outputs) store with sc1 and never nt;
+    nontemporal-store kernels store with nt."""
+    kern = _apply_kernels(product_kernels)
+    sc1 = [(k, b) for k, b in kern.items() if k[2] == 0 and k[3] & KSC1]
+    nt = [(k, b) for k, b in kern.items() if k[2] == 0 and k[3] & KNTSTORE and not k[3] & KFUSE]
+    assert sc1 and nt
+    for key, body in sc1:
+        st = [i for i in body if i.startswith("global_store_dwordx4")]
+        assert st and all(i.endswith(" sc1") for i in st), (key, st[:2])
+    for key, body in nt:
+        st = [i for i in body if i.startswith("global_store_dwordx4")]
+        assert st and all(re.search(r"\bnt\b", i) for i in st), (key, st[:2])
+
+
+def test_misaligned_path_kernels_exist(product_kernels):
+    """The realigning fallback (MODE 3) and the byte-granular remainder (MODE 2)
+    exist for every row count."""
+    kern = _apply_kernels(product_kernels)
+    for R in (1, 2, 3, 4):
+        assert any(k[0] == R and k[2] == 3 for k in kern), R
+        assert any(k[0] == R and k[2] == 2 for k in kern), R

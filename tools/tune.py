@@ -51,6 +51,8 @@ def main():
     ap.add_argument("--diag", action="store_true", help="also time the XOR-only ceiling kernel")
     ap.add_argument("--ref", action="store_true", help="also time torch copy / xor references")
     ap.add_argument("--same-pattern", action="store_true", help="decode: every block loses the same shards")
+    ap.add_argument("--compact", action="store_true",
+                    help="decode: rebuild into a compact [B][erasures][pitch] output (reconstruct_batch_dev_out)")
     a = ap.parse_args()
     if a.config in CFG:
         k, p, block, er, B = CFG[a.config]
@@ -92,11 +94,17 @@ def main():
             for j in range(er):   # {b, b+3, b+6, b+9} mod n (n = 10, or k+p if smaller): distinct for n >= 3*er - 2
                 present[rows, (b + 3 * j) % n] = 0
         algo = B * (k + er) * S
+        if a.compact:
+            out = torch.zeros((B, er, pitch), dtype=torch.uint8, device=dev)
+            shards[torch.from_numpy(present == 0).to(dev)] = 0
 
-        def run():
-            rs.reconstruct_batch_dev(shards, present, shard_len=S)
+            def run():
+                rs.reconstruct_batch_dev_out(shards, present, out, shard_len=S)
+        else:
+            def run():
+                rs.reconstruct_batch_dev(shards, present, shard_len=S)
     base = {"chunks": 1, "nt_load": 0, "nt_store": 0, "occ8": 0, "grid": -1, "diag": 0, "depth": 3, "wgs_per_cu": 0, "occ": 0, "early": 0, "spre": 0,
-            "threads": 256, "fuse_tail": 0, "glds": 0, "serial": 0, "uvec": -2}
+            "threads": 256, "fuse_tail": 0, "glds": 0, "serial": 0, "uvec": -2, "sc1_store": 0}
     variants = []
     for spec in a.variants.split(";"):
         kn = dict(base)
