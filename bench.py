@@ -32,7 +32,7 @@ sys.path.insert(0, HERE)
 
 # torch and shmr_amd are imported by the worker only (run()): the launcher
 # parent of `--gpus N` must not touch the GPU before it starts its children.
-np = torch = dist = shmr_amd = placement = None
+np = torch = dist = shmr_amd = placement = _native = None
 
 METRIC = "GiB/s erasure-encoded (device-resident), RS(8,3) 4 MiB StorageBlocks, 1/2/4/8 GPUs"
 HBM_PEAK = 8.0e12          # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -88,6 +88,10 @@ def parse():
                          "separate compact [blocks][erasures][pitch] output -- the crate's semantics, every None "
                          "shard rebuilt into a fresh buffer (reference src/vfs/block.rs:556-565; "
                          "shmr_ec_reconstruct_batch_dev_out)")
+    ap.add_argument("--process-model", default="process", choices=["process", "single"],
+                    help="process: one process per GPU (torchrun, or self-spawned for --gpus N); single: one "
+                         "process drives all N GPUs with one host thread + stream each (the reference daemon's "
+                         "shape, src/lib.rs:36-59)")
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher rehearsal without a GPU: ranks join the process group, exchange their "
                          "identities and rank 0 prints one JSON line (tests/test_bench_launch.py)")
@@ -158,6 +162,10 @@ def launch_check(args) -> None:
 
 def main():
     args = parse()
+    if args.process_model == "single":
+        if "WORLD_SIZE" in os.environ and os.environ["WORLD_SIZE"] != "1":
+            raise SystemExit("--process-model single runs as one process (not under a launcher)")
+        return run_single(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch(args.gpus, sys.argv[1:]))
     if args.launch_check:
@@ -165,8 +173,283 @@ def main():
     run(args)
 
 
-def run(args):
-    global np, torch, dist, shmr_amd, placement
+WORKLOADS = {"encode83": "RS(8,3) encode, 4 MiB StorageBlocks, device-resident",
+             "decode83": "RS(8,3) reconstruct, 1 missing data shard (b mod 8), 4 MiB blocks",
+             "encode104": "RS(10,4) encode, 16 MiB StorageBlocks, device-resident",
+             "decode104": "RS(10,4) reconstruct, 2 erasures {b mod 10, (b+3) mod 10}, 16 MiB",
+             "encode42": "RS(4,2) encode, 1 MiB StorageBlocks, device-resident",
+             "codec104": "RS(10,4) encode + reconstruct of 2 erasures {b mod 10, (b+3) mod 10} per step, 16 MiB"}
+
+
+class Shape:
+    """The configuration's arithmetic and HBM layout (same on every device)."""
+
+    def __init__(self, args):
+        k, p, block_bytes, erasures = CONFIGS[args.config]
+        self.k, self.p, self.block_bytes = k, p, block_bytes
+        self.S = shmr_amd.calculate_shard_size(block_bytes, k)
+        self.B = args.blocks or (1024 if block_bytes <= (1 << 20) else 512 if block_bytes <= (4 << 20) else 64)
+        self.codec = erasures is not None and erasures < 0
+        self.erasures = -erasures if self.codec else erasures
+        self.compact = self.erasures is not None and args.rebuild_out == "compact"
+        rows = p if self.erasures is None else self.erasures
+        self.tuning = shmr_amd.describe_variant(0 if self.erasures is None else 2 if self.compact else 1, k, rows)
+        if self.codec:
+            self.tuning = f"encode: {shmr_amd.describe_variant(False, k, p)}; reconstruct: {self.tuning}"
+        # HBM layout: shard i of block b at (b*k + i) * pitch with pitch = S
+        # rounded up to 4 KiB, plus one 4 KiB page when that is a multiple of
+        # 64 KiB: S = 524,288 (RS(8,3) 4 MiB) gets 528,384-byte slots (0.8 %
+        # padding) instead of the reference's contiguous block buffer, whose
+        # 2^19 shard stride measured 1.8 points of HBM peak slower (DESIGN.md
+        # section 4); S = 1,677,722 (RS(10,4) 16 MiB) gets the page-aligned
+        # 1,679,360-byte slots (0.1 %) and no page.
+        a = max(1, args.pitch_align)          # 1: pitch = S, the reference's packing (any alignment)
+        pitch = (self.S + a - 1) // a * a
+        pad = args.pitch_pad
+        if pad < 0:
+            pad = 0 if a == 1 else (4096 if pitch % 65536 == 0 else 0)
+        self.pitch = pitch + pad
+        S, e = self.S, self.erasures
+        self.algo_bytes_per_block = (k + p) * S if e is None else (k + e) * S + ((k + p) * S if self.codec else 0)
+        self.payload_bytes_per_block = k * S
+
+
+class Workload:
+    """One device's batch: B whole blocks (global blocks rank + j * world,
+    j < B: weak scaling, round-robin), synthetic data generated on the device,
+    and the step that runs the hot path over all of them on `stream`."""
+
+    def __init__(self, args, shape, dev, rank, world, rs, stream):
+        self.shape, self.dev, self.rank, self.rs, self.stream = shape, dev, rank, rs, stream
+        self.bufs = []
+        k, p, S, B, pitch = shape.k, shape.p, shape.S, shape.B, shape.pitch
+        g = torch.Generator(device=dev)
+        g.manual_seed(SEED + rank)
+        self.args = args
+        with torch.cuda.device(dev), torch.cuda.stream(stream):
+            if shape.erasures is None:
+                self.data = self.vram((B, k, pitch))
+                self.data.copy_(torch.randint(0, 256, (B, k, pitch), dtype=torch.uint8, device=dev, generator=g))
+                self.parity = self.vram((B, p, pitch))
+            else:
+                e = shape.erasures
+                self.shards = self.vram((B, k + p, pitch))
+                self.shards.zero_()
+                self.shards[:, :k, :S] = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=dev, generator=g)
+                rs.encode_batch_dev(self.shards[:, :k], self.shards[:, k:], shard_len=S,
+                                    data_shard_pitch=pitch, parity_shard_pitch=pitch)
+                present = np.ones((B, k + p), dtype=np.uint8)
+                gb = np.array(placement.weak_batch(B, rank, world))         # global block ids of this device
+                if e == 1:
+                    present[np.arange(B), gb % k] = 0                      # SURVEY 8(d) config 3
+                else:
+                    present[np.arange(B), gb % 10] = 0                     # config 4: {b%10, (b+3)%10}
+                    present[np.arange(B), (gb + 3) % 10] = 0
+                self.present = present
+                self.erased = torch.from_numpy(present == 0).to(dev)
+                self.rebuilt = None
+                self.reference = self.shards[:, :, :S].clone() if shape.codec else None
+                if shape.compact:
+                    # rebuilt shards into their own [B][erasures][pitch] array; the
+                    # erased slots of the block buffer are zeroed and never read
+                    self.rebuilt = self.vram((B, e, pitch))
+                    self.rebuilt.zero_()
+                    self.originals = self.shards[self.erased][:, :S].clone().view(B, e, S)
+                    self.shards[self.erased] = 0
+        torch.cuda.synchronize(dev)
+
+    def vram(self, shape):
+        """Batch tensor: torch's allocator, or with --contig physically
+        contiguous VRAM from shmr_ec_device_alloc (DESIGN.md §6, footprint)."""
+        if not self.args.contig:
+            return torch.empty(shape, dtype=torch.uint8, device=self.dev)
+        self.bufs.append(shmr_amd.DeviceBuffer(int(np.prod(shape)), device=self.dev.index, contiguous=True))
+        return self.bufs[-1].tensor(shape)
+
+    def encode(self):
+        sh = self.shape
+        if sh.erasures is None:
+            self.rs.encode_batch_dev(self.data, self.parity, shard_len=sh.S)
+        else:
+            self.rs.encode_batch_dev(self.shards[:, :sh.k], self.shards[:, sh.k:], shard_len=sh.S,
+                                     data_shard_pitch=sh.pitch, parity_shard_pitch=sh.pitch)
+
+    def rebuild(self):
+        if self.shape.compact:
+            self.rs.reconstruct_batch_dev_out(self.shards, self.present, self.rebuilt, shard_len=self.shape.S)
+        else:
+            self.rs.reconstruct_batch_dev(self.shards, self.present, shard_len=self.shape.S)
+
+    def step(self):
+        """One pass of the hot path over the whole batch (enqueued on the
+        current stream, which the callers set to self.stream)."""
+        if self.shape.erasures is None:
+            self.encode()
+        elif self.shape.codec:
+            # encode, then rebuild the erased shards: two launches per step,
+            # algorithmic bytes of both ((k+p)S + (k+e)S per block)
+            self.encode()
+            self.rebuild()
+        else:
+            self.rebuild()
+
+    def ramp_and_warmup(self):
+        """Untimed clock ramp: the same step until ramp_seconds of wall time
+        have passed (measured: with only 5 warmup steps, ~2 ms of work, the
+        first timed steps run 10-15 % slow while the GPU clock ramps up), then
+        the W warmup steps."""
+        n, t = 0, time.perf_counter()
+        with torch.cuda.device(self.dev), torch.cuda.stream(self.stream):
+            while time.perf_counter() - t < self.args.ramp_seconds:
+                for _ in range(8):
+                    self.step()
+                n += 8
+                self.stream.synchronize()
+            for _ in range(self.args.warmup):
+                self.step()
+            self.stream.synchronize()
+        return n
+
+    def timed(self, steps):
+        """K steps bracketed by HIP events on this device's stream; returns the
+        per-step times in ms (the stream is drained on return)."""
+        with torch.cuda.device(self.dev), torch.cuda.stream(self.stream):
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+            evs[0].record(self.stream)
+            for i in range(steps):
+                self.step()
+                evs[i + 1].record(self.stream)
+            self.stream.synchronize()
+        return [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)]
+
+    def round_trip(self):
+        """codec configs: the timed steps ran over already-consistent blocks --
+        wipe the parity, encode, wipe the erased shards, rebuild them, and check
+        every shard against the originals (device-side comparison)."""
+        sh = self.shape
+        with torch.cuda.device(self.dev), torch.cuda.stream(self.stream):
+            self.shards[:, sh.k:] = 0
+            self.encode()
+            self.shards[self.erased] = 0
+            if sh.compact:
+                self.rebuilt.zero_()
+            self.rebuild()
+            self.stream.synchronize()
+            if sh.compact:
+                ok = bool(torch.equal(self.rebuilt[:, :, :sh.S], self.originals)) and bool(
+                    torch.equal(self.shards[~self.erased][:, :sh.S], self.reference[~self.erased]))
+            else:
+                ok = bool(torch.equal(self.shards[:, :, :sh.S], self.reference))
+        return ok
+
+
+def device_identity(dev, rank):
+    props = torch.cuda.get_device_properties(dev)
+    return {"rank": rank, "device": dev.index,
+            "pci_bus_id": f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}",
+            "name": props.name}
+
+
+def report(args, shape, world, ranks, elapsed, step_ms, ramp_steps, process_model, extra=None):
+    """The one JSON line: value = payload of every block of every device over
+    `elapsed` (max over devices); the roofline is the slowest device's."""
+    B = shape.B
+    value = shape.payload_bytes_per_block * B * world * args.steps / elapsed / 2 ** 30
+    kern_s = float(np.mean(step_ms)) / 1e3          # one dominant launch per step (two for codec104)
+    achieved = shape.algo_bytes_per_block * B / kern_s
+    build_id = _native.lib().shmr_ec_build_id().decode()
+    out = {
+        "metric": METRIC if args.config == "encode83" else f"GiB/s {args.config} (device-resident)",
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "process_model": process_model,
+        "ranks_seen": len(ranks),
+        "devices": ranks,
+        "distinct_gpus": len({r["pci_bus_id"] for r in ranks}),
+        "launcher": (os.environ.get("SHMR_BENCH_LAUNCHER", "torchrun" if world > 1 else "single")
+                     if process_model == "process" else "threads"),
+        "library": {"flavour": _native.flavour(), "build_id": build_id},
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "clock_ramp": {"seconds": args.ramp_seconds, "steps": ramp_steps},
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic uniform random bytes generated on-device (torch.randint, seeded per rank)",
+        "config": {
+            "workload": WORKLOADS[args.config],
+            "data_shards": shape.k, "parity_shards": shape.p, "shard_bytes": shape.S, "blocks_per_gpu": B,
+            "global_batch_blocks": B * world,
+            "parallelism": (f"blocks round-robin over {world} GPU(s), no data-path collectives " +
+                            (f"({args.backend} only for the timing barrier / max-over-ranks)"
+                             if process_model == "process" else
+                             "(one process, one host thread + stream per GPU: the daemon's shape)")),
+            "tuning": shape.tuning,
+            "memory": ("physically contiguous VRAM (shmr_ec_device_alloc)" if args.contig
+                       else "torch caching allocator (hipMalloc)"),
+            "shard_pitch_bytes": shape.pitch,
+            "rebuild_out": (None if shape.erasures is None else
+                            "compact [blocks][erasures][pitch] output (crate semantics: a fresh buffer per None "
+                            "shard)" if shape.compact else "in place, in the erased shards' own slots"),
+            "shard_layout": ("contiguous shards (the reference's block buffer)" if shape.pitch == shape.S else
+                             f"shard slots of {shape.pitch} B for {shape.S} B shards"
+                             + (" (one 4 KiB page past the 4 KiB-aligned size for a power-of-two stride, "
+                                "DESIGN.md section 4)" if shape.pitch - shape.S >= 4096 else " (4 KiB-aligned)")),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved / 1e9, 2),
+            "peak": HBM_PEAK / 1e9,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK, 4),
+            "traffic": None,
+            "kernel_ms_avg": round(kern_s * 1e3, 4),
+            "algorithmic_bytes_per_launch": shape.algo_bytes_per_block * B,
+        },
+        "cpu_baseline": None,
+    }
+    traffic, source = load_traffic(traffic_key(args), B, build_id, shape.tuning)
+    out["roofline"]["traffic"] = traffic
+    out["roofline"]["traffic_source"] = source
+    if shape.codec:
+        # two launches per step: the roofline figures are per step (both launches)
+        out["roofline"]["launches_per_step"] = 2
+        out["roofline"]["algorithmic_bytes_per_step"] = out["roofline"].pop("algorithmic_bytes_per_launch")
+        out["roofline"]["step_ms_avg"] = out["roofline"].pop("kernel_ms_avg")
+    out.update(extra or {})
+    return out
+
+
+def cpu_leg(args, shape, w):
+    """cpu_baseline (rank 0 at N = 1 only): the oracle's restatement of the
+    crate's loops timed on this host's cores, checking the GPU's outputs of
+    the sampled blocks."""
+    k, p, S = shape.k, shape.p, shape.S
+    if shape.codec:
+        enc = cpu_baseline(k, p, S, shape.block_bytes, w.shards[:, :k], w.shards[:, k:], args.cpu_seconds / 2,
+                           args.cpu_threads)
+        dec = cpu_baseline_decode(k, p, S, w.shards, w.present, args.cpu_seconds / 2, args.cpu_threads, w.rebuilt)
+        rate = 1.0 / (1.0 / enc["value"] + 1.0 / dec["value"])
+        return {
+            "value": round(rate, 3), "unit": "GiB/s", "cores": enc["cores"], "kind": "port",
+            "sample": "encode and reconstruct legs timed separately on bounded samples of the same "
+                      "workload, combined as one step: 1 / (1/encode + 1/reconstruct); "
+                      f"encode: {enc['sample']}; reconstruct: {dec['sample']}",
+            "encode_GiBps": enc["value"], "reconstruct_GiBps": dec["value"],
+            "cpu_model": enc["cpu_model"], "cpu_quota_cores": enc["cpu_quota_cores"],
+            "gpu_parity_bit_exact_on_sample": enc["gpu_parity_bit_exact_on_sample"],
+            "gpu_rebuilt_bit_exact_on_sample": dec["gpu_rebuilt_bit_exact_on_sample"],
+        }
+    if shape.erasures is None:
+        return cpu_baseline(k, p, S, shape.block_bytes, w.data, w.parity, args.cpu_seconds, args.cpu_threads)
+    return cpu_baseline_decode(k, p, S, w.shards, w.present, args.cpu_seconds, args.cpu_threads, w.rebuilt)
+
+
+def import_runtime(args):
+    global np, torch, dist, shmr_amd, placement, _native
     import numpy as np  # noqa: F811
     import torch  # noqa: F811  (before shmr_amd: share one HIP runtime)
     import torch.distributed as dist  # noqa: F811
@@ -175,6 +458,15 @@ def run(args):
         os.environ["SHMR_EC_FLAVOUR"] = "tools"
     import shmr_amd  # noqa: F811
     from shmr_amd import _native, placement  # noqa: F811
+    for kv in filter(None, args.tune.split(",")):
+        key, val = kv.split("=")
+        shmr_amd.set_tuning(**{key: int(val)})
+
+
+def run(args):
+    """One process per GPU (torchrun or the self-launcher): this process's
+    rank encodes / rebuilds its own B blocks on its GPU."""
+    import_runtime(args)
     if args.gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE')}")
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -195,257 +487,74 @@ def run(args):
             dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    props = torch.cuda.get_device_properties(dev)
-    me = {"rank": rank, "device": local,
-          "pci_bus_id": f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}",
-          "name": props.name}
-    ranks = [me]
+    ranks = [device_identity(dev, rank)]
     if world > 1:
         ranks = [None] * dist.get_world_size()
-        dist.all_gather_object(ranks, me)      # gloo by default: identities only, no data path
+        dist.all_gather_object(ranks, device_identity(dev, rank))   # gloo by default: identities only
 
-    k, p, block_bytes, erasures = CONFIGS[args.config]
-    S = shmr_amd.calculate_shard_size(block_bytes, k)
-    B = args.blocks or (1024 if block_bytes <= (1 << 20) else 512 if block_bytes <= (4 << 20) else 64)
-    for kv in filter(None, args.tune.split(",")):
-        key, val = kv.split("=")
-        shmr_amd.set_tuning(**{key: int(val)})
-    codec = erasures is not None and erasures < 0
-    if codec:
-        erasures = -erasures
-    op = "encode" if erasures is None else "decode"
-    rows = p if erasures is None else erasures
-    compact = erasures is not None and args.rebuild_out == "compact"
-    tuning = shmr_amd.describe_variant(0 if op == "encode" else 2 if compact else 1, k, rows)
-    if codec:
-        tuning = f"encode: {shmr_amd.describe_variant(False, k, p)}; reconstruct: {tuning}"
-    rs = shmr_amd.ReedSolomon(k, p)
-
-    # Synthetic blocks, generated on the GPU from a per-rank seed (inputs
-    # resident in HBM before timing).  HBM layout: shard i of block b at
-    # (b*k + i) * pitch with pitch = S rounded up to 4 KiB, plus one 4 KiB page
-    # when that is a multiple of 64 KiB: S = 524,288 (RS(8,3) 4 MiB) gets
-    # 528,384-byte slots (0.8 % padding) instead of the reference's contiguous
-    # block buffer, whose 2^19 shard stride measured 1.8 points of HBM peak
-    # slower; S = 1,677,722 (RS(10,4) 16 MiB) gets the
-    # page-aligned 1,679,360-byte slots (0.1 %) and no page.
-    a = max(1, args.pitch_align)          # 1: pitch = S, the reference's packing (any alignment)
-    pitch = (S + a - 1) // a * a
-    pad = args.pitch_pad
-    if pad < 0:
-        pad = 0 if a == 1 else (4096 if pitch % 65536 == 0 else 0)
-    pitch += pad
-    g = torch.Generator(device=dev)
-    g.manual_seed(SEED + rank)
-    bufs = []
-
-    def vram(shape):
-        """Batch tensor: torch's allocator, or with --contig physically
-        contiguous VRAM from shmr_ec_device_alloc (DESIGN.md §6, footprint)."""
-        if not args.contig:
-            return torch.empty(shape, dtype=torch.uint8, device=dev)
-        bufs.append(shmr_amd.DeviceBuffer(int(np.prod(shape)), device=dev.index, contiguous=True))
-        return bufs[-1].tensor(shape)
-
-    if erasures is None:
-        data = vram((B, k, pitch))
-        data.copy_(torch.randint(0, 256, (B, k, pitch), dtype=torch.uint8, device=dev, generator=g))
-        parity = vram((B, p, pitch))
-
-        def step():
-            rs.encode_batch_dev(data, parity, shard_len=S)
-        algo_bytes_per_block = (k + p) * S
-        payload_bytes_per_block = k * S
-    else:
-        shards = vram((B, k + p, pitch))
-        shards.zero_()
-        shards[:, :k, :S] = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=dev, generator=g)
-        rs.encode_batch_dev(shards[:, :k], shards[:, k:], shard_len=S,
-                            data_shard_pitch=pitch, parity_shard_pitch=pitch)
-        present = np.ones((B, k + p), dtype=np.uint8)
-        gb = np.array(placement.weak_batch(B, rank, world))         # global block ids of this rank
-        if erasures == 1:
-            present[np.arange(B), gb % k] = 0                      # SURVEY 8(d) config 3
-        else:
-            present[np.arange(B), gb % 10] = 0                     # config 4: {b%10, (b+3)%10}
-            present[np.arange(B), (gb + 3) % 10] = 0
-        rebuilt = None
-        if compact:
-            # rebuilt shards into their own [B][erasures][pitch] array; the
-            # erased slots of the block buffer are zeroed and never read
-            rebuilt = vram((B, erasures, pitch))
-            rebuilt.zero_()
-            originals = shards[torch.from_numpy(present == 0).to(dev)][:, :S].clone().view(B, erasures, S)
-            shards[torch.from_numpy(present == 0).to(dev)] = 0
-
-        def rebuild():
-            if compact:
-                rs.reconstruct_batch_dev_out(shards, present, rebuilt, shard_len=S)
-            else:
-                rs.reconstruct_batch_dev(shards, present, shard_len=S)
-
-        if codec:
-            # encode, then rebuild the erased shards in place: two launches per
-            # step, algorithmic bytes of both ((k+p)S + (k+e)S per block)
-            reference = shards[:, :, :S].clone()
-
-            def step():
-                rs.encode_batch_dev(shards[:, :k], shards[:, k:], shard_len=S,
-                                    data_shard_pitch=pitch, parity_shard_pitch=pitch)
-                rebuild()
-            algo_bytes_per_block = (k + p) * S + (k + erasures) * S
-        else:
-            step = rebuild
-            algo_bytes_per_block = (k + erasures) * S
-        payload_bytes_per_block = k * S
-    torch.cuda.synchronize(dev)
-
-    stream = torch.cuda.current_stream(dev)
-    # Untimed clock ramp: run the same step until ramp_seconds of wall time
-    # have passed (measured: with only 5 warmup steps, ~2 ms of work, the
-    # first timed steps run 10-15 % slow while the GPU clock ramps up).
-    ramp_steps, t_ramp = 0, time.perf_counter()
-    while time.perf_counter() - t_ramp < args.ramp_seconds:
-        for _ in range(8):
-            step()
-        ramp_steps += 8
-        torch.cuda.synchronize(dev)
-    for _ in range(args.warmup):
-        step()
+    shape = Shape(args)
+    rs = shmr_amd.ReedSolomon(shape.k, shape.p)
+    w = Workload(args, shape, dev, rank, world, rs, torch.cuda.current_stream(dev))
+    ramp_steps = w.ramp_and_warmup()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    evs[0].record(stream)
-    for i in range(args.steps):
-        step()
-        evs[i + 1].record(stream)
+    step_ms = w.timed(args.steps)
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
-    gpu_s = sum(step_ms) / 1e3
-    elapsed = max(wall, gpu_s)
+    elapsed = max(wall, sum(step_ms) / 1e3)
     elapsed = placement.max_over_ranks(elapsed, device=dev if args.backend == "nccl" else None)
-
-    total_payload = payload_bytes_per_block * B * world * args.steps
-    value = total_payload / elapsed / 2 ** 30
-    kern_s = float(np.mean(step_ms)) / 1e3          # one dominant launch per step
-    achieved = algo_bytes_per_block * B / kern_s
-    out = {
-        "metric": METRIC if args.config == "encode83" else f"GiB/s {args.config} (device-resident)",
-        "value": round(value, 3),
-        "unit": "GiB/s",
-        "n_gpus": world,
-        "ranks_seen": len(ranks),
-        "devices": ranks,
-        "distinct_gpus": len({r["pci_bus_id"] for r in ranks}),
-        "launcher": os.environ.get("SHMR_BENCH_LAUNCHER", "torchrun" if world > 1 else "single"),
-        "library": {"flavour": _native.flavour(), "build_id": _native.lib().shmr_ec_build_id().decode()},
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "clock_ramp": {"seconds": args.ramp_seconds, "steps": ramp_steps},
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic uniform random bytes generated on-device (torch.randint, seeded per rank)",
-        "config": {
-            "workload": {"encode83": "RS(8,3) encode, 4 MiB StorageBlocks, device-resident",
-                         "decode83": "RS(8,3) reconstruct, 1 missing data shard (b mod 8), 4 MiB blocks",
-                         "encode104": "RS(10,4) encode, 16 MiB StorageBlocks, device-resident",
-                         "decode104": "RS(10,4) reconstruct, 2 erasures {b mod 10, (b+3) mod 10}, 16 MiB",
-                         "encode42": "RS(4,2) encode, 1 MiB StorageBlocks, device-resident",
-                         "codec104": "RS(10,4) encode + reconstruct of 2 erasures {b mod 10, (b+3) mod 10} "
-                                     "per step, 16 MiB"}[args.config],
-            "data_shards": k, "parity_shards": p, "shard_bytes": S, "blocks_per_gpu": B,
-            "global_batch_blocks": B * world,
-            "parallelism": f"blocks round-robin over {world} GPU(s), no data-path collectives "
-                           f"({args.backend} only for the timing barrier / max-over-ranks)",
-            "tuning": tuning,
-            "memory": "physically contiguous VRAM (shmr_ec_device_alloc)" if args.contig else "torch caching allocator (hipMalloc)",
-            "shard_pitch_bytes": pitch,
-            "rebuild_out": (None if erasures is None else
-                            "compact [blocks][erasures][pitch] output (crate semantics: a fresh buffer per None "
-                            "shard)" if compact else "in place, in the erased shards' own slots"),
-            "shard_layout": ("contiguous shards (the reference's block buffer)" if pitch == S else
-                             f"shard slots of {pitch} B for {S} B shards"
-                             + (" (one 4 KiB page past the 4 KiB-aligned size for a power-of-two stride, "
-                                "DESIGN.md section 4)" if pitch - S >= 4096 else " (4 KiB-aligned)")),
-        },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": round(achieved / 1e9, 2),
-            "peak": HBM_PEAK / 1e9,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK, 4),
-            "traffic": None,
-            "kernel_ms_avg": round(kern_s * 1e3, 4),
-            "algorithmic_bytes_per_launch": algo_bytes_per_block * B,
-        },
-        "cpu_baseline": None,
-    }
-    traffic, source = load_traffic(traffic_key(args), B, out["library"]["build_id"], tuning)
-    out["roofline"]["traffic"] = traffic
-    out["roofline"]["traffic_source"] = source
-    if codec:
-        # two launches per step: the roofline figures are per step (both launches)
-        out["roofline"]["launches_per_step"] = 2
-        out["roofline"]["algorithmic_bytes_per_step"] = out["roofline"].pop("algorithmic_bytes_per_launch")
-        out["roofline"]["step_ms_avg"] = out["roofline"].pop("kernel_ms_avg")
-        # the timed steps ran over already-consistent blocks: wipe the parity,
-        # encode, wipe the erased shards, rebuild them, and check every shard
-        # against the originals
-        erased = torch.from_numpy(present == 0).to(dev)
-        shards[:, k:] = 0
-        rs.encode_batch_dev(shards[:, :k], shards[:, k:], shard_len=S,
-                            data_shard_pitch=pitch, parity_shard_pitch=pitch)
-        if compact:
-            # the encode rewrote the erased parity slots: clear them again
-            shards[erased] = 0
-            rebuilt.zero_()
-            rebuild()
-            torch.cuda.synchronize(dev)
-            ok = bool(torch.equal(rebuilt[:, :, :S], originals)) and bool(
-                torch.equal(shards[~erased][:, :S], reference[~erased]))
-        else:
-            shards[erased] = 0
-            rebuild()
-            torch.cuda.synchronize(dev)
-            ok = bool(torch.equal(shards[:, :, :S], reference))
-        out["roofline"]["round_trip_bit_exact"] = ok
-        del reference
+    out = report(args, shape, world, ranks, elapsed, step_ms, ramp_steps, "process")
+    if shape.codec:
+        out["roofline"]["round_trip_bit_exact"] = w.round_trip()
     if rank == 0 and world == 1 and not args.no_cpu:
-        if codec:
-            enc = cpu_baseline(k, p, S, block_bytes, shards[:, :k], shards[:, k:], args.cpu_seconds / 2,
-                               args.cpu_threads)
-            dec = cpu_baseline_decode(k, p, S, shards, present, args.cpu_seconds / 2, args.cpu_threads,
-                                      rebuilt)
-            rate = 1.0 / (1.0 / enc["value"] + 1.0 / dec["value"])
-            out["cpu_baseline"] = {
-                "value": round(rate, 3), "unit": "GiB/s", "cores": enc["cores"], "kind": "port",
-                "sample": "encode and reconstruct legs timed separately on bounded samples of the same "
-                          "workload, combined as one step: 1 / (1/encode + 1/reconstruct); "
-                          f"encode: {enc['sample']}; reconstruct: {dec['sample']}",
-                "encode_GiBps": enc["value"], "reconstruct_GiBps": dec["value"],
-                "cpu_model": enc["cpu_model"], "cpu_quota_cores": enc["cpu_quota_cores"],
-                "gpu_parity_bit_exact_on_sample": enc["gpu_parity_bit_exact_on_sample"],
-                "gpu_rebuilt_bit_exact_on_sample": dec["gpu_rebuilt_bit_exact_on_sample"],
-            }
-        elif erasures is None:
-            out["cpu_baseline"] = cpu_baseline(k, p, S, block_bytes, data, parity, args.cpu_seconds, args.cpu_threads)
-        else:
-            out["cpu_baseline"] = cpu_baseline_decode(k, p, S, shards, present, args.cpu_seconds, args.cpu_threads,
-                                                      rebuilt)
+        out["cpu_baseline"] = cpu_leg(args, shape, w)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def run_single(args):
+    """The reference daemon's process model (src/lib.rs:36-59: one process;
+    rayon fans blocks out, src/vfs/mod.rs:93-96): one process drives N GPUs,
+    one host thread + HIP stream per GPU, whole blocks round-robin (device d
+    owns global blocks d + j * N).  Aggregate = all devices' data / the slowest
+    device's time (per-device HIP events, and the wall clock around all)."""
+    import_runtime(args)
+    n = args.gpus
+    ndev = torch.cuda.device_count()
+    if n > ndev and os.environ.get("SHMR_BENCH_SHARE_GPU") != "1":
+        raise SystemExit(f"--gpus {n} but only {ndev} GPU(s) visible")
+    devs = [torch.device("cuda", d % ndev) for d in range(n)]
+    shape = Shape(args)
+    rs = shmr_amd.ReedSolomon(shape.k, shape.p)
+    for d in sorted({x.index for x in devs}):
+        shmr_amd.device_init(d)                   # one-time per-device state, outside the timed region
+    works = []
+    for d, dev in enumerate(devs):
+        works.append(Workload(args, shape, dev, d, n, rs, torch.cuda.Stream(device=dev)))
+    ranks = [device_identity(dev, d) for d, dev in enumerate(devs)]
+    results, wall = placement.fan_out([w.ramp_and_warmup for w in works], [lambda w=w: w.timed(args.steps)
+                                                                             for w in works])
+    ramp_steps = max(r[0] for r in results)
+    per_dev_ms = [r[1] for r in results]
+    dev_s = [sum(ms) / 1e3 for ms in per_dev_ms]
+    slowest = int(np.argmax(dev_s))
+    elapsed = max(wall, max(dev_s))
+    extra = {"per_device": [{"device": ranks[d], "ms_per_step": round(dev_s[d] / args.steps * 1e3, 4),
+                             "frac": round(shape.algo_bytes_per_block * shape.B / (float(np.mean(per_dev_ms[d])) / 1e3)
+                                           / HBM_PEAK, 4)} for d in range(n)]}
+    out = report(args, shape, n, ranks, elapsed, per_dev_ms[slowest], ramp_steps, "single", extra)
+    if shape.codec:
+        out["roofline"]["round_trip_bit_exact"] = all(w.round_trip() for w in works)
+    if n == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_leg(args, shape, works[0])
+    print(json.dumps(out), flush=True)
 
 
 def traffic_key(args) -> str:

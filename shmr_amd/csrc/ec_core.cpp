@@ -37,6 +37,7 @@ struct Tuning {
     std::atomic<int> glds{kAuto};
     std::atomic<int> serial{kAuto};
     std::atomic<int> sc1_store{kAuto};
+    std::atomic<int> realign{kAuto};
 };
 Tuning g_tune[2];   // [kEncode], [kDecode]
 std::atomic<int> g_bounce_kib{kBounceKibDefault};
@@ -189,7 +190,7 @@ int set_tuning(const char* key, int value) {
             {"chunks", kAuto}, {"nt_load", kAuto}, {"nt_store", kAuto}, {"occ8", 0},
             {"grid", -1},      {"diag", 0},        {"threads", 256},    {"depth", kAuto},   {"wgs_per_cu", kAuto},
             {"occ", kAuto},    {"early", kAuto},   {"spre", kAuto},     {"fuse_tail", kAuto},
-            {"glds", kAuto},   {"serial", kAuto},   {"sc1_store", kAuto}};
+            {"glds", kAuto},   {"serial", kAuto},   {"sc1_store", kAuto}, {"realign", kAuto}};
         const auto it = kDefaults.find(k);
         return (it != kDefaults.end() && it->second == value) ? SHMR_EC_OK : SHMR_EC_INVALID_ARGUMENT;
     }
@@ -234,6 +235,8 @@ int set_tuning(const char* key, int value) {
             T.serial = value == kAuto ? kAuto : (value != 0);
         } else if (k == "sc1_store") {
             T.sc1_store = value == kAuto ? kAuto : (value != 0);
+        } else if (k == "realign") {
+            T.realign = value == kAuto ? kAuto : (value != 0);
         } else {
             return SHMR_EC_INVALID_ARGUMENT;
         }
@@ -268,6 +271,7 @@ int get_tuning(const char* key) {
     if (k == "glds") return T.glds;
     if (k == "serial") return T.serial;
     if (k == "sc1_store") return T.sc1_store;
+    if (k == "realign") return T.realign;
     return SHMR_EC_INVALID_ARGUMENT;
 }
 
@@ -625,15 +629,29 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
     // device at init; every access still covers only the lane's own bytes),
     // else the realigning kernel below.  Mapped host shards never do: the
     // probe covered device memory only.
-    const bool aligned = ptrs ? L.ptrs_aligned
-                              : (aligned16(uintptr_t(L.in_base)) && aligned16(uintptr_t(L.out_base)) &&
-                                 aligned16(L.in_bpitch) && aligned16(L.in_spitch) && aligned16(L.out_bpitch) &&
-                                 aligned16(L.out_spitch)) ||
-                                    (!L.host_mapped && unaligned_vector(dev));
+    const bool out16 = aligned16(uintptr_t(L.out_base)) && aligned16(L.out_bpitch) && aligned16(L.out_spitch);
+    const bool aligned16_all =
+        ptrs ? L.ptrs_aligned
+             : aligned16(uintptr_t(L.in_base)) && aligned16(L.in_bpitch) && aligned16(L.in_spitch) && out16;
+    const bool aligned = aligned16_all || (!ptrs && !L.host_mapped && unaligned_vector(dev));
     for (uint32_t row0 = 0; row0 < plan.m; row0 += kern::kMaxRowsPerLaunch) {
         const uint32_t rows = std::min<uint32_t>(kern::kMaxRowsPerLaunch, plan.m - row0);
         count_device(dev, kDevLaunches);
         kern::Variant var = launch_variant(op, plan.k, rows, L.host_mapped, ptrs, bs.segs != nullptr, L.compact);
+        // Misaligned shards on a device with unaligned vector access: the
+        // policy's kernels as they are, or (knob "realign", tools build) the
+        // realigning-load form of the plain tile
+        if (!aligned16_all && g_tune[op].realign.load() == 1 && !ptrs) {
+            var.realign = true;
+            var.early = var.spre = var.glds = false;
+        }
+        // sc1 stores are raw buffer stores: a 2 GiB resource per output row,
+        // and 16-byte aligned outputs only (the unaligned-access probe covers
+        // the global instructions); otherwise nontemporal global stores
+        if (var.sc1_store && (len >= (uint64_t(1) << 31) - 4096 || ptrs || !out16)) {
+            var.sc1_store = false;
+            var.nt_store = true;
+        }
         const uint64_t tb = kern::tile_bytes(var.u, var.threads);
         kern::ApplyArgs a{};
         a.in_base = L.in_base;

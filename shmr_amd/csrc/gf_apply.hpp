@@ -94,6 +94,7 @@ struct Variant {
     bool glds = false;       // input ring in LDS filled by LDS-DMA (depth = slots; full tiles only)
     bool serial = false;     // GF math one dword at a time (fewer live registers, more waves)
     bool sc1_store = false;  // stores with the sc1 cache policy instead of nontemporal
+    bool realign = false;    // misaligned shards: aligned loads realigned across lanes (DPP), unaligned stores
 };
 
 // rows in [1, kMaxRowsPerLaunch].  mode 0: full tiles, every shard base

@@ -55,6 +55,12 @@ constexpr int kSerial = 1 << 22;
 // Stores with the sc1 cache policy instead of nontemporal (compact rebuilt-
 // shard outputs: a separate, densely written array).
 constexpr int kSc1Store = 1 << 23;
+// Shards off 16-byte alignment (the reference's packed block buffer): every
+// lane loads its ALIGNED 16-byte chunk, takes the next lane's leading bytes
+// with a DPP wavefront shift (v_mov_b32_dpp wave_shl:1) and realigns in
+// registers; only lane 63 loads one more chunk (the next wave's first).
+// Stores stay unaligned 16-byte vector stores (probe-verified device only).
+constexpr int kRealign = 1 << 24;
 // Bits 12-15: occupancy target in waves per SIMD (0 = compiler's choice);
 // the register allocator must then fit 512 / target VGPRs.
 constexpr int kOccShift = 12;
@@ -121,15 +127,30 @@ __device__ __forceinline__ u32x4 load16(const uint8_t* p) {
 
 template <int F>
 __device__ __forceinline__ void store16(uint8_t* p, u32x4 v) {
-    if constexpr ((F & kSc1Store) != 0) {
-        // global_store_dwordx4 with the sc1 policy bit (no builtin takes the
-        // cache-policy bits of a global store).  The last use of v: nothing
-        // after the tile's stores depends on them.
-        asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(v) : "memory");
-    } else if constexpr ((F & kNtStore) != 0) {
+    if constexpr ((F & kNtStore) != 0) {
         __builtin_nontemporal_store(v, reinterpret_cast<u32x4_u*>(p));
     } else {
         *reinterpret_cast<u32x4_u*>(p) = v;
+    }
+}
+
+// 16-byte store at column col of a wave-uniform output row.  kSc1Store: a raw
+// buffer store with the sc1 cache-policy bit (aux 16; no global-store builtin
+// takes policy bits, and an inline-asm store would hide the >8-byte store-data
+// hazard from the compiler).  The resource covers 2 GiB from the row base:
+// the policy keeps sc1 to shards shorter than that (ec_core launch_set).
+template <int F>
+__device__ __forceinline__ void store16_row(uint8_t* row, uint64_t col, u32x4 v) {
+    if constexpr ((F & kSc1Store) != 0) {
+        // (readfirstlane returns int: widen through uint32_t, never sign-extend)
+        const uint64_t a = uint64_t(uintptr_t(row));
+        const uint64_t ua = uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(a)))) |
+                            (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(a >> 32)))) << 32);
+        const __amdgpu_buffer_rsrc_t rsrc =
+            __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(uintptr_t(ua)), 0, 0x7fffffff, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, uint32_t(col), 0, 16);
+    } else {
+        store16<F>(row + col, v);
     }
 }
 
@@ -216,11 +237,11 @@ __device__ __forceinline__ void st_shifted(uint8_t* p, u32x4 v) {
 template <int MODE, int F>
 __device__ __forceinline__ void st(uint8_t* base, uint64_t col, uint64_t len, u32x4 v) {
     if constexpr (MODE == 0) {
-        store16<F>(base + col, v);
+        store16_row<F>(base, col, v);
     } else if constexpr (MODE == 3) {
         st_shifted<F>(base + col, v);
     } else if constexpr (MODE == 1) {
-        if (col + 16 <= len) store16<F>(base + col, v);
+        if (col + 16 <= len) store16_row<F>(base, col, v);
         else store_bytes(base + col, v, int64_t(len) - int64_t(col));
     } else {
         store_bytes(base + col, v, int64_t(len) - int64_t(col));
@@ -278,6 +299,85 @@ __device__ __forceinline__ void read_tabs(const Ctx& c, uint32_t t, Tab (&tb)[R]
 template <int R, int U, int F>
 __device__ __forceinline__ void glds_tile(const ApplyArgs& a, const Ctx& c, const uint8_t* ib, uint8_t* ob, uint64_t col0);
 
+// Lane L's 16 bytes at byte offset m (1..15) of the 32-byte window formed by
+// its own aligned chunk and lane L+1's; lane 63 supplies `edge` (the next
+// wave's first chunk) as its neighbour.  wave_shl:1 moves lane L+1's dword
+// to lane L; lane 63 has no source lane and keeps `edge`.
+__device__ __forceinline__ u32x4 realign_lanes(const u32x4& lo, const u32x4& edge, uint32_t m) {
+    const u32x4 nx{uint32_t(__builtin_amdgcn_update_dpp(int(edge.x), int(lo.x), 0x130, 0xf, 0xf, false)),
+                   uint32_t(__builtin_amdgcn_update_dpp(int(edge.y), int(lo.y), 0x130, 0xf, 0xf, false)),
+                   uint32_t(__builtin_amdgcn_update_dpp(int(edge.z), int(lo.z), 0x130, 0xf, 0xf, false)),
+                   uint32_t(__builtin_amdgcn_update_dpp(int(edge.w), int(lo.w), 0x130, 0xf, 0xf, false))};
+    return funnel16(lo, nx, m);
+}
+
+// Full tile (kRealign) over misaligned shards: the depth-2 register ring of
+// do_tile, each slot holding the lane's aligned chunk(s), lane 63's edge
+// chunk(s) and the shard's misalignment m (wave-uniform, a scalar).
+template <int R, int U, int F>
+__device__ __forceinline__ void realign_tile(const ApplyArgs& a, const Ctx& c, const uint8_t* ib, uint8_t* ob,
+                                             uint64_t col0) {
+    constexpr int TH = threads_of<F>();
+    constexpr int NB = 2;
+    const uint32_t k = a.k;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave0 = tid - lane;
+    uint32_t acc[U][R][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[u][r][j] = 0u;
+    u32x4 rlo[NB][U], red[NB][U];
+    uint32_t rm[NB];
+    auto load = [&](int s, uint32_t t) {
+        const uint32_t tt = t < k ? t : k - 1;
+        const uint8_t* base = ib + c.s_in_off[tt] + col0;
+        const uint32_t m = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(uintptr_t(base)) & 15u)));
+        rm[s] = m;
+        const uint8_t* al = base - m;
+#pragma unroll
+        for (int u = 0; u < U; ++u) rlo[s][u] = load16<F>(al + (uint64_t(u) * TH + tid) * 16);
+        // Lane 63's neighbour: the next wave's first chunk.  Every lane issues
+        // the same (wave-uniform) address -- one 16-byte request, and no
+        // branch around a load, which would make the compiler's wait counts
+        // merge conservatively and drain the look-ahead.  With m != 0 the chunk
+        // holds bytes of this tile; with m == 0 it is not needed and the
+        // address stays on the wave's own last chunk (never past the buffer).
+        const uint32_t edge = wave0 + (m ? 64u : 63u);
+#pragma unroll
+        for (int u = 0; u < U; ++u) red[s][u] = load16<F>(al + (uint64_t(u) * TH + edge) * 16);
+    };
+    load(0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    for (uint32_t t = 0; t < k; t += NB) {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            load((i + 1) % NB, t + i + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            if (t + i < k) {
+                Tab tb[R];
+                read_tabs<R>(c, t + i, tb);
+                const uint32_t m = rm[i];
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    mac<R, F>(acc[u], m ? realign_lanes(rlo[i][u], red[i][u], m) : rlo[i][u], tb);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        uint8_t* o = ob + c.s_out_off[r];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            store16<F>(o + col0 + (uint64_t(u) * TH + tid) * 16,
+                       u32x4{acc[u][r][0], acc[u][r][1], acc[u][r][2], acc[u][r][3]});
+    }
+}
+
 // One tile: lanes own columns col0 + (u * TH + tid) * 16, u < U.
 //
 // sched_barrier(0) pins program order: without it the scheduler sinks the
@@ -295,6 +395,10 @@ __device__ __forceinline__ void do_tile(const ApplyArgs& a, const Ctx& c, const 
                                         uint64_t col0) {
     if constexpr ((F & kGlds) != 0 && MODE == 0) {
         glds_tile<R, U, F>(a, c, ib, ob, col0);
+        return;
+    }
+    if constexpr ((F & kRealign) != 0 && MODE == 0) {
+        realign_tile<R, U, F>(a, c, ib, ob, col0);
         return;
     }
     constexpr int TH = threads_of<F>();
@@ -718,7 +822,8 @@ inline int variant_flags(const Variant& v) {
            (v.depth == 5 ? kDepth5 : 0) | (v.depth == 9 ? kDepth9 : 0) | (v.depth == 2 ? kDepth2 : 0) |
            (v.depth == 1 ? kDepth1 : 0) | ((v.occ & 15) << kOccShift) | (v.early ? kEarly : 0) |
            (v.spre ? kSPre : 0) | (v.fuse_tail ? kFuse : 0) | (v.ptrs ? kPtrs : 0) | (v.segs ? kSegs : 0) |
-           (v.glds ? kGlds : 0) | (v.serial ? kSerial : 0) | (v.sc1_store ? kSc1Store : 0);
+           (v.glds ? kGlds : 0) | (v.serial ? kSerial : 0) | (v.sc1_store ? kSc1Store : 0) |
+           (v.realign ? kRealign : 0);
 }
 
 }  // namespace

@@ -608,7 +608,7 @@ def test_device_buffer_view_keeps_buffer_alive(gpu):
 
 # ------------------------------------------------ misaligned (contiguous) layouts
 @pytest.mark.gpu
-@pytest.mark.parametrize("path", ["auto", "realign", "vector"])
+@pytest.mark.parametrize("path", ["auto", "realign", "vector", "dpp"])
 @pytest.mark.parametrize("k,p,L,B,off", [
     (10, 4, 1677722, 3, 0),      # RS(10,4) 16 MiB: the reference's block buffer, shard i at i * S
     (8, 3, 524288 + 4096 + 5, 4, 3),   # odd pitch and a misaligned base
@@ -622,17 +622,20 @@ def test_contiguous_layout_realigned(gpu, path, k, p, L, B, off):
     policy (the vector kernels on a device that passed the unaligned-access
     probe); tools build "realign" (knob uvec=0): the realigning kernel for full
     4 KiB tiles, the remainder byte-granular; "vector" (uvec=1): the vector
-    kernels unconditionally.  Encode into the buffer's parity slots, then
+    kernels unconditionally; "dpp" (uvec=1, realign=1): aligned loads realigned
+    across lanes with a DPP wavefront shift.  Encode into the buffer's parity slots, then
     rebuild two erased shards per block in place, all against the oracle;
     bytes outside the shards stay untouched."""
     if path == "auto":
         return _contiguous_layout_check(gpu, k, p, L, B, off)
     with _native.tools():
         shmr_amd.set_tuning(uvec=0 if path == "realign" else 1)
+        if path == "dpp":
+            shmr_amd.set_tuning(realign=1)
         try:
             _contiguous_layout_check(gpu, k, p, L, B, off)
         finally:
-            shmr_amd.set_tuning(uvec=-2)
+            shmr_amd.set_tuning(uvec=-2, realign=-2)
 
 
 def _contiguous_layout_check(gpu, k, p, L, B, off):

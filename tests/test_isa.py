@@ -7,7 +7,8 @@ ones.  Their 16-byte accesses go through an under-aligned vector type (well-
 defined C++ at any address); this pins that the compiler still lowers every
 full-tile kernel's data path to global_load_dwordx4 / global_store_dwordx4 --
 no byte-granular or split accesses -- and that the sc1 policy reaches the
-compact-output kernels' stores.
+compact-output kernels' stores (raw buffer stores: no global-store builtin
+takes cache-policy bits).
 """
 import os
 import re
@@ -69,14 +70,15 @@ def test_full_tile_kernels_use_dwordx4(product_kernels):
     for (R, U, mode, F), body in full.items():
         ops = [i.split()[0] for i in body]
         assert "global_load_dwordx4" in ops, (R, U, F)
-        assert "global_store_dwordx4" in ops, (R, U, F)
+        store16 = "buffer_store_dwordx4" if F & KSC1 else "global_store_dwordx4"
+        assert store16 in ops, (R, U, F)
         # no byte accesses at all; 16-bit loads only read the plan's u16 shard
         # indices (stage_plan), never shard data
         narrow = [o for o in ops if re.fullmatch(r"(global|flat|buffer)_(load_(ubyte|sbyte)|store_(byte|short))\w*", o)]
         assert not narrow, ((R, U, F), narrow[:4])
         # data stores: R outputs x U chunks per lane, all 16-byte
-        stores = [o for o in ops if o.startswith("global_store")]
-        assert set(stores) == {"global_store_dwordx4"}, ((R, U, F), set(stores))
+        stores = [o for o in ops if re.match(r"(global|buffer|flat)_store", o)]
+        assert set(stores) == {store16}, ((R, U, F), set(stores))
 
 
 def test_store_cache_policy(product_kernels):
@@ -87,8 +89,8 @@ def test_store_cache_policy(product_kernels):
     nt = [(k, b) for k, b in kern.items() if k[2] == 0 and k[3] & KNTSTORE and not k[3] & KFUSE]
     assert sc1 and nt
     for key, body in sc1:
-        st = [i for i in body if i.startswith("global_store_dwordx4")]
-        assert st and all(i.endswith(" sc1") for i in st), (key, st[:2])
+        st = [i for i in body if re.match(r"(global|buffer)_store_dwordx4", i)]
+        assert st and all(i.startswith("buffer_store_dwordx4") and i.endswith(" sc1") for i in st), (key, st[:2])
     for key, body in nt:
         st = [i for i in body if i.startswith("global_store_dwordx4")]
         assert st and all(re.search(r"\bnt\b", i) for i in st), (key, st[:2])

@@ -51,6 +51,9 @@ def main():
     ap.add_argument("--diag", action="store_true", help="also time the XOR-only ceiling kernel")
     ap.add_argument("--ref", action="store_true", help="also time torch copy / xor references")
     ap.add_argument("--same-pattern", action="store_true", help="decode: every block loses the same shards")
+    ap.add_argument("--packed", action="store_true",
+                    help="the reference's block buffer: shard i of block b at (b*(k+p) + i) * S, no padding "
+                         "(block.rs:408-419; off 16-byte alignment when S % 16 != 0)")
     ap.add_argument("--compact", action="store_true",
                     help="decode: rebuild into a compact [B][erasures][pitch] output (reconstruct_batch_dev_out)")
     a = ap.parse_args()
@@ -65,7 +68,16 @@ def main():
     rs = shmr_amd.ReedSolomon(k, p)
     g = torch.Generator(device=dev)
     g.manual_seed(1)
-    if er == 0:
+    if er == 0 and a.packed:
+        t = k + p
+        flat = torch.randint(0, 256, (B * t * S,), dtype=torch.uint8, device=dev, generator=g)
+        data = flat.as_strided((B, k, S), (t * S, S, 1))
+        parity = flat[k * S:].as_strided((B, p, S), (t * S, S, 1))
+        algo = B * (k + p) * S
+
+        def run():
+            rs.encode_batch_dev(data, parity, shard_len=S, data_shard_pitch=S, parity_shard_pitch=S)
+    elif er == 0:
         P = (S + 255) // 256 * 256 + a.pad
         if a.bpad:   # extra bytes per block pitch (block stride != k * shard pitch)
             flat = torch.randint(0, 256, (B * (k * P + a.bpad),), dtype=torch.uint8, device=dev, generator=g)
@@ -81,7 +93,7 @@ def main():
         def run():
             rs.encode_batch_dev(data, parity, shard_len=S)
     else:
-        pitch = (S + 255) // 256 * 256 + a.pad
+        pitch = S if a.packed else (S + 255) // 256 * 256 + a.pad
         shards = torch.zeros((B, k + p, pitch), dtype=torch.uint8, device=dev)
         shards[:, :k, :S] = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=dev, generator=g)
         present = np.ones((B, k + p), np.uint8)
@@ -104,7 +116,7 @@ def main():
             def run():
                 rs.reconstruct_batch_dev(shards, present, shard_len=S)
     base = {"chunks": 1, "nt_load": 0, "nt_store": 0, "occ8": 0, "grid": -1, "diag": 0, "depth": 3, "wgs_per_cu": 0, "occ": 0, "early": 0, "spre": 0,
-            "threads": 256, "fuse_tail": 0, "glds": 0, "serial": 0, "uvec": -2, "sc1_store": 0}
+            "threads": 256, "fuse_tail": 0, "glds": 0, "serial": 0, "uvec": -2, "sc1_store": 0, "realign": 0}
     variants = []
     for spec in a.variants.split(";"):
         kn = dict(base)
