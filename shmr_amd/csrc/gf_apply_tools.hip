@@ -264,7 +264,9 @@ __device__ __forceinline__ void spre_tile(const ApplyArgs& a, const uint8_t* pla
     X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kRealign | kSerial) \
     X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kRealign) \
     X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kRealign) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kRealign)
+    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kRealign) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kRealign | kSerial) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kRealign)
 
 template <int R>
 hipError_t dispatch_tools(const ApplyArgs& a, const Variant& v, int grid_cap, hipStream_t s) {
