@@ -92,6 +92,8 @@ def parse():
                     help="process: one process per GPU (torchrun, or self-spawned for --gpus N); single: one "
                          "process drives all N GPUs with one host thread + stream each (the reference daemon's "
                          "shape, src/lib.rs:36-59)")
+    ap.add_argument("--single-stream", default="own", choices=["own", "current"],
+                    help=argparse.SUPPRESS)   # single model: a stream per device, or torch's current stream (A/B)
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher rehearsal without a GPU: ranks join the process group, exchange their "
                          "identities and rank 0 prints one JSON line (tests/test_bench_launch.py)")
@@ -537,7 +539,8 @@ def run_single(args):
         shmr_amd.device_init(d)                   # one-time per-device state, outside the timed region
     works = []
     for d, dev in enumerate(devs):
-        works.append(Workload(args, shape, dev, d, n, rs, torch.cuda.Stream(device=dev)))
+        st = torch.cuda.Stream(device=dev) if args.single_stream == "own" else torch.cuda.current_stream(dev)
+        works.append(Workload(args, shape, dev, d, n, rs, st))
     ranks = [device_identity(dev, d) for d, dev in enumerate(devs)]
     results, wall = placement.fan_out([w.ramp_and_warmup for w in works], [lambda w=w: w.timed(args.steps)
                                                                              for w in works])

@@ -6,6 +6,11 @@
 //  * scalar-loaded tables and offsets, no LDS (spre_tile): -1.0 to -6.5;
 //  * the XOR-only diagnostic twin (diag_mac; WRONG results by design), the
 //    ceiling of the kernel's own access pattern;
+//  * the DPP realigning-load tile for misaligned shards (realign_tile):
+//    -2.7 / -2.7 points against the unaligned vector path on
+//    the reference's packed RS(10,4) buffer;
+//  * sc1 stores into compact rebuilt-shard outputs: -0.6 to +0.3 against
+//    nontemporal stores;
 //  * ring depths 1/3/5/9, 128/512-lane workgroups, occupancy targets and the
 //    other knob combinations of the instantiation list below.
 #include <hip/hip_runtime.h>
@@ -172,6 +177,94 @@ __device__ __forceinline__ void spre_tile(const ApplyArgs& a, const uint8_t* pla
     }
 }
 
+// Lane L's 16 bytes at byte offset m (1..15) of the 32-byte window formed by
+// its own aligned chunk and lane L+1's; lane 63 supplies `edge` (the next
+// wave's first chunk) as its neighbour.  wave_shl:1 moves lane L+1's dword
+// to lane L; lane 63 has no source lane and keeps `edge`.
+__device__ __forceinline__ u32x4 realign_lanes(const u32x4& lo, const u32x4& edge, uint32_t m) {
+    const u32x4 nx{uint32_t(__builtin_amdgcn_update_dpp(int(edge.x), int(lo.x), 0x130, 0xf, 0xf, false)),
+                   uint32_t(__builtin_amdgcn_update_dpp(int(edge.y), int(lo.y), 0x130, 0xf, 0xf, false)),
+                   uint32_t(__builtin_amdgcn_update_dpp(int(edge.z), int(lo.z), 0x130, 0xf, 0xf, false)),
+                   uint32_t(__builtin_amdgcn_update_dpp(int(edge.w), int(lo.w), 0x130, 0xf, 0xf, false))};
+    return funnel16(lo, nx, m);
+}
+
+// ---- realigning-load tile (flag kRealign) --------------------------------
+// Shards off 16-byte alignment (the reference's packed block buffer): every
+// lane loads its ALIGNED 16-byte chunk, takes the next lane's leading bytes
+// with a DPP wavefront shift (v_mov_b32_dpp wave_shl:1) and realigns in
+// registers; lane 63's neighbour is the next wave's first chunk.  Stores stay
+// unaligned 16-byte vector stores (probe-verified device only).  The depth-2
+// register ring of do_tile, each slot holding the lane's aligned chunk(s),
+// the edge chunk(s) and the shard's misalignment m (wave-uniform, a scalar).
+// Measured against the unaligned vector path: -2.7 points on both RS(10,4)
+// encode and 2-erasure rebuild (profiles/r03/tune_*_packed_realign.txt): a
+// wave still touches the same nine 128-byte lines per 1 KiB of a misaligned
+// shard, and the edge load and the DPP moves come on top.
+template <int R, int U, int F>
+__device__ __forceinline__ void realign_tile(const ApplyArgs& a, const Ctx& c, const uint8_t* ib, uint8_t* ob,
+                                             uint64_t col0) {
+    constexpr int TH = threads_of<F>();
+    constexpr int NB = 2;
+    const uint32_t k = a.k;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave0 = tid - lane;
+    uint32_t acc[U][R][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[u][r][j] = 0u;
+    u32x4 rlo[NB][U], red[NB][U];
+    uint32_t rm[NB];
+    auto load = [&](int s, uint32_t t) {
+        const uint32_t tt = t < k ? t : k - 1;
+        const uint8_t* base = ib + c.s_in_off[tt] + col0;
+        const uint32_t m = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(uintptr_t(base)) & 15u)));
+        rm[s] = m;
+        const uint8_t* al = base - m;
+#pragma unroll
+        for (int u = 0; u < U; ++u) rlo[s][u] = load16<F>(al + (uint64_t(u) * TH + tid) * 16);
+        // Lane 63's neighbour: the next wave's first chunk.  Every lane issues
+        // the same (wave-uniform) address -- one 16-byte request, and no
+        // branch around a load, which would make the compiler's wait counts
+        // merge conservatively and drain the look-ahead.  With m != 0 the chunk
+        // holds bytes of this tile; with m == 0 it is not needed and the
+        // address stays on the wave's own last chunk (never past the buffer).
+        const uint32_t edge = wave0 + (m ? 64u : 63u);
+#pragma unroll
+        for (int u = 0; u < U; ++u) red[s][u] = load16<F>(al + (uint64_t(u) * TH + edge) * 16);
+    };
+    load(0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    for (uint32_t t = 0; t < k; t += NB) {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            load((i + 1) % NB, t + i + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            if (t + i < k) {
+                Tab tb[R];
+                read_tabs<R>(c, t + i, tb);
+                const uint32_t m = rm[i];
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    mac<R, F>(acc[u], m ? realign_lanes(rlo[i][u], red[i][u], m) : rlo[i][u], tb);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        uint8_t* o = ob + c.s_out_off[r];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            store16<F>(o + col0 + (uint64_t(u) * TH + tid) * 16,
+                       u32x4{acc[u][r][0], acc[u][r][1], acc[u][r][2], acc[u][r][3]});
+    }
+}
+
 #define SHMR_VARIANTS_TOOLS(X) \
     X(1, 0) \
     X(1, kNtLoad) \
@@ -266,7 +359,15 @@ __device__ __forceinline__ void spre_tile(const ApplyArgs& a, const uint8_t* pla
     X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kRealign) \
     X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kRealign) \
     X(2, kNtLoad | kNtStore | kDepth2 | kRealign | kSerial) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kRealign)
+    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kRealign) \
+    X(1, kNtLoad | kSc1Store | kDepth2) \
+    X(2, kNtLoad | kSc1Store | kDepth2) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kFuse) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kFuse) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse)
 
 template <int R>
 hipError_t dispatch_tools(const ApplyArgs& a, const Variant& v, int grid_cap, hipStream_t s) {

@@ -45,6 +45,7 @@ def main():
                     help="';'-separated knob sets applied on top of the defaults (prefix-free keys)")
     ap.add_argument("--json", default="")
     ap.add_argument("--pad", type=int, default=0, help="extra bytes per shard pitch (de-alias 2^n strides)")
+    ap.add_argument("--align", type=int, default=256, help="shard pitch = S rounded up to this (bench.py: 4096)")
     ap.add_argument("--bpad", type=int, default=0, help="encode: extra bytes per block pitch")
     ap.add_argument("--ppad", type=int, default=None,
                     help="encode: parity shard pitch = S rounded to 256 B plus this (default: --pad, as the data)")
@@ -78,7 +79,7 @@ def main():
         def run():
             rs.encode_batch_dev(data, parity, shard_len=S, data_shard_pitch=S, parity_shard_pitch=S)
     elif er == 0:
-        P = (S + 255) // 256 * 256 + a.pad
+        P = (S + a.align - 1) // a.align * a.align + a.pad
         if a.bpad:   # extra bytes per block pitch (block stride != k * shard pitch)
             flat = torch.randint(0, 256, (B * (k * P + a.bpad),), dtype=torch.uint8, device=dev, generator=g)
             data = flat.as_strided((B, k, P), (k * P + a.bpad, P, 1))
@@ -86,14 +87,14 @@ def main():
                 (B, p, P), (p * P + a.bpad, P, 1))
         else:
             data = torch.randint(0, 256, (B, k, P), dtype=torch.uint8, device=dev, generator=g)
-            PP = P if a.ppad is None else (S + 255) // 256 * 256 + a.ppad
+            PP = P if a.ppad is None else (S + a.align - 1) // a.align * a.align + a.ppad
             parity = torch.empty((B, p, PP), dtype=torch.uint8, device=dev)
         algo = B * (k + p) * S
 
         def run():
             rs.encode_batch_dev(data, parity, shard_len=S)
     else:
-        pitch = S if a.packed else (S + 255) // 256 * 256 + a.pad
+        pitch = S if a.packed else (S + a.align - 1) // a.align * a.align + a.pad
         shards = torch.zeros((B, k + p, pitch), dtype=torch.uint8, device=dev)
         shards[:, :k, :S] = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=dev, generator=g)
         present = np.ones((B, k + p), np.uint8)
