@@ -6,7 +6,7 @@
 //
 //   hipcc -O3 --offload-arch=gfx950 tools/membench.hip -o tools/_bin/membench
 //   membench [shard_bytes=524288] [blocks=512] [iters=20]
-//   env: MEMBENCH_ALLOC=contig (physically contiguous VRAM), MEMBENCH_ONLY=83,
+//   env: MEMBENCH_ALLOC=contig (physically contiguous VRAM), MEMBENCH_ONLY=83 | 104,
 //        MEMBENCH_PITCH=<bytes> (shard slot > S: padded layout, bench.py --pitch-pad)
 //
 // Prints one JSON line per (pattern, variant): TB/s of algorithmic bytes
@@ -159,6 +159,11 @@ int main(int argc, char** argv) {
         kin_rout<8, 3, 1, 3><<<uint32_t(S / 4096 * B), 256>>>(in, out, P, S / 4096, uint32_t(S / 4096 * B), sink);
     CK(hipDeviceSynchronize());
     for (int rep = 0; rep < 2; ++rep) {
+        if (only && std::strcmp(only, "104") == 0) {   // the RS(10,4) encode pattern only
+            run<10, 4, 1, kNtL | kNtS>("nt", in, out, S, B, sink, iters);
+            run<10, 4, 2, kNtL | kNtS>("nt", in, out, S, B, sink, iters);
+            continue;
+        }
         pattern<8, 3>(in, out, S, B, sink, iters);
         if (only && std::strcmp(only, "83") == 0) continue;
         pattern<8, 1>(in, out, S, B, sink, iters);
