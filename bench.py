@@ -83,11 +83,11 @@ def parse():
                          "aligned pitch is a multiple of 64 KiB (power-of-two shard sizes: RS(8,3) 4 MiB, RS(4,2) "
                          "1 MiB: +1.7-1.8 points of HBM peak), none with --pitch-align 1; 0 = the reference's "
                          "contiguous block buffer for those sizes (DESIGN.md section 4)")
-    ap.add_argument("--rebuild-out", default="inplace", choices=["inplace", "compact"],
-                    help="decode configs: rebuild the erased shards in place in their block's slots, or into a "
-                         "separate compact [blocks][erasures][pitch] output -- the crate's semantics, every None "
-                         "shard rebuilt into a fresh buffer (reference src/vfs/block.rs:556-565; "
-                         "shmr_ec_reconstruct_batch_dev_out)")
+    ap.add_argument("--rebuild-out", default="compact", choices=["inplace", "compact"],
+                    help="decode configs: rebuild the erased shards into a separate compact "
+                         "[blocks][erasures][pitch] output -- the crate's semantics, every None shard rebuilt into "
+                         "a fresh buffer (reference src/vfs/block.rs:556-565; shmr_ec_reconstruct_batch_dev_out; "
+                         "default) -- or in place, in their block's own slots")
     ap.add_argument("--process-model", default="process", choices=["process", "single"],
                     help="process: one process per GPU (torchrun, or self-spawned for --gpus N); single: one "
                          "process drives all N GPUs with one host thread + stream each (the reference daemon's "
@@ -563,8 +563,8 @@ def run_single(args):
 def traffic_key(args) -> str:
     """Key of the PMC record for this run's configuration and layout: the
     config name, plus "+packed" for the reference's packing (--pitch-align 1),
-    "+contig" for --pitch-pad 0 on a power-of-two shard, "+compact" for a
-    compact rebuild output."""
+    "+contig" for --pitch-pad 0 on a power-of-two shard, "+inplace" for a
+    decode rebuilt in place (the compact output is the default)."""
     key = args.config
     if args.pitch_align == 1:
         key += "+packed"
@@ -572,8 +572,8 @@ def traffic_key(args) -> str:
         key += "+contig"
     elif (args.pitch_align, args.pitch_pad) != (4096, -1):
         key += f"+pitch{args.pitch_align}_{args.pitch_pad}"
-    if args.rebuild_out == "compact" and CONFIGS[args.config][3] is not None:
-        key += "+compact"
+    if args.rebuild_out == "inplace" and CONFIGS[args.config][3] is not None:
+        key += "+inplace"
     return key
 
 

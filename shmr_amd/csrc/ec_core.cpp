@@ -88,14 +88,14 @@ std::atomic<int> g_uvec{kAuto};
 //
 // Reconstructs into a compact output (shmr_ec_reconstruct_batch_dev_out: the
 // rebuilt shards of a block written densely to a separate array, the crate's
-// fresh-allocation semantics) take the in-place policy.  Measured
-// (profiles/r03/tune_decode*_compact.txt, interleaved in one process): for
-// RS(8,3) 1-erasure rebuilds nontemporal stores with the 7-workgroup cap run
-// 76.4 % of peak against 75.2-75.8 % with sc1 stores (either cap) and 72 %
-// with plain stores; for RS(10,4) 2-erasure rebuilds sc1 and nontemporal are
-// within 0.3 point (77.2 / 76.9 %).  The sc1 variants stay in the tools build.
+// fresh-allocation semantics) store with the sc1 cache policy and no
+// residency cap.  Measured with real parity content, in-place and compact
+// interleaved in one process (profiles/r03/r03c/, r03b/): RS(10,4) 2-erasure
+// rebuilds 81.1 / 81.2 % of peak (two boxes) against 77.4 % with nontemporal
+// stores into the same compact output and 77.5 % in place; RS(8,3) 1-erasure
+// rebuilds sc1 and nontemporal-with-cap within 0.6 point of each other on
+// three boxes (73.7-79.7 %, the box decides).  Plain stores lose 3-6 points.
 kern::Variant variant_policy(OpClass op, unsigned k, unsigned rows, bool host_mapped, bool compact = false) {
-    (void)compact;
     kern::Variant v;
     if (op == kDecode && rows == 1 && !host_mapped) v.wgs_per_cu = 7;
     // U = 2 (8 KiB tiles) for 4-row launches, encode and reconstruct alike: a
@@ -115,6 +115,11 @@ kern::Variant variant_policy(OpClass op, unsigned k, unsigned rows, bool host_ma
     v.early = op == kEncode && (k <= 8 || rows >= 4) && !host_mapped;
     v.serial = op == kEncode && rows >= 4 && !host_mapped;
     v.fuse_tail = true;   // only where len % tile != 0 (RS(10,4): -5.5 % encode, -5.8 % decode time)
+    if (compact && op == kDecode && !host_mapped) {
+        v.sc1_store = true;
+        v.nt_store = false;
+        v.wgs_per_cu = 0;
+    }
     return v;
 }
 

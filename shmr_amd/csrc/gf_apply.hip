@@ -39,8 +39,8 @@ namespace kern {
 namespace {
 
 // The variants the tuning policy (ec_core.cpp variant_policy / launch_variant)
-// can select: depth-2 ring, nontemporal stores, nontemporal loads unless the
-// shards are mapped host memory, U = 1
+// can select: depth-2 ring, nontemporal stores (sc1 for compact rebuilt-shard
+// outputs), nontemporal loads unless the shards are mapped host memory, U = 1
 // or 2, with the early prologue, fused tails, shard-pointer tables and segment
 // launches as launch forms.  An unsupported combination returns
 // hipErrorInvalidValue (the C ABI reports SHMR_EC_INVALID_ARGUMENT).
@@ -70,7 +70,15 @@ namespace {
     X(2, kNtStore | kDepth2 | kPtrs | kSegs) \
     X(2, kNtStore | kDepth2 | kPtrs | kSegs | kFuse) \
     X(1, kNtLoad | kNtStore | kDepth2 | kPtrs) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kPtrs)
+    X(2, kNtLoad | kNtStore | kDepth2 | kPtrs) \
+    X(1, kNtLoad | kSc1Store | kDepth2) \
+    X(2, kNtLoad | kSc1Store | kDepth2) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kFuse) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kFuse) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse)
 
 template <int R>
 hipError_t dispatch_full(const ApplyArgs& a, const Variant& v, int grid_cap, hipStream_t s) {

@@ -9,8 +9,6 @@
 //  * the DPP realigning-load tile for misaligned shards (realign_tile):
 //    -2.7 / -2.7 points against the unaligned vector path on
 //    the reference's packed RS(10,4) buffer;
-//  * sc1 stores into compact rebuilt-shard outputs: -0.6 to +0.3 against
-//    nontemporal stores;
 //  * ring depths 1/3/5/9, 128/512-lane workgroups, occupancy targets and the
 //    other knob combinations of the instantiation list below.
 #include <hip/hip_runtime.h>
@@ -360,14 +358,11 @@ __device__ __forceinline__ void realign_tile(const ApplyArgs& a, const Ctx& c, c
     X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kRealign) \
     X(2, kNtLoad | kNtStore | kDepth2 | kRealign | kSerial) \
     X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kRealign) \
-    X(1, kNtLoad | kSc1Store | kDepth2) \
-    X(2, kNtLoad | kSc1Store | kDepth2) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kFuse) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kFuse) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse)
+    X(2, kNtStore | kDepth2 | kEarly | kSerial | kFuse) \
+    X(2, kNtLoad | kDepth2 | kEarly | kSerial | kFuse) \
+    X(2, kDepth2 | kEarly | kSerial | kFuse) \
+    X(1, kNtStore | kDepth2 | kSegs | kFuse) \
+    X(1, kDepth2 | kSegs | kFuse)
 
 template <int R>
 hipError_t dispatch_tools(const ApplyArgs& a, const Variant& v, int grid_cap, hipStream_t s) {

@@ -52,7 +52,9 @@ constexpr int kGlds = 1 << 21;   // tools: input ring in LDS filled by LDS-DMA
 // before the first XOR (48 live temporaries at R = 4), trading ILP inside a
 // wave for registers (more waves per SIMD).
 constexpr int kSerial = 1 << 22;
-// tools: stores with the sc1 cache policy (raw buffer stores, store16_row)
+// Stores with the sc1 cache policy instead of nontemporal (compact rebuilt-
+// shard outputs: a separate, densely written array; raw buffer stores,
+// store16_row)
 constexpr int kSc1Store = 1 << 23;
 // tools: misaligned shards by aligned loads realigned across lanes (DPP)
 constexpr int kRealign = 1 << 24;

@@ -211,10 +211,10 @@ def test_tuning_api():
     assert "early=0" in shmr_amd.describe_variant(True, 4, 2)
     assert "fuse_tail=1" in shmr_amd.describe_variant(False, 10, 4)
     assert "fuse_tail=1" in shmr_amd.describe_variant(True, 10, 2)
-    # reconstructs into a compact output (decode=2) take the in-place policy
-    # (measured: nontemporal stores beat sc1, profiles/r03/tune_decode*_compact.txt)
-    assert shmr_amd.describe_variant(2, 8, 1) == shmr_amd.describe_variant(True, 8, 1)
-    assert "sc1_store" not in shmr_amd.describe_variant(2, 10, 2)
+    # reconstructs into a compact output (decode=2) store with sc1, no residency cap
+    assert "sc1_store=1" in shmr_amd.describe_variant(2, 10, 2)
+    assert "nt_store=0" in shmr_amd.describe_variant(2, 8, 1) and "wgs_per_cu=0" in shmr_amd.describe_variant(2, 8, 1)
+    assert "sc1_store" not in shmr_amd.describe_variant(True, 8, 1)
     shmr_amd.set_tuning(sc1_store=-2)
     with pytest.raises(shmr_amd.Error):
         shmr_amd.set_tuning(sc1_store=0)

@@ -81,28 +81,20 @@ def test_full_tile_kernels_use_dwordx4(product_kernels):
         assert set(stores) == {store16}, ((R, U, F), set(stores))
 
 
-def test_store_cache_policy(product_kernels, tmp_path):
-    """Nontemporal-store product kernels store with nt; the tools build's sc1
-    kernels (compact-output measurement variants) store with sc1 through raw
+def test_store_cache_policy(product_kernels):
+    """sc1 kernels (compact rebuilt-shard outputs) store with sc1 through raw
     buffer stores -- never an inline-asm store, which would hide the >8-byte
-    store-data hazard from the compiler."""
+    store-data hazard from the compiler -- and nontemporal-store kernels with nt."""
     kern = _apply_kernels(product_kernels)
+    sc1 = [(k, b) for k, b in kern.items() if k[2] == 0 and k[3] & KSC1]
     nt = [(k, b) for k, b in kern.items() if k[2] == 0 and k[3] & KNTSTORE and not k[3] & KFUSE]
-    assert nt and not any(k[3] & KSC1 for k in kern)
-    for key, body in nt:
-        st = [i for i in body if i.startswith("global_store_dwordx4")]
-        assert st and all(re.search(r"\bnt\b", i) for i in st), (key, st[:2])
-    # the tools library links two kernel TUs; the sc1 variants live in the
-    # tools-only one, whose object the build leaves next to the library
-    obj = os.path.join(os.path.dirname(_native._PATHS["tools"]), "obj_tools", "gf_apply_tools.o")
-    if not os.path.exists(obj):
-        pytest.skip("tools kernel object not built here")
-    tools = _apply_kernels(_disasm(obj, tmp_path))
-    sc1 = [(k, b) for k, b in tools.items() if k[2] == 0 and k[3] & KSC1]
-    assert sc1
+    assert sc1 and nt
     for key, body in sc1:
         st = [i for i in body if re.match(r"(global|buffer)_store_dwordx4", i)]
         assert st and all(i.startswith("buffer_store_dwordx4") and i.endswith(" sc1") for i in st), (key, st[:2])
+    for key, body in nt:
+        st = [i for i in body if i.startswith("global_store_dwordx4")]
+        assert st and all(re.search(r"\bnt\b", i) for i in st), (key, st[:2])
 
 
 def test_misaligned_path_kernels_exist(product_kernels):

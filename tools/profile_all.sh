@@ -13,10 +13,10 @@ bash "$D/profile.sh" "$T" encode104 64 $((64 * 14 * 1677722))
 bash "$D/profile.sh" "$T" decode104 64 $((64 * 12 * 1677722))
 bash "$D/profile.sh" "$T" encode42 1024 1610612736
 bash "$D/profile.sh" "$T" codec104 64 $((64 * 26 * 1677722)) --sum-kernels
-# round 3: the compact rebuilt-shard output (crate semantics) and the reference's packed /
-# contiguous layouts (bench.py traffic_key)
-KEY=decode83+compact BENCH_EXTRA="--rebuild-out compact" bash "$D/profile.sh" "$T" decode83 512 2415919104
-KEY=decode104+compact BENCH_EXTRA="--rebuild-out compact" bash "$D/profile.sh" "$T" decode104 64 $((64 * 12 * 1677722))
+# round 3: decodes rebuilt in place (the compact output, the crate's semantics, is the bench
+# default) and the reference's packed / contiguous layouts (bench.py traffic_key)
+KEY=decode83+inplace BENCH_EXTRA="--rebuild-out inplace" bash "$D/profile.sh" "$T" decode83 512 2415919104
+KEY=decode104+inplace BENCH_EXTRA="--rebuild-out inplace" bash "$D/profile.sh" "$T" decode104 64 $((64 * 12 * 1677722))
 KEY=encode104+packed BENCH_EXTRA="--pitch-align 1" bash "$D/profile.sh" "$T" encode104 64 $((64 * 14 * 1677722))
 KEY=decode104+packed BENCH_EXTRA="--pitch-align 1" bash "$D/profile.sh" "$T" decode104 64 $((64 * 12 * 1677722))
 KEY=encode83+contig BENCH_EXTRA="--pitch-pad 0" bash "$D/profile.sh" "$T" encode83 512 2952790016
