@@ -252,12 +252,15 @@ class Workload:
                 self.rebuilt = None
                 self.reference = self.shards[:, :, :S].clone() if shape.codec else None
                 if shape.compact:
-                    # rebuilt shards into their own [B][erasures][pitch] array; the
-                    # erased slots of the block buffer are zeroed and never read
+                    # rebuilt shards into their own [B][erasures][pitch] array; for a
+                    # pure rebuild the erased slots of the block buffer are zeroed
+                    # (never read); codec104's encode needs every data shard, so
+                    # there they stay
                     self.rebuilt = self.vram((B, e, pitch))
                     self.rebuilt.zero_()
                     self.originals = self.shards[self.erased][:, :S].clone().view(B, e, S)
-                    self.shards[self.erased] = 0
+                    if not shape.codec:
+                        self.shards[self.erased] = 0
         torch.cuda.synchronize(dev)
 
     def vram(self, shape):
@@ -340,6 +343,9 @@ class Workload:
             if sh.compact:
                 ok = bool(torch.equal(self.rebuilt[:, :, :sh.S], self.originals)) and bool(
                     torch.equal(self.shards[~self.erased][:, :sh.S], self.reference[~self.erased]))
+                # put the rebuilt shards back into their slots (the buffer is whole
+                # again for the cpu_baseline leg's parity check)
+                self.shards[..., :sh.S][self.erased] = self.rebuilt[:, :, :sh.S].reshape(-1, sh.S)
             else:
                 ok = bool(torch.equal(self.shards[:, :, :sh.S], self.reference))
         return ok
