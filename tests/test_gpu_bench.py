@@ -31,9 +31,11 @@ def run_bench(*args):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("config,blocks", [("encode83", 16), ("decode83", 16), ("codec104", 4)])
-def test_bench_line_contract(gpu, config, blocks):
-    d = run_bench("--config", config, "--blocks", str(blocks))
+@pytest.mark.parametrize("config,blocks,extra", [("encode83", 16, ()), ("decode83", 16, ()), ("codec104", 4, ()),
+                                                ("decode83", 16, ("--rebuild-out", "inplace")),
+                                                ("codec104", 4, ("--rebuild-out", "inplace"))])
+def test_bench_line_contract(gpu, config, blocks, extra):
+    d = run_bench("--config", config, "--blocks", str(blocks), *extra)
     assert KEYS <= set(d)
     assert d["value"] > 0 and d["unit"] == "GiB/s" and d["n_gpus"] == 1 and d["steps"] == 3
     assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["dtype"] == "u8"
@@ -57,3 +59,18 @@ def test_bench_line_contract(gpu, config, blocks):
 def test_bench_contiguous_vram(gpu):
     d = run_bench("--blocks", "16", "--contig", "--no-cpu")
     assert d["value"] > 0 and "contiguous" in d["config"]["memory"] and d["cpu_baseline"] is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config", ["encode83", "codec104"])
+def test_bench_single_process_model(gpu, config):
+    """--process-model single: one process, one thread + stream per GPU (here
+    one GPU); the line names the model and carries the per-device figures."""
+    d = run_bench("--config", config, "--blocks", "8", "--process-model", "single")
+    assert KEYS <= set(d)
+    assert d["process_model"] == "single" and d["launcher"] == "threads"
+    assert d["n_gpus"] == 1 and d["ranks_seen"] == 1 and d["distinct_gpus"] == 1
+    assert len(d["per_device"]) == 1 and 0 < d["per_device"][0]["frac"] < 1
+    assert d["cpu_baseline"]["value"] > 0
+    if config == "codec104":
+        assert d["roofline"]["round_trip_bit_exact"] is True
