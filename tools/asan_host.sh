@@ -7,7 +7,7 @@
 #   tools/asan_host.sh run [out_dir]      # every case of shmr_vfs_test
 set -euo pipefail
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
-BIN="$ROOT/tools/_bin/vfs_test_asan"
+BIN="$ROOT/tools/_probe/vfs_test_asan"
 HIPCC=/opt/rocm/bin/hipcc
 CPU_CASES="block_topology_try_from virtual_block_new_block virtual_block_unbuffered_backing virtual_block_unbuffered
 virtual_block_buffered virtual_block_erasure_buffered block_errors virtual_file_1 virtual_file_2_4_mb virtual_file_errors
@@ -21,7 +21,7 @@ case "${1:-}" in
 build)
     # libshmr_ec.so's host code (C ABI, launch core, host engine) instrumented
     # too; the kernels are unchanged (-Xarch_host: host compilation only)
-    L="$ROOT/tools/_bin/asan_lib"
+    L="$ROOT/tools/_probe/asan_lib"
     mkdir -p "$L"
     SAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer"
     CXXF="-O1 -g -std=c++17 -fPIC -Wall -I$ROOT/include -I$ROOT/shmr_amd/csrc"
@@ -37,7 +37,7 @@ build)
     done
     $HIPCC --offload-arch=gfx950 -shared -fPIC $SAN -o "$L/libshmr_ec.so" "$L"/*.o -Wl,-soname,libshmr_ec.so -lpthread
     rm -f "$L"/*.o
-    $HIPCC -O1 -g -std=c++17 $SAN -I"$ROOT/include" -o "$ROOT/tools/_bin/abi_check_asan" "$ROOT/tools/abi_check.cpp" \
+    $HIPCC -O1 -g -std=c++17 $SAN -I"$ROOT/include" -o "$ROOT/tools/_probe/abi_check_asan" "$ROOT/tools/abi_check.cpp" \
         -L"$L" -lshmr_ec -Wl,-rpath,'$ORIGIN/asan_lib'
     $HIPCC -O1 -g -std=c++17 $SAN -Wall -I"$ROOT/include" -I"$ROOT/shmr_amd/host" -o "$BIN" \
         "$ROOT/shmr_amd/host/vfs_test.cpp" "$ROOT/shmr_amd/host/vfs.cpp" "$ROOT/shmr_amd/host/record.cpp" \
@@ -50,7 +50,7 @@ run)
     export ASAN_OPTIONS=detect_leaks=0:protect_shadow_gap=0:halt_on_error=1
     export UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1
     fail=0
-    if timeout -k 10 120 "$ROOT/tools/_bin/abi_check_asan" > "$OUT/abi_check.log" 2>&1; then
+    if timeout -k 10 120 "$ROOT/tools/_probe/abi_check_asan" > "$OUT/abi_check.log" 2>&1; then
         echo "abi_check PASS"
     else
         echo "abi_check FAIL (see $OUT/abi_check.log)"; exit 1

@@ -9,8 +9,8 @@
 # Usage: tools/counter_passes.sh <outdir>
 set -u
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
-OUT="$1"
-mkdir -p "$OUT"
+mkdir -p "$1"
+OUT="$(cd "$1" && pwd)"
 cd /tmp && export TMPDIR=/tmp
 PASSES=(
   "p1:TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum GRBM_GUI_ACTIVE"

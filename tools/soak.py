@@ -91,7 +91,7 @@ def worker(tid, deadline, errors, counts):
                     want = oracle_encode(k, p, list(blk[b, :k]))
                     if not all(np.array_equal(blk[b, i], want[i]) for i in range(k, k + p)):
                         errors.append((tid, "mapped batch encode", k, p, L, B))
-            else:              # device-resident batch on this thread's stream
+            else:              # device-resident batch on this thread's stream: encode, in-place and compact rebuild
                 B = int(rng.integers(1, 9))
                 P = (L + 255) // 256 * 256
                 with torch.cuda.stream(stream):
@@ -103,11 +103,24 @@ def worker(tid, deadline, errors, counts):
                     for b in range(B):
                         present[b, rng.choice(k + p, size=int(rng.integers(1, p + 1)), replace=False)] = 0
                     full = d.clone()
-                    d[torch.from_numpy(present == 0).cuda()] = 0
+                    erased = torch.from_numpy(present == 0).cuda()
+                    d[erased] = 0
                     rs.reconstruct_batch_dev(d, present, shard_len=L)
                     ok = torch.equal(d[:, :, :L], full[:, :, :L])
+                    # compact rebuild (the crate's fresh-buffer semantics) from a copy
+                    # whose erased slots are poisoned: they must not be read
+                    src = full.clone()
+                    src[erased] = 0xEE
+                    out = torch.zeros((B, int((present == 0).sum(axis=1).max()), P), dtype=torch.uint8, device="cuda")
+                    rs.reconstruct_batch_dev_out(src, present, out, shard_len=L)
                 stream.synchronize()
                 h = full.cpu().numpy()
+                ho = out.cpu().numpy()
+                for b in range(B):
+                    for j, i in enumerate(np.flatnonzero(present[b] == 0)):
+                        if not np.array_equal(ho[b, j, :L], h[b, i, :L]):
+                            errors.append((tid, "batch_dev compact", k, p, L, B))
+                            break
                 for b in range(B):
                     want = oracle_encode(k, p, list(host[b]))
                     if not all(np.array_equal(h[b, i, :L], want[i]) for i in range(k, k + p)):
