@@ -195,19 +195,27 @@ __device__ __forceinline__ u32x4 realign_lanes(const u32x4& lo, const u32x4& edg
 // unaligned 16-byte vector stores (probe-verified device only).  The depth-2
 // register ring of do_tile, each slot holding the lane's aligned chunk(s),
 // the edge chunk(s) and the shard's misalignment m (wave-uniform, a scalar).
-// Measured against the unaligned vector path: -2.7 points on both RS(10,4)
-// encode and 2-erasure rebuild (profiles/r03/tune_*_packed_realign.txt): a
-// wave still touches the same nine 128-byte lines per 1 KiB of a misaligned
-// shard, and the edge load and the DPP moves come on top.
+// Why: a misaligned 16-byte vector load is split into several L1 (TCP)
+// accesses -- 64 TCP cache accesses per KiB of RS(10,4) encode traffic on the
+// packed buffer against 18 on aligned slots (profiles/r03/counters_encode104.md).
+// The first form (lanes of instruction u over columns u * TH + tid, an edge
+// load per instruction) measured -2.7 points against the unaligned vector
+// path (profiles/r03/tune_*_packed_realign.txt).  Here each wave reads one
+// contiguous U KiB run, so an edge load per run (a scalar load instead would
+// share lgkmcnt with the LDS table reads and serialise the look-ahead).
 template <int R, int U, int F>
 __device__ __forceinline__ void realign_tile(const ApplyArgs& a, const Ctx& c, const uint8_t* ib, uint8_t* ob,
                                              uint64_t col0) {
-    constexpr int TH = threads_of<F>();
     constexpr int NB = 2;
     const uint32_t k = a.k;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave0 = tid - lane;
+    // Wave-contiguous runs: chunk u of lane L in wave w covers column chunk
+    // (w * U + u) * 64 + L, so a wave's U instructions read one contiguous
+    // U KiB run and lane 63's neighbour in instruction u < U-1 is lane 0 of
+    // instruction u+1 (readlane); only the run's end needs the edge load.
+    auto chunk = [&](int u) { return uint64_t(wave0 * U + uint32_t(u) * 64u + lane); };
     uint32_t acc[U][R][4];
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -215,7 +223,7 @@ __device__ __forceinline__ void realign_tile(const ApplyArgs& a, const Ctx& c, c
         for (int r = 0; r < R; ++r)
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[u][r][j] = 0u;
-    u32x4 rlo[NB][U], red[NB][U];
+    u32x4 rlo[NB][U], red[NB];
     uint32_t rm[NB];
     auto load = [&](int s, uint32_t t) {
         const uint32_t tt = t < k ? t : k - 1;
@@ -224,16 +232,18 @@ __device__ __forceinline__ void realign_tile(const ApplyArgs& a, const Ctx& c, c
         rm[s] = m;
         const uint8_t* al = base - m;
 #pragma unroll
-        for (int u = 0; u < U; ++u) rlo[s][u] = load16<F>(al + (uint64_t(u) * TH + tid) * 16);
-        // Lane 63's neighbour: the next wave's first chunk.  Every lane issues
-        // the same (wave-uniform) address -- one 16-byte request, and no
-        // branch around a load, which would make the compiler's wait counts
-        // merge conservatively and drain the look-ahead.  With m != 0 the chunk
-        // holds bytes of this tile; with m == 0 it is not needed and the
-        // address stays on the wave's own last chunk (never past the buffer).
-        const uint32_t edge = wave0 + (m ? 64u : 63u);
-#pragma unroll
-        for (int u = 0; u < U; ++u) red[s][u] = load16<F>(al + (uint64_t(u) * TH + edge) * 16);
+        for (int u = 0; u < U; ++u) rlo[s][u] = load16<F>(al + chunk(u) * 16);
+        // the chunk after the run (wave-uniform address, one request; with
+        // m == 0 it stays on the run's own last chunk, never past the buffer)
+        red[s] = load16<F>(al + (uint64_t(wave0) * U + uint64_t(U) * 64u - (m ? 0u : 1u)) * 16);
+    };
+    auto neighbour = [&](const u32x4 (&lo)[U], const u32x4& edge, int u) -> u32x4 {
+        if (u + 1 < U) {
+            const u32x4& nx = lo[u + 1];
+            return u32x4{uint32_t(__builtin_amdgcn_readlane(int(nx.x), 0)), uint32_t(__builtin_amdgcn_readlane(int(nx.y), 0)),
+                         uint32_t(__builtin_amdgcn_readlane(int(nx.z), 0)), uint32_t(__builtin_amdgcn_readlane(int(nx.w), 0))};
+        }
+        return edge;
     };
     load(0, 0);
     __builtin_amdgcn_sched_barrier(0);
@@ -248,7 +258,7 @@ __device__ __forceinline__ void realign_tile(const ApplyArgs& a, const Ctx& c, c
                 const uint32_t m = rm[i];
 #pragma unroll
                 for (int u = 0; u < U; ++u)
-                    mac<R, F>(acc[u], m ? realign_lanes(rlo[i][u], red[i][u], m) : rlo[i][u], tb);
+                    mac<R, F>(acc[u], m ? realign_lanes(rlo[i][u], neighbour(rlo[i], red[i], u), m) : rlo[i][u], tb);
             }
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -258,8 +268,7 @@ __device__ __forceinline__ void realign_tile(const ApplyArgs& a, const Ctx& c, c
         uint8_t* o = ob + c.s_out_off[r];
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            store16<F>(o + col0 + (uint64_t(u) * TH + tid) * 16,
-                       u32x4{acc[u][r][0], acc[u][r][1], acc[u][r][2], acc[u][r][3]});
+            store16<F>(o + col0 + chunk(u) * 16, u32x4{acc[u][r][0], acc[u][r][1], acc[u][r][2], acc[u][r][3]});
     }
 }
 
