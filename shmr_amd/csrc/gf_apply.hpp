@@ -95,6 +95,7 @@ struct Variant {
     bool serial = false;     // GF math one dword at a time (fewer live registers, more waves)
     bool sc1_store = false;  // stores with the sc1 cache policy instead of nontemporal
     bool realign = false;    // misaligned shards: aligned loads realigned across lanes (DPP), unaligned stores
+    bool peel = false;       // depth-2 ring with the tail peeled (no look-ahead load past the last shard)
 };
 
 // rows in [1, kMaxRowsPerLaunch].  mode 0: full tiles, every shard base

@@ -367,11 +367,25 @@ __device__ __forceinline__ void realign_tile(const ApplyArgs& a, const Ctx& c, c
     X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kRealign) \
     X(2, kNtLoad | kNtStore | kDepth2 | kRealign | kSerial) \
     X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kRealign) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kRealign) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse | kRealign) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kRealign) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kFuse | kRealign) \
     X(2, kNtStore | kDepth2 | kEarly | kSerial | kFuse) \
     X(2, kNtLoad | kDepth2 | kEarly | kSerial | kFuse) \
     X(2, kDepth2 | kEarly | kSerial | kFuse) \
     X(1, kNtStore | kDepth2 | kSegs | kFuse) \
-    X(1, kDepth2 | kSegs | kFuse)
+    X(1, kDepth2 | kSegs | kFuse) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kPeel) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial | kPeel) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kPeel) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kFuse | kPeel) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kPeel) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kPeel) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kPeel) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse | kPeel)
 
 template <int R>
 hipError_t dispatch_tools(const ApplyArgs& a, const Variant& v, int grid_cap, hipStream_t s) {

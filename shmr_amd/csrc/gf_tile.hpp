@@ -58,6 +58,10 @@ constexpr int kSerial = 1 << 22;
 constexpr int kSc1Store = 1 << 23;
 // tools: misaligned shards by aligned loads realigned across lanes (DPP)
 constexpr int kRealign = 1 << 24;
+// tools: the depth-2 ring with its tail peeled -- no look-ahead load past the
+// last shard (the default ring re-reads shard k-1 there: one extra wave load
+// per shard run, an L2 hit) and still no load behind a branch inside the loop
+constexpr int kPeel = 1 << 25;
 // Bits 12-15: occupancy target in waves per SIMD (0 = compiler's choice);
 // the register allocator must then fit 512 / target VGPRs.
 constexpr int kOccShift = 12;
@@ -300,6 +304,34 @@ template <int R, int U, int F>
 __device__ __forceinline__ void realign_tile(const ApplyArgs& a, const Ctx& c, const uint8_t* ib, uint8_t* ob,
                                              uint64_t col0);
 
+// Depth-2 ring with the tail peeled (kPeel): slot 0 holds shard 0 on entry;
+// the loop body is unconditional (exact wait counts), and the one or two
+// shards left after it are consumed with no load past shard k-1.  The branch
+// between the two tails is uniform and nothing is pending after either.
+template <class Load, class Consume, class Ring>
+__device__ __forceinline__ void ring2_peeled(Load& load, Consume& consume, uint32_t k, Ring (&ring)[2]) {
+    uint32_t t = 0;
+    for (; t + 2 < k; t += 2) {
+        load(ring[1], t + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        consume(ring[0], t);
+        __builtin_amdgcn_sched_barrier(0);
+        load(ring[0], t + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        consume(ring[1], t + 1);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (t + 1 < k) {
+        load(ring[1], t + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        consume(ring[0], t);
+        __builtin_amdgcn_sched_barrier(0);
+        consume(ring[1], t + 1);
+    } else {
+        consume(ring[0], t);
+    }
+}
+
 // One tile: lanes own columns col0 + (u * TH + tid) * 16, u < U.
 //
 // sched_barrier(0) pins program order: without it the scheduler sinks the
@@ -395,13 +427,17 @@ __device__ __forceinline__ void do_tile(const ApplyArgs& a, const Ctx& c, const 
 #pragma unroll
     for (int i = 0; i < NB - 1; ++i) load(ring[i], i);
     __builtin_amdgcn_sched_barrier(0);
-    for (uint32_t t = 0; t < k; t += NB) {
+    if constexpr ((F & kPeel) != 0 && NB == 2) {
+        ring2_peeled(load, consume, k, ring);
+    } else {
+        for (uint32_t t = 0; t < k; t += NB) {
 #pragma unroll
-        for (int i = 0; i < NB; ++i) {
-            load(ring[(i + NB - 1) % NB], t + i + NB - 1);
-            __builtin_amdgcn_sched_barrier(0);
-            if (t + i < k) consume(ring[i], t + i);
-            __builtin_amdgcn_sched_barrier(0);
+            for (int i = 0; i < NB; ++i) {
+                load(ring[(i + NB - 1) % NB], t + i + NB - 1);
+                __builtin_amdgcn_sched_barrier(0);
+                if (t + i < k) consume(ring[i], t + i);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
     }
 #pragma unroll
@@ -563,13 +599,17 @@ __device__ __forceinline__ void early_tile(const ApplyArgs& a, const uint8_t* pl
 #pragma unroll
         for (int u = 0; u < U; ++u) mac<R, F>(acc[u], buf[u], tb);
     };
-    for (uint32_t t = 0; t < k; t += NB) {
+    if constexpr ((F & kPeel) != 0 && NB == 2) {
+        ring2_peeled(load, consume, k, ring);
+    } else {
+        for (uint32_t t = 0; t < k; t += NB) {
 #pragma unroll
-        for (int i = 0; i < NB; ++i) {
-            load(ring[(i + NB - 1) % NB], t + i + NB - 1);
-            __builtin_amdgcn_sched_barrier(0);
-            if (t + i < k) consume(ring[i], t + i);
-            __builtin_amdgcn_sched_barrier(0);
+            for (int i = 0; i < NB; ++i) {
+                load(ring[(i + NB - 1) % NB], t + i + NB - 1);
+                __builtin_amdgcn_sched_barrier(0);
+                if (t + i < k) consume(ring[i], t + i);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
     }
 #pragma unroll
@@ -745,7 +785,7 @@ inline int variant_flags(const Variant& v) {
            (v.depth == 1 ? kDepth1 : 0) | ((v.occ & 15) << kOccShift) | (v.early ? kEarly : 0) |
            (v.spre ? kSPre : 0) | (v.fuse_tail ? kFuse : 0) | (v.ptrs ? kPtrs : 0) | (v.segs ? kSegs : 0) |
            (v.glds ? kGlds : 0) | (v.serial ? kSerial : 0) | (v.sc1_store ? kSc1Store : 0) |
-           (v.realign ? kRealign : 0);
+           (v.realign ? kRealign : 0) | (v.peel ? kPeel : 0);
 }
 
 }  // namespace

@@ -125,12 +125,15 @@ def test_compact_inconsistent_shards_follow_crate(gpu):
     del torch
 
 
-@pytest.mark.parametrize("path", ["auto", "realign"])
-def test_compact_packed_layout(gpu, path):
+@pytest.mark.parametrize("off", [3, 0])
+@pytest.mark.parametrize("path", ["auto", "realign", "dpp"])
+def test_compact_packed_layout(gpu, path, off):
     """The reference's packed block buffer (shard i at i * S, RS(10,4) 16 MiB:
     off 16-byte alignment) read in place, rebuilt shards to a compact output
-    whose rows are misaligned too.  "realign": the tools build's realigning
-    kernel (knob uvec=0) instead of the unaligned vector path."""
+    whose rows are misaligned too (off = 3) or start aligned (off = 0: sc1
+    stores allowed).  "realign": the tools build's realigning kernel (knob
+    uvec=0) instead of the unaligned vector path; "dpp": aligned loads
+    realigned across lanes (uvec=1, realign=1)."""
     import torch
 
     def check():
@@ -148,8 +151,8 @@ def test_compact_packed_layout(gpu, path):
             present[b, [(b * 3) % t, (b * 3 + 5) % t]] = 0
         dev = torch.from_numpy(blocks.copy()).to(gpu)
         dev[torch.from_numpy(present == 0).to(gpu)] = POISON
-        flat = torch.full((3 + B * 2 * S + 64,), GUARD, dtype=torch.uint8, device=gpu)
-        out = flat[3:3 + B * 2 * S].view(B, 2, S)
+        flat = torch.full((off + B * 2 * S + 64,), GUARD, dtype=torch.uint8, device=gpu)
+        out = flat[off:off + B * 2 * S].view(B, 2, S)
         shmr_amd.ReedSolomon(k, p).reconstruct_batch_dev_out(dev, present, out, shard_len=S)
         torch.cuda.synchronize()
         got = out.cpu().numpy()
@@ -157,32 +160,35 @@ def test_compact_packed_layout(gpu, path):
             for j, i in enumerate(np.flatnonzero(present[b] == 0)):
                 assert np.array_equal(got[b, j], blocks[b, i]), (b, i)
         edge = flat.cpu().numpy()
-        assert (edge[:3] == GUARD).all() and (edge[3 + B * 2 * S:] == GUARD).all()
+        assert (edge[:off] == GUARD).all() and (edge[off + B * 2 * S:] == GUARD).all()
 
     if path == "auto":
         return check()
     with _native.tools():
-        shmr_amd.set_tuning(uvec=0)
+        shmr_amd.set_tuning(uvec=0) if path == "realign" else shmr_amd.set_tuning(uvec=1, realign=1)
         try:
             check()
         finally:
-            shmr_amd.set_tuning(uvec=-2)
+            shmr_amd.set_tuning(uvec=-2, realign=-2)
 
 
-def test_compact_store_policies_match(gpu):
+@pytest.mark.parametrize("k", [8, 7])
+def test_compact_store_policies_match(gpu, k):
     """sc1 (the policy), nontemporal and plain stores into the compact output
-    give identical bytes (tools build knobs)."""
+    give identical bytes, and so does the peeled shard ring (tools build
+    knobs; k = 7 ends the ring on an odd shard)."""
     with _native.tools():
-        k, p, S, B = 8, 3, 65536 * 2 + 4096, 16
+        p, S, B = 3, 65536 * 2 + 4096, 16
         present = np.ones((B, k + p), np.uint8)
         present[np.arange(B), np.arange(B) % k] = 0
         outs = []
-        for knobs in ({}, {"decode.sc1_store": 0, "decode.nt_store": 1}, {"decode.sc1_store": 0, "decode.nt_store": 0}):
+        for knobs in ({}, {"decode.sc1_store": 0, "decode.nt_store": 1}, {"decode.sc1_store": 0, "decode.nt_store": 0},
+                      {"decode.peel": 1}):
             shmr_amd.set_tuning(**knobs)
             try:
                 outs.append(_run(gpu, k, p, S, B, present, seed=5))
             finally:
-                shmr_amd.set_tuning(**{"decode.sc1_store": -2, "decode.nt_store": -2})
+                shmr_amd.set_tuning(**{"decode.sc1_store": -2, "decode.nt_store": -2, "decode.peel": -2})
         assert all(np.array_equal(outs[0], o) for o in outs[1:])
 
 
