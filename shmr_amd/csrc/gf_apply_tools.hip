@@ -385,6 +385,8 @@ __device__ __forceinline__ void realign_tile(const ApplyArgs& a, const Ctx& c, c
     X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kPeel) \
     X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kPeel) \
     X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kPeel) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kPeel) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kFuse | kPeel) \
     X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse | kPeel)
 
 template <int R>
