@@ -116,6 +116,11 @@ kern::Variant variant_policy(OpClass op, unsigned k, unsigned rows, bool host_ma
     v.early = op == kEncode && (k <= 8 || rows >= 4) && !host_mapped;
     v.serial = op == kEncode && rows >= 4 && !host_mapped;
     v.fuse_tail = true;   // only where len % tile != 0 (RS(10,4): -5.5 % encode, -5.8 % decode time)
+    // reconstructs peel the shard ring's tail (no look-ahead load past the
+    // last input): RS(8,3) compact +0.9, in place +1.0, RS(10,4) compact +0.5
+    // points; the early-prologue encodes lose with it (RS(8,3) -2.5), so they
+    // keep the clamped look-ahead (profiles/r03/r03h/tune_*_peel.txt)
+    v.peel = op == kDecode && !host_mapped;
     if (compact && op == kDecode && !host_mapped) {
         v.sc1_store = true;
         v.nt_store = false;
@@ -307,6 +312,7 @@ kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_m
     if (T.peel.load() != kAuto) v.peel = T.peel.load() != 0;
     if (v.sc1_store) v.nt_store = false;   // one store policy per kernel
     if (v.glds) v.early = v.spre = false;   // the LDS-DMA ring is a form of the plain tile
+    if (v.glds || v.depth != 2) v.peel = false;   // peeling is a form of the depth-2 register ring
     return v;
 }
 
@@ -653,7 +659,7 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
         // realigning-load form of the plain tile
         if (!aligned16_all && g_tune[op].realign.load() == 1 && !ptrs) {
             var.realign = true;
-            var.early = var.spre = var.glds = false;
+            var.early = var.spre = var.glds = var.peel = false;   // the realigning tile keeps its own ring
         }
         // sc1 stores are raw buffer stores: a 2 GiB resource per output row,
         // and 16-byte aligned outputs only (the unaligned-access probe covers

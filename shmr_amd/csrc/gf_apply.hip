@@ -57,10 +57,14 @@ namespace {
     X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse) \
     X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial) \
     X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kSegs) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kSegs) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kPeel) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kPeel) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kPeel) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kFuse | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kPeel) \
     X(1, kNtStore | kDepth2 | kPtrs) \
     X(2, kNtStore | kDepth2 | kPtrs) \
     X(1, kNtStore | kDepth2 | kPtrs | kFuse) \
@@ -71,14 +75,16 @@ namespace {
     X(2, kNtStore | kDepth2 | kPtrs | kSegs | kFuse) \
     X(1, kNtLoad | kNtStore | kDepth2 | kPtrs) \
     X(2, kNtLoad | kNtStore | kDepth2 | kPtrs) \
-    X(1, kNtLoad | kSc1Store | kDepth2) \
-    X(2, kNtLoad | kSc1Store | kDepth2) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kFuse) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kFuse) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse)
+    X(1, kNtLoad | kNtStore | kDepth2 | kPtrs | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kPtrs | kPeel) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kPeel) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kPeel) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kFuse | kPeel) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kFuse | kPeel) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kPeel) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse | kPeel) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs | kPeel) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse | kPeel)
 
 template <int R>
 hipError_t dispatch_full(const ApplyArgs& a, const Variant& v, int grid_cap, hipStream_t s) {

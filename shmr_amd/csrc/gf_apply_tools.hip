@@ -380,14 +380,18 @@ __device__ __forceinline__ void realign_tile(const ApplyArgs& a, const Ctx& c, c
     X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPeel) \
     X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial | kPeel) \
     X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial | kPeel) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kPeel) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kFuse | kPeel) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kPeel) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kPeel) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kPeel) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kPeel) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kFuse | kPeel) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse | kPeel)
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSegs) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse) \
+    X(1, kNtLoad | kSc1Store | kDepth2) \
+    X(2, kNtLoad | kSc1Store | kDepth2) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kFuse) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kFuse) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse)
 
 template <int R>
 hipError_t dispatch_tools(const ApplyArgs& a, const Variant& v, int grid_cap, hipStream_t s) {
