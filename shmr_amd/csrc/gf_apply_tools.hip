@@ -355,6 +355,10 @@ __device__ __forceinline__ void realign_tile(const ApplyArgs& a, const Ctx& c, c
     X(1, kNtLoad | kDepth2 | kFuse) \
     X(1, kNtLoad | kDepth2 | kSegs) \
     X(1, kNtLoad | kDepth2 | kSegs | kFuse) \
+    X(1, kNtLoad | kDepth2 | kPeel) \
+    X(1, kNtLoad | kDepth2 | kFuse | kPeel) \
+    X(1, kNtLoad | kDepth2 | kSegs | kPeel) \
+    X(1, kNtLoad | kDepth2 | kSegs | kFuse | kPeel) \
     X(2, kNtLoad | kDepth2) \
     X(2, kNtLoad | kDepth2 | kSegs) \
     X(1, kNtLoad | kNtStore | kDepth2 | kRealign) \
