@@ -39,6 +39,7 @@ struct Tuning {
     std::atomic<int> sc1_store{kAuto};
     std::atomic<int> realign{kAuto};
     std::atomic<int> peel{kAuto};
+    std::atomic<int> wave_run{kAuto};
 };
 Tuning g_tune[2];   // [kEncode], [kDecode]
 std::atomic<int> g_bounce_kib{kBounceKibDefault};
@@ -201,7 +202,7 @@ int set_tuning(const char* key, int value) {
             {"chunks", kAuto}, {"nt_load", kAuto}, {"nt_store", kAuto}, {"occ8", 0},
             {"grid", -1},      {"diag", 0},        {"threads", 256},    {"depth", kAuto},   {"wgs_per_cu", kAuto},
             {"occ", kAuto},    {"early", kAuto},   {"spre", kAuto},     {"fuse_tail", kAuto},
-            {"glds", kAuto},   {"serial", kAuto},   {"sc1_store", kAuto}, {"realign", kAuto}, {"peel", kAuto}};
+            {"glds", kAuto},   {"serial", kAuto},   {"sc1_store", kAuto}, {"realign", kAuto}, {"peel", kAuto}, {"wave_run", kAuto}};
         const auto it = kDefaults.find(k);
         return (it != kDefaults.end() && it->second == value) ? SHMR_EC_OK : SHMR_EC_INVALID_ARGUMENT;
     }
@@ -250,6 +251,8 @@ int set_tuning(const char* key, int value) {
             T.realign = value == kAuto ? kAuto : (value != 0);
         } else if (k == "peel") {
             T.peel = value == kAuto ? kAuto : (value != 0);
+        } else if (k == "wave_run") {
+            T.wave_run = value == kAuto ? kAuto : (value != 0);
         } else {
             return SHMR_EC_INVALID_ARGUMENT;
         }
@@ -286,6 +289,7 @@ int get_tuning(const char* key) {
     if (k == "sc1_store") return T.sc1_store;
     if (k == "realign") return T.realign;
     if (k == "peel") return T.peel;
+    if (k == "wave_run") return T.wave_run;
     return SHMR_EC_INVALID_ARGUMENT;
 }
 
@@ -310,6 +314,7 @@ kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_m
     if (T.serial.load() != kAuto) v.serial = T.serial.load() != 0;
     if (T.sc1_store.load() != kAuto) v.sc1_store = T.sc1_store.load() != 0;
     if (T.peel.load() != kAuto) v.peel = T.peel.load() != 0;
+    if (T.wave_run.load() != kAuto) v.wave_run = T.wave_run.load() != 0;
     if (v.sc1_store) v.nt_store = false;   // one store policy per kernel
     if (v.glds) v.early = v.spre = false;   // the LDS-DMA ring is a form of the plain tile
     if (v.glds || v.depth != 2) v.peel = false;   // peeling is a form of the depth-2 register ring

@@ -384,6 +384,16 @@ __device__ __forceinline__ void realign_tile(const ApplyArgs& a, const Ctx& c, c
     X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPeel) \
     X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial | kPeel) \
     X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kSerial | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSerial | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kPeel | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kPeel | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kPeel | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kPeel | kWaveRun) \
     X(1, kNtLoad | kNtStore | kDepth2 | kSegs) \
     X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse) \
     X(2, kNtLoad | kNtStore | kDepth2 | kSegs) \

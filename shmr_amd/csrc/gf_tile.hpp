@@ -62,6 +62,11 @@ constexpr int kRealign = 1 << 24;
 // last shard (the default ring re-reads shard k-1 there: one extra wave load
 // per shard run, an L2 hit) and still no load behind a branch inside the loop
 constexpr int kPeel = 1 << 25;
+// tools: U > 1 slots of a lane in wave-contiguous runs (chunk (w * U + u) *
+// 64 + lane: each wave covers one contiguous U KiB run) instead of
+// workgroup-strided slots (u * TH + tid) -- fewer partial cache lines at run
+// edges when the shards are off alignment
+constexpr int kWaveRun = 1 << 26;
 // Bits 12-15: occupancy target in waves per SIMD (0 = compiler's choice);
 // the register allocator must then fit 512 / target VGPRs.
 constexpr int kOccShift = 12;
@@ -332,7 +337,17 @@ __device__ __forceinline__ void ring2_peeled(Load& load, Consume& consume, uint3
     }
 }
 
-// One tile: lanes own columns col0 + (u * TH + tid) * 16, u < U.
+// Column chunk of a lane's slot u: workgroup-strided (u * TH + tid) or, with
+// kWaveRun, the wave's contiguous run ((w * U + u) * 64 + lane).
+template <int U, int TH, int F>
+__device__ __forceinline__ uint64_t slot_chunk(int u, uint32_t tid) {
+    if constexpr ((F & kWaveRun) != 0 && U > 1)
+        return uint64_t((tid & ~63u) * U + uint32_t(u) * 64u + (tid & 63u));
+    else
+        return uint64_t(u) * TH + tid;
+}
+
+// One tile: lanes own columns col0 + slot_chunk(u, tid) * 16, u < U.
 //
 // sched_barrier(0) pins program order: without it the scheduler sinks the
 // look-ahead loads next to their consumers and the wave drains vmcnt(0)
@@ -413,7 +428,7 @@ __device__ __forceinline__ void do_tile(const ApplyArgs& a, const Ctx& c, const 
         const uint32_t tt = t < k ? t : k - 1;
         const uint8_t* base = ib + c.s_in_off[tt];
 #pragma unroll
-        for (int u = 0; u < U; ++u) buf[u] = ld<MODE, F>(base, col0 + (uint64_t(u) * TH + tid) * 16, len);
+        for (int u = 0; u < U; ++u) buf[u] = ld<MODE, F>(base, col0 + slot_chunk<U, TH, F>(u, tid) * 16, len);
     };
     auto consume = [&](const u32x4 (&buf)[U], uint32_t t) {
         Tab tb[R];
@@ -445,7 +460,7 @@ __device__ __forceinline__ void do_tile(const ApplyArgs& a, const Ctx& c, const 
         uint8_t* o = ob + c.s_out_off[r];
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            st<MODE, F>(o, col0 + (uint64_t(u) * TH + tid) * 16, len,
+            st<MODE, F>(o, col0 + slot_chunk<U, TH, F>(u, tid) * 16, len,
                         u32x4{acc[u][r][0], acc[u][r][1], acc[u][r][2], acc[u][r][3]});
     }
 }
@@ -571,7 +586,7 @@ __device__ __forceinline__ void early_tile(const ApplyArgs& a, const uint8_t* pl
         const uint32_t t = uint32_t(i) < k ? uint32_t(i) : k - 1;
         const uint8_t* base = ib + uint64_t(plan_u16(in_idx, t)) * a.in_spitch;
 #pragma unroll
-        for (int u = 0; u < U; ++u) ring[i][u] = ld<MODE, F>(base, col0 + (uint64_t(u) * TH + tid) * 16, len);
+        for (int u = 0; u < U; ++u) ring[i][u] = ld<MODE, F>(base, col0 + slot_chunk<U, TH, F>(u, tid) * 16, len);
     }
     __builtin_amdgcn_sched_barrier(0);
     if (!first) lds_barrier();   // the previous tile's LDS readers are done
@@ -591,7 +606,7 @@ __device__ __forceinline__ void early_tile(const ApplyArgs& a, const uint8_t* pl
         const uint32_t tt = t < k ? t : k - 1;
         const uint8_t* base = ib + c.s_in_off[tt];
 #pragma unroll
-        for (int u = 0; u < U; ++u) buf[u] = ld<MODE, F>(base, col0 + (uint64_t(u) * TH + tid) * 16, len);
+        for (int u = 0; u < U; ++u) buf[u] = ld<MODE, F>(base, col0 + slot_chunk<U, TH, F>(u, tid) * 16, len);
     };
     auto consume = [&](const u32x4 (&buf)[U], uint32_t t) {
         Tab tb[R];
@@ -617,7 +632,7 @@ __device__ __forceinline__ void early_tile(const ApplyArgs& a, const uint8_t* pl
         uint8_t* o = ob + c.s_out_off[r];
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            st<MODE, F>(o, col0 + (uint64_t(u) * TH + tid) * 16, len,
+            st<MODE, F>(o, col0 + slot_chunk<U, TH, F>(u, tid) * 16, len,
                         u32x4{acc[u][r][0], acc[u][r][1], acc[u][r][2], acc[u][r][3]});
     }
 }
@@ -785,7 +800,7 @@ inline int variant_flags(const Variant& v) {
            (v.depth == 1 ? kDepth1 : 0) | ((v.occ & 15) << kOccShift) | (v.early ? kEarly : 0) |
            (v.spre ? kSPre : 0) | (v.fuse_tail ? kFuse : 0) | (v.ptrs ? kPtrs : 0) | (v.segs ? kSegs : 0) |
            (v.glds ? kGlds : 0) | (v.serial ? kSerial : 0) | (v.sc1_store ? kSc1Store : 0) |
-           (v.realign ? kRealign : 0) | (v.peel ? kPeel : 0);
+           (v.realign ? kRealign : 0) | (v.peel ? kPeel : 0) | (v.wave_run ? kWaveRun : 0);
 }
 
 }  // namespace

@@ -131,7 +131,7 @@ def test_reconstruct_all_patterns_10_4(gpu):
 
 # --------------------------------------------------------------- device batch API
 KNOBS = ("chunks", "nt_load", "nt_store", "occ8", "grid", "threads", "depth", "wgs_per_cu", "occ", "early", "spre",
-         "fuse_tail", "glds", "serial", "peel")
+         "fuse_tail", "glds", "serial", "peel", "wave_run")
 
 
 def _dev_encode_check(gpu, k, p, L, B, pitch=None, **knobs):
@@ -175,7 +175,7 @@ def test_encode_batch_dev(gpu, k, p, L, B):
 
 
 BASE = dict(chunks=1, nt_load=0, nt_store=0, occ8=0, grid=-1, threads=256, depth=3, wgs_per_cu=0, occ=0, early=0, spre=0,
-            fuse_tail=0, glds=0, serial=0, peel=0)
+            fuse_tail=0, glds=0, serial=0, peel=0, wave_run=0)
 VARIANTS = [dict(BASE, **v) for v in (
     {}, dict(nt_load=1), dict(nt_store=1), dict(nt_load=1, nt_store=1),
     dict(occ8=1, nt_load=1, nt_store=1),
@@ -218,7 +218,10 @@ VARIANTS = [dict(BASE, **v) for v in (
     dict(nt_load=1, nt_store=1, depth=2, early=1, fuse_tail=1, peel=1),
     dict(nt_load=1, nt_store=1, depth=2, fuse_tail=1, peel=1),
     dict(chunks=2, nt_load=1, nt_store=1, depth=2, early=1, serial=1, peel=1),
-    dict(chunks=2, nt_load=1, nt_store=1, depth=2, early=1, fuse_tail=1, serial=1, peel=1))]
+    dict(chunks=2, nt_load=1, nt_store=1, depth=2, early=1, fuse_tail=1, serial=1, peel=1),
+    # U = 2 slots in wave-contiguous runs
+    dict(chunks=2, nt_load=1, nt_store=1, depth=2, early=1, fuse_tail=1, serial=1, wave_run=1),
+    dict(chunks=2, nt_load=1, nt_store=1, depth=2, fuse_tail=1, wave_run=1))]
 
 
 @pytest.mark.parametrize("knobs", VARIANTS, ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items() if BASE[k] != v) or "base")
