@@ -314,7 +314,15 @@ kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_m
     if (T.serial.load() != kAuto) v.serial = T.serial.load() != 0;
     if (T.sc1_store.load() != kAuto) v.sc1_store = T.sc1_store.load() != 0;
     if (T.peel.load() != kAuto) v.peel = T.peel.load() != 0;
-    if (T.wave_run.load() != kAuto) v.wave_run = T.wave_run.load() != 0;
+    // U = 2 slots in wave-contiguous runs on device memory: RS(10,4) packed
+    // encode +1.9 points (misaligned parity stores +2.2), aligned +0.1 - 0.4,
+    // 4-erasure rebuild +0.8 (profiles/r03/r03k/); the realigning, LDS-DMA
+    // and scalar-table tiles keep their own column maps
+    if (T.wave_run.load() != kAuto)
+        v.wave_run = T.wave_run.load() != 0;
+    else
+        v.wave_run = v.u > 1 && v.nt_load && v.depth == 2 && v.threads == 256 && !v.occ8 && !host_mapped && !v.glds &&
+                     !v.spre;
     if (v.sc1_store) v.nt_store = false;   // one store policy per kernel
     if (v.glds) v.early = v.spre = false;   // the LDS-DMA ring is a form of the plain tile
     if (v.glds || v.depth != 2) v.peel = false;   // peeling is a form of the depth-2 register ring
@@ -664,7 +672,7 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
         // realigning-load form of the plain tile
         if (!aligned16_all && g_tune[op].realign.load() == 1 && !ptrs) {
             var.realign = true;
-            var.early = var.spre = var.glds = var.peel = false;   // the realigning tile keeps its own ring
+            var.early = var.spre = var.glds = var.peel = var.wave_run = false;   // the realigning tile keeps its own ring
         }
         // sc1 stores are raw buffer stores: a 2 GiB resource per output row,
         // and 16-byte aligned outputs only (the unaligned-access probe covers

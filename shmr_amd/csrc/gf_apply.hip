@@ -46,25 +46,25 @@ namespace {
 // hipErrorInvalidValue (the C ABI reports SHMR_EC_INVALID_ARGUMENT).
 #define SHMR_VARIANTS_PRODUCT(X) \
     X(1, kNtLoad | kNtStore | kDepth2) \
-    X(2, kNtLoad | kNtStore | kDepth2) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kWaveRun) \
     X(1, kNtStore | kDepth2) \
     X(2, kNtStore | kDepth2) \
     X(1, kNtLoad | kNtStore | kDepth2 | kEarly) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kWaveRun) \
     X(1, kNtLoad | kNtStore | kDepth2 | kFuse) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kFuse) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kWaveRun) \
     X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial | kWaveRun) \
     X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kPeel) \
     X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kPeel) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kPeel) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kPeel | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kPeel | kWaveRun) \
     X(1, kNtLoad | kNtStore | kDepth2 | kPeel) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kPeel | kWaveRun) \
     X(1, kNtLoad | kNtStore | kDepth2 | kFuse | kPeel) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kPeel | kWaveRun) \
     X(1, kNtStore | kDepth2 | kPtrs) \
     X(2, kNtStore | kDepth2 | kPtrs) \
     X(1, kNtStore | kDepth2 | kPtrs | kFuse) \
@@ -74,17 +74,17 @@ namespace {
     X(2, kNtStore | kDepth2 | kPtrs | kSegs) \
     X(2, kNtStore | kDepth2 | kPtrs | kSegs | kFuse) \
     X(1, kNtLoad | kNtStore | kDepth2 | kPtrs) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kPtrs) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kPtrs | kWaveRun) \
     X(1, kNtLoad | kNtStore | kDepth2 | kPtrs | kPeel) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kPtrs | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kPtrs | kPeel | kWaveRun) \
     X(1, kNtLoad | kSc1Store | kDepth2 | kPeel) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kPeel) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kPeel | kWaveRun) \
     X(1, kNtLoad | kSc1Store | kDepth2 | kFuse | kPeel) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kFuse | kPeel) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kFuse | kPeel | kWaveRun) \
     X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kPeel) \
     X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse | kPeel) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs | kPeel) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse | kPeel)
+    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs | kPeel | kWaveRun) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse | kPeel | kWaveRun)
 
 template <int R>
 hipError_t dispatch_full(const ApplyArgs& a, const Variant& v, int grid_cap, hipStream_t s) {

@@ -384,16 +384,8 @@ __device__ __forceinline__ void realign_tile(const ApplyArgs& a, const Ctx& c, c
     X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPeel) \
     X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial | kPeel) \
     X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial | kPeel) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial | kWaveRun) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial | kWaveRun) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kWaveRun) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kWaveRun) \
     X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kSerial | kWaveRun) \
     X(2, kNtLoad | kNtStore | kDepth2 | kSerial | kWaveRun) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kPeel | kWaveRun) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kPeel | kWaveRun) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kPeel | kWaveRun) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kPeel | kWaveRun) \
     X(1, kNtLoad | kNtStore | kDepth2 | kSegs) \
     X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse) \
     X(2, kNtLoad | kNtStore | kDepth2 | kSegs) \
@@ -405,7 +397,23 @@ __device__ __forceinline__ void realign_tile(const ApplyArgs& a, const Ctx& c, c
     X(1, kNtLoad | kSc1Store | kDepth2 | kSegs) \
     X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse) \
     X(2, kNtLoad | kSc1Store | kDepth2 | kSegs) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse)
+    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse) \
+    X(2, kNtLoad | kNtStore | kDepth2) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kFuse) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kPtrs) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kPtrs | kPeel) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kPeel) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kFuse | kPeel) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs | kPeel) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse | kPeel)
 
 template <int R>
 hipError_t dispatch_tools(const ApplyArgs& a, const Variant& v, int grid_cap, hipStream_t s) {

@@ -216,6 +216,9 @@ def test_tuning_api():
     # reconstructs peel the shard ring's tail; encodes keep the look-ahead
     assert "peel=1" in shmr_amd.describe_variant(2, 10, 2) and "peel=1" in shmr_amd.describe_variant(True, 8, 1)
     assert "peel=1" not in shmr_amd.describe_variant(False, 8, 3)
+    # U = 2 launches (4-row encodes and rebuilds) take wave-contiguous runs
+    assert "wave_run=1" in shmr_amd.describe_variant(False, 10, 4) and "wave_run=1" in shmr_amd.describe_variant(True, 10, 4)
+    assert "wave_run=1" not in shmr_amd.describe_variant(False, 8, 3)
     assert "nt_store=0" in shmr_amd.describe_variant(2, 8, 1) and "wgs_per_cu=0" in shmr_amd.describe_variant(2, 8, 1)
     assert "sc1_store" not in shmr_amd.describe_variant(True, 8, 1)
     shmr_amd.set_tuning(sc1_store=-2)
