@@ -40,6 +40,7 @@ struct Tuning {
     std::atomic<int> realign{kAuto};
     std::atomic<int> peel{kAuto};
     std::atomic<int> wave_run{kAuto};
+    std::atomic<int> st_align{kAuto};
 };
 Tuning g_tune[2];   // [kEncode], [kDecode]
 std::atomic<int> g_bounce_kib{kBounceKibDefault};
@@ -202,7 +203,7 @@ int set_tuning(const char* key, int value) {
             {"chunks", kAuto}, {"nt_load", kAuto}, {"nt_store", kAuto}, {"occ8", 0},
             {"grid", -1},      {"diag", 0},        {"threads", 256},    {"depth", kAuto},   {"wgs_per_cu", kAuto},
             {"occ", kAuto},    {"early", kAuto},   {"spre", kAuto},     {"fuse_tail", kAuto},
-            {"glds", kAuto},   {"serial", kAuto},   {"sc1_store", kAuto}, {"realign", kAuto}, {"peel", kAuto}, {"wave_run", kAuto}};
+            {"glds", kAuto},   {"serial", kAuto},   {"sc1_store", kAuto}, {"realign", kAuto}, {"peel", kAuto}, {"wave_run", kAuto}, {"st_align", kAuto}};
         const auto it = kDefaults.find(k);
         return (it != kDefaults.end() && it->second == value) ? SHMR_EC_OK : SHMR_EC_INVALID_ARGUMENT;
     }
@@ -253,6 +254,8 @@ int set_tuning(const char* key, int value) {
             T.peel = value == kAuto ? kAuto : (value != 0);
         } else if (k == "wave_run") {
             T.wave_run = value == kAuto ? kAuto : (value != 0);
+        } else if (k == "st_align") {
+            T.st_align = value == kAuto ? kAuto : (value != 0);
         } else {
             return SHMR_EC_INVALID_ARGUMENT;
         }
@@ -290,6 +293,7 @@ int get_tuning(const char* key) {
     if (k == "realign") return T.realign;
     if (k == "peel") return T.peel;
     if (k == "wave_run") return T.wave_run;
+    if (k == "st_align") return T.st_align;
     return SHMR_EC_INVALID_ARGUMENT;
 }
 
@@ -674,6 +678,9 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
             var.realign = true;
             var.early = var.spre = var.glds = var.peel = var.wave_run = false;   // the realigning tile keeps its own ring
         }
+        // Misaligned output rows (knob "st_align", tools build): aligned
+        // stores realigned across lanes in the full tiles
+        if (!out16 && !ptrs && g_tune[op].st_align.load() == 1 && !var.realign) var.st_align = true;
         // sc1 stores are raw buffer stores: a 2 GiB resource per output row,
         // and 16-byte aligned outputs only (the unaligned-access probe covers
         // the global instructions); otherwise nontemporal global stores

@@ -96,7 +96,8 @@ struct Variant {
     bool sc1_store = false;  // stores with the sc1 cache policy instead of nontemporal
     bool realign = false;    // misaligned shards: aligned loads realigned across lanes (DPP), unaligned stores
     bool peel = false;       // depth-2 ring with the tail peeled (no look-ahead load past the last shard)
-    bool wave_run = false;   // U > 1 slots in wave-contiguous runs (tools)
+    bool wave_run = false;   // U > 1 slots in wave-contiguous runs
+    bool st_align = false;   // misaligned output rows: aligned stores realigned across lanes (tools)
 };
 
 // rows in [1, kMaxRowsPerLaunch].  mode 0: full tiles, every shard base

@@ -272,6 +272,72 @@ __device__ __forceinline__ void realign_tile(const ApplyArgs& a, const Ctx& c, c
     }
 }
 
+// ---- aligned-store runs (flag kStAlign) ------------------------------------
+// An output row off 16-byte alignment by mo (wave-uniform): misaligned 16-byte
+// vector stores cost ~18 % of a streaming copy's rate where misaligned loads
+// cost nothing (profiles/r03/r03m/misalign_bench.jsonl).  The wave's U slots
+// cover one contiguous run of U * 64 chunks at p; lane L of slot u stores the
+// ALIGNED chunk made of its predecessor's last mo bytes and its own first
+// 16 - mo (predecessor by DPP wave_shr:1; slot u > 0's lane 0 takes slot
+// u-1's lane 63 by readlane).  The run's first chunk (lane 0 of slot 0: bytes
+// [mo, 16) of the aligned chunk below p) and the chunk after its end (lane 63
+// of slot U-1: bytes [0, mo)) are partial: masked dword stores plus the split
+// dword's short / byte stores; the neighbouring run writes the complementary
+// bytes.
+__device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {
+    return uint32_t(__builtin_amdgcn_update_dpp(int(old), int(v), 0x138, 0xf, 0xf, false));
+}
+
+template <int U, int F>
+__device__ __forceinline__ void store_run_aligned(uint8_t* p, const u32x4 (&v)[U]) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t mo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(uintptr_t(p)) & 15u)));
+    if (mo == 0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) store16<F>(p + (uint64_t(u) * 64 + lane) * 16, v[u]);
+        return;
+    }
+    uint8_t* a = p - mo;   // the aligned chunk holding the run's first byte
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        u32x4 carry = v[u];
+        if (u > 0)
+            carry = u32x4{uint32_t(__builtin_amdgcn_readlane(int(v[u - 1].x), 63)),
+                          uint32_t(__builtin_amdgcn_readlane(int(v[u - 1].y), 63)),
+                          uint32_t(__builtin_amdgcn_readlane(int(v[u - 1].z), 63)),
+                          uint32_t(__builtin_amdgcn_readlane(int(v[u - 1].w), 63))};
+        const u32x4 prev{dpp_shr1(carry.x, v[u].x), dpp_shr1(carry.y, v[u].y), dpp_shr1(carry.z, v[u].z),
+                         dpp_shr1(carry.w, v[u].w)};
+        if (u > 0 || lane != 0)
+            store16<F>(a + (uint64_t(u) * 64 + lane) * 16, funnel16(prev, v[u], 16u - mo));
+    }
+    const bool head = lane == 0, tail = lane == 63;
+    const u32x4 src = tail ? v[U - 1] : v[0];
+    const u32x4 rot = funnel16(src, src, 16u - mo);   // the lane's bytes in the output chunk's frame
+    uint8_t* q = tail ? a + uint64_t(U) * 1024 : a;
+    const uint32_t w[4] = {rot.x, rot.y, rot.z, rot.w};
+#pragma unroll
+    for (uint32_t d = 0; d < 4; ++d)
+        if ((head && 4 * d >= mo) || (tail && 4 * d + 4 <= mo)) *reinterpret_cast<uint32_t*>(q + 4 * d) = w[d];
+    if (mo & 3u) {
+        const uint32_t d = mo >> 2;
+        uint32_t x = w[0];
+#pragma unroll
+        for (uint32_t j = 1; j < 4; ++j)
+            if (d == j) x = w[j];
+        if ((mo & 3u) == 2u) {   // the split dword's two halves
+            if (head) *reinterpret_cast<uint16_t*>(q + 4 * d + 2) = uint16_t(x >> 16);
+            if (tail) *reinterpret_cast<uint16_t*>(q + 4 * d) = uint16_t(x);
+        } else {
+#pragma unroll
+            for (uint32_t b = 0; b < 4; ++b) {
+                const uint32_t pos = 4 * d + b;
+                if ((head && pos >= mo) || (tail && pos < mo)) q[pos] = uint8_t(x >> (8 * b));
+            }
+        }
+    }
+}
+
 #define SHMR_VARIANTS_TOOLS(X) \
     X(1, 0) \
     X(1, kNtLoad) \
@@ -386,6 +452,20 @@ __device__ __forceinline__ void realign_tile(const ApplyArgs& a, const Ctx& c, c
     X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial | kPeel) \
     X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kSerial | kWaveRun) \
     X(2, kNtLoad | kNtStore | kDepth2 | kSerial | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial | kWaveRun | kStAlign) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial | kWaveRun | kStAlign) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kWaveRun | kStAlign) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kWaveRun | kStAlign) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kStAlign) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kStAlign) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kPeel | kStAlign) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kPeel | kStAlign) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kFuse | kPeel | kStAlign) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kPeel | kStAlign) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kPeel | kWaveRun | kStAlign) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kPeel | kWaveRun | kStAlign) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kPeel | kWaveRun | kStAlign) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kPeel | kWaveRun | kStAlign) \
     X(1, kNtLoad | kNtStore | kDepth2 | kSegs) \
     X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse) \
     X(2, kNtLoad | kNtStore | kDepth2 | kSegs) \

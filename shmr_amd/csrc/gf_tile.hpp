@@ -67,6 +67,10 @@ constexpr int kPeel = 1 << 25;
 // workgroup-strided slots (u * TH + tid) -- fewer partial cache lines at run
 // edges when the shards are off alignment
 constexpr int kWaveRun = 1 << 26;
+// tools: full tiles store misaligned output rows with ALIGNED 16-byte stores
+// (each lane's chunk realigned with the previous lane's by a DPP wavefront
+// shift; the run's two partial chunks by masked narrow stores)
+constexpr int kStAlign = 1 << 27;
 // Bits 12-15: occupancy target in waves per SIMD (0 = compiler's choice);
 // the register allocator must then fit 512 / target VGPRs.
 constexpr int kOccShift = 12;
@@ -255,6 +259,8 @@ __device__ __forceinline__ void st(uint8_t* base, uint64_t col, uint64_t len, u3
 }
 
 // Tools-only forms (gf_apply_tools.hip).
+template <int U, int F>
+__device__ __forceinline__ void store_run_aligned(uint8_t* p, const u32x4 (&v)[U]);
 template <int R>
 __device__ __forceinline__ void diag_mac(uint32_t (&acc)[R][4], const u32x4& d, const Tab (&tb)[R]);
 
@@ -345,6 +351,37 @@ __device__ __forceinline__ uint64_t slot_chunk(int u, uint32_t tid) {
         return uint64_t((tid & ~63u) * U + uint32_t(u) * 64u + (tid & 63u));
     else
         return uint64_t(u) * TH + tid;
+}
+
+// The tile's R output rows from the accumulators.  kStAlign (tools), full
+// tiles: one aligned-store run per wave and row -- the wave's U slots when
+// they are contiguous (kWaveRun, or U = 1), else one run per slot.
+template <int R, int U, int TH, int MODE, int F>
+__device__ __forceinline__ void store_rows(uint8_t* ob, const Ctx& c, uint64_t col0, uint64_t len, uint32_t tid,
+                                           const uint32_t (&acc)[U][R][4]) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        uint8_t* o = ob + c.s_out_off[r];
+        if constexpr ((F & kStAlign) != 0 && MODE == 0) {
+            if constexpr (U == 1 || (F & kWaveRun) != 0) {
+                u32x4 v[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) v[u] = u32x4{acc[u][r][0], acc[u][r][1], acc[u][r][2], acc[u][r][3]};
+                store_run_aligned<U, F>(o + col0 + uint64_t((tid & ~63u) * U) * 16, v);
+            } else {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const u32x4 v[1] = {u32x4{acc[u][r][0], acc[u][r][1], acc[u][r][2], acc[u][r][3]}};
+                    store_run_aligned<1, F>(o + col0 + (uint64_t(u) * TH + (tid & ~63u)) * 16, v);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                st<MODE, F>(o, col0 + slot_chunk<U, TH, F>(u, tid) * 16, len,
+                            u32x4{acc[u][r][0], acc[u][r][1], acc[u][r][2], acc[u][r][3]});
+        }
+    }
 }
 
 // One tile: lanes own columns col0 + slot_chunk(u, tid) * 16, u < U.
@@ -455,14 +492,7 @@ __device__ __forceinline__ void do_tile(const ApplyArgs& a, const Ctx& c, const 
             }
         }
     }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        uint8_t* o = ob + c.s_out_off[r];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            st<MODE, F>(o, col0 + slot_chunk<U, TH, F>(u, tid) * 16, len,
-                        u32x4{acc[u][r][0], acc[u][r][1], acc[u][r][2], acc[u][r][3]});
-    }
+    store_rows<R, U, TH, MODE, F>(ob, c, col0, len, tid, acc);
 }
 
 // Byte offset of the LDS input ring (tools, kGlds) behind the staged plan.
@@ -627,14 +657,7 @@ __device__ __forceinline__ void early_tile(const ApplyArgs& a, const uint8_t* pl
             }
         }
     }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        uint8_t* o = ob + c.s_out_off[r];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            st<MODE, F>(o, col0 + slot_chunk<U, TH, F>(u, tid) * 16, len,
-                        u32x4{acc[u][r][0], acc[u][r][1], acc[u][r][2], acc[u][r][3]});
-    }
+    store_rows<R, U, TH, MODE, F>(ob, c, col0, len, tid, acc);
 }
 
 template <int R, int U, int MODE, int F, bool IDENT>
@@ -800,7 +823,8 @@ inline int variant_flags(const Variant& v) {
            (v.depth == 1 ? kDepth1 : 0) | ((v.occ & 15) << kOccShift) | (v.early ? kEarly : 0) |
            (v.spre ? kSPre : 0) | (v.fuse_tail ? kFuse : 0) | (v.ptrs ? kPtrs : 0) | (v.segs ? kSegs : 0) |
            (v.glds ? kGlds : 0) | (v.serial ? kSerial : 0) | (v.sc1_store ? kSc1Store : 0) |
-           (v.realign ? kRealign : 0) | (v.peel ? kPeel : 0) | (v.wave_run ? kWaveRun : 0);
+           (v.realign ? kRealign : 0) | (v.peel ? kPeel : 0) | (v.wave_run ? kWaveRun : 0) |
+           (v.st_align ? kStAlign : 0);
 }
 
 }  // namespace

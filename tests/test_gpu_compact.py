@@ -126,14 +126,15 @@ def test_compact_inconsistent_shards_follow_crate(gpu):
 
 
 @pytest.mark.parametrize("off", [3, 0])
-@pytest.mark.parametrize("path", ["auto", "realign", "dpp"])
+@pytest.mark.parametrize("path", ["auto", "realign", "dpp", "st_align"])
 def test_compact_packed_layout(gpu, path, off):
     """The reference's packed block buffer (shard i at i * S, RS(10,4) 16 MiB:
     off 16-byte alignment) read in place, rebuilt shards to a compact output
     whose rows are misaligned too (off = 3) or start aligned (off = 0: sc1
     stores allowed).  "realign": the tools build's realigning kernel (knob
     uvec=0) instead of the unaligned vector path; "dpp": aligned loads
-    realigned across lanes (uvec=1, realign=1)."""
+    realigned across lanes (uvec=1, realign=1); "st_align": aligned stores
+    realigned across lanes (uvec=1, st_align=1)."""
     import torch
 
     def check():
@@ -165,11 +166,12 @@ def test_compact_packed_layout(gpu, path, off):
     if path == "auto":
         return check()
     with _native.tools():
-        shmr_amd.set_tuning(uvec=0) if path == "realign" else shmr_amd.set_tuning(uvec=1, realign=1)
+        knobs = {"realign": dict(uvec=0), "dpp": dict(uvec=1, realign=1), "st_align": dict(uvec=1, st_align=1)}[path]
+        shmr_amd.set_tuning(**knobs)
         try:
             check()
         finally:
-            shmr_amd.set_tuning(uvec=-2, realign=-2)
+            shmr_amd.set_tuning(uvec=-2, realign=-2, st_align=-2)
 
 
 @pytest.mark.parametrize("k", [8, 7])

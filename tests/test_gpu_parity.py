@@ -617,7 +617,7 @@ def test_device_buffer_view_keeps_buffer_alive(gpu):
 
 # ------------------------------------------------ misaligned (contiguous) layouts
 @pytest.mark.gpu
-@pytest.mark.parametrize("path", ["auto", "realign", "vector", "dpp"])
+@pytest.mark.parametrize("path", ["auto", "realign", "vector", "dpp", "st_align"])
 @pytest.mark.parametrize("k,p,L,B,off", [
     (10, 4, 1677722, 3, 0),      # RS(10,4) 16 MiB: the reference's block buffer, shard i at i * S
     (8, 3, 524288 + 4096 + 5, 4, 3),   # odd pitch and a misaligned base
@@ -632,7 +632,8 @@ def test_contiguous_layout_realigned(gpu, path, k, p, L, B, off):
     probe); tools build "realign" (knob uvec=0): the realigning kernel for full
     4 KiB tiles, the remainder byte-granular; "vector" (uvec=1): the vector
     kernels unconditionally; "dpp" (uvec=1, realign=1): aligned loads realigned
-    across lanes with a DPP wavefront shift.  Encode into the buffer's parity slots, then
+    across lanes with a DPP wavefront shift; "st_align" (uvec=1, st_align=1):
+    aligned stores realigned across lanes, partial chunks at the runs' ends.  Encode into the buffer's parity slots, then
     rebuild two erased shards per block in place, all against the oracle;
     bytes outside the shards stay untouched."""
     if path == "auto":
@@ -641,10 +642,12 @@ def test_contiguous_layout_realigned(gpu, path, k, p, L, B, off):
         shmr_amd.set_tuning(uvec=0 if path == "realign" else 1)
         if path == "dpp":
             shmr_amd.set_tuning(realign=1)
+        if path == "st_align":
+            shmr_amd.set_tuning(st_align=1)
         try:
             _contiguous_layout_check(gpu, k, p, L, B, off)
         finally:
-            shmr_amd.set_tuning(uvec=-2, realign=-2)
+            shmr_amd.set_tuning(uvec=-2, realign=-2, st_align=-2)
 
 
 def _contiguous_layout_check(gpu, k, p, L, B, off):

@@ -4,8 +4,8 @@ shards and the parity shards each either in the reference's packed block
 buffer (shard i of block b at (b*(k+p) + i) * S, off 16-byte alignment when
 S % 16 != 0; block.rs:408-419) or in 4 KiB-aligned slots, interleaved rounds
 in one process, the product policy against the DPP-realigned loads (tools
-knobs uvec=1, realign=1) and the wave-contiguous slot mapping (wave_run=1,
-with and without the early prologue).
+knobs uvec=1, realign=1) and the realigned aligned stores (st_align=1, with
+and without the early prologue).
 
     python tools/misalign_split.py [--k 10 --p 4 --block-mib 16 --blocks 64]
 """
@@ -25,9 +25,9 @@ import torch  # noqa: E402
 os.environ.setdefault("SHMR_EC_FLAVOUR", "tools")   # kernel knobs: the tools build
 import shmr_amd  # noqa: E402
 
-_AUTO = dict(uvec=-2, realign=-2, wave_run=-2, early=-2, serial=-2)
-VARIANTS = {"policy": _AUTO, "realign": dict(_AUTO, uvec=1, realign=1), "wave_run": dict(_AUTO, wave_run=1),
-            "wave_run_plain": dict(_AUTO, wave_run=1, early=0, serial=0)}
+_AUTO = dict(uvec=-2, realign=-2, wave_run=-2, early=-2, serial=-2, st_align=-2)
+VARIANTS = {"policy": _AUTO, "realign": dict(_AUTO, uvec=1, realign=1), "st_align": dict(_AUTO, st_align=1),
+            "st_align_plain": dict(_AUTO, st_align=1, early=0, serial=0)}
 
 
 def main():
