@@ -7,7 +7,9 @@
 //   hipcc -O3 --offload-arch=gfx950 tools/membench.hip -o tools/_bin/membench
 //   membench [shard_bytes=524288] [blocks=512] [iters=20]
 //   env: MEMBENCH_ALLOC=contig (physically contiguous VRAM), MEMBENCH_ONLY=83 | 104,
-//        MEMBENCH_PITCH=<bytes> (shard slot > S: padded layout, bench.py --pitch-pad)
+//        MEMBENCH_PITCH=<bytes> (shard slot > S: padded layout, bench.py --pitch-pad; a slot
+//        off 16-byte alignment, e.g. 1677722 with S = 1671168, puts shards where the
+//        reference's packed RS(10,4) block buffer has them), MEMBENCH_ONLY=102 (10 -> 2)
 //
 // Prints one JSON line per (pattern, variant): TB/s of algorithmic bytes
 // (K + R) * S * B and the fraction of the 8 TB/s HBM peak.
@@ -19,6 +21,7 @@
 #include <cstring>
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef u32x4 u32x4_u __attribute__((aligned(1)));   // MEMBENCH_PITCH may put shards off 16-byte alignment
 
 #define CK(x)                                                                                \
     do {                                                                                     \
@@ -33,13 +36,13 @@ constexpr int kNtL = 1, kNtS = 2, kRemap = 4;
 
 template <int F>
 __device__ __forceinline__ u32x4 ld(const uint8_t* p) {
-    if constexpr (F & kNtL) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-    else return *reinterpret_cast<const u32x4*>(p);
+    if constexpr (F & kNtL) return __builtin_nontemporal_load(reinterpret_cast<const u32x4_u*>(p));
+    else return *reinterpret_cast<const u32x4_u*>(p);
 }
 template <int F>
 __device__ __forceinline__ void st(uint8_t* p, u32x4 v) {
-    if constexpr (F & kNtS) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
-    else *reinterpret_cast<u32x4*>(p) = v;
+    if constexpr (F & kNtS) __builtin_nontemporal_store(v, reinterpret_cast<u32x4_u*>(p));
+    else *reinterpret_cast<u32x4_u*>(p) = v;
 }
 
 // K == 0: write-only.  R == 0: read-only (one conditional atomic per lane).
@@ -162,6 +165,10 @@ int main(int argc, char** argv) {
         if (only && std::strcmp(only, "104") == 0) {   // the RS(10,4) encode pattern only
             run<10, 4, 1, kNtL | kNtS>("nt", in, out, S, B, sink, iters);
             run<10, 4, 2, kNtL | kNtS>("nt", in, out, S, B, sink, iters);
+            continue;
+        }
+        if (only && std::strcmp(only, "102") == 0) {   // the RS(10,4) 2-erasure rebuild's streams
+            run<10, 2, 1, kNtL | kNtS>("nt", in, out, S, B, sink, iters);
             continue;
         }
         pattern<8, 3>(in, out, S, B, sink, iters);
