@@ -1,0 +1,2 @@
+#!/bin/bash
+exec bash "$(dirname "$0")/r03p.sh" 1
