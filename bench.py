@@ -19,6 +19,7 @@ blocks bit-for-bit.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import platform
@@ -88,6 +89,11 @@ def parse():
                          "[blocks][erasures][pitch] output -- the crate's semantics, every None shard rebuilt into "
                          "a fresh buffer (reference src/vfs/block.rs:556-565; shmr_ec_reconstruct_batch_dev_out; "
                          "default) -- or in place, in their block's own slots")
+    ap.add_argument("--layout", default="batch", choices=["batch", "ptrs"],
+                    help="batch: one [blocks][shards][pitch] tensor per role (shmr_ec_*_batch_dev); ptrs: every "
+                         "shard its own GPU allocation named by a pointer table (shmr_ec_*_ptrs_dev) -- the "
+                         "crate's shape, where each shard is a Vec<u8> of its own (reference block.rs:408-427) and "
+                         "each rebuilt shard a fresh buffer (block.rs:556-565); not with codec104")
     ap.add_argument("--process-model", default="process", choices=["process", "single"],
                     help="process: one process per GPU (torchrun, or self-spawned for --gpus N); single: one "
                          "process drives all N GPUs with one host thread + stream each (the reference daemon's "
@@ -222,12 +228,17 @@ class Workload:
     and the step that runs the hot path over all of them on `stream`."""
 
     def __init__(self, args, shape, dev, rank, world, rs, stream):
-        self.shape, self.dev, self.rank, self.rs, self.stream = shape, dev, rank, rs, stream
+        self.shape, self.dev, self.rank, self.world, self.rs, self.stream = shape, dev, rank, world, rs, stream
         self.bufs = []
         k, p, S, B, pitch = shape.k, shape.p, shape.S, shape.B, shape.pitch
         g = torch.Generator(device=dev)
         g.manual_seed(SEED + rank)
         self.args = args
+        self.ptrs = args.layout == "ptrs"
+        if self.ptrs:
+            self._init_ptrs(g)
+            torch.cuda.synchronize(dev)
+            return
         with torch.cuda.device(dev), torch.cuda.stream(stream):
             if shape.erasures is None:
                 self.data = self.vram((B, k, pitch))
@@ -263,6 +274,47 @@ class Workload:
                         self.shards[self.erased] = 0
         torch.cuda.synchronize(dev)
 
+    def _init_ptrs(self, g):
+        """--layout ptrs: every shard a separate torch allocation (the crate's
+        Vec<u8> per shard); the pointer table is marshalled once, as a Rust
+        shim would keep its Vec of pointers, and each step is one C call."""
+        sh, dev, rs = self.shape, self.dev, self.rs
+        k, p, S, B = sh.k, sh.p, sh.S, sh.B
+        t = k + p
+        if sh.codec:
+            raise SystemExit("--layout ptrs: encode and decode configs only (not codec104)")
+        with torch.cuda.device(dev), torch.cuda.stream(self.stream):
+            blocks = [[torch.randint(0, 256, (S,), dtype=torch.uint8, device=dev, generator=g) for _ in range(k)]
+                      + [torch.zeros(S, dtype=torch.uint8, device=dev) for _ in range(p)] for _ in range(B)]
+            self.stream_ptr = ctypes.c_void_p(self.stream.cuda_stream)
+            self.blocks = blocks
+            if sh.erasures is None:
+                self.keep, _, _, self.ptab = rs._dev_table(blocks, lambda b, i: True)
+                # [B, k|p, S] views for the cpu_baseline leg's parity check (copies, after timing)
+                self.data = _Stacked(blocks, 0, k)
+                self.parity = _Stacked(blocks, k, t)
+                return
+            rs.encode_ptrs_dev(blocks)
+            present = np.ones((B, t), dtype=np.uint8)
+            gb = np.array(placement.weak_batch(B, self.rank, self.world))     # global block ids of this device
+            if sh.erasures == 1:
+                present[np.arange(B), gb % k] = 0
+            else:
+                present[np.arange(B), gb % 10] = 0
+                present[np.arange(B), (gb + 3) % 10] = 0
+            self.present = present
+            # absent entries: fresh output buffers (the crate allocates vec![0; len] per None)
+            self.originals = [[blocks[b][i].clone() for i in np.flatnonzero(present[b] == 0)] for b in range(B)]
+            self.outs = [[torch.zeros(S, dtype=torch.uint8, device=dev) for _ in np.flatnonzero(present[b] == 0)]
+                         for b in range(B)]
+            table = []
+            for b in range(B):
+                it = iter(self.outs[b])
+                table.append([blocks[b][i] if present[b, i] else next(it) for i in range(t)])
+            self.keep, _, _, self.ptab = rs._dev_table(table, lambda b, i: True)
+            self.shards = _Stacked(blocks, 0, t)
+            self.rebuilt = _Stacked(self.outs, 0, sh.erasures)
+
     def vram(self, shape):
         """Batch tensor: torch's allocator, or with --contig physically
         contiguous VRAM from shmr_ec_device_alloc (footprint)."""
@@ -273,6 +325,10 @@ class Workload:
 
     def encode(self):
         sh = self.shape
+        if self.ptrs:
+            _native_check(self.rs._L.shmr_ec_encode_ptrs_dev(self.rs._h, self.ptab, sh.B, sh.S, self.dev.index,
+                                                             self.stream_ptr))
+            return
         if sh.erasures is None:
             self.rs.encode_batch_dev(self.data, self.parity, shard_len=sh.S)
         else:
@@ -280,6 +336,12 @@ class Workload:
                                      data_shard_pitch=sh.pitch, parity_shard_pitch=sh.pitch)
 
     def rebuild(self):
+        if self.ptrs:
+            pr = self.present
+            _native_check(self.rs._L.shmr_ec_reconstruct_ptrs_dev(
+                self.rs._h, self.ptab, pr.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), self.shape.B, self.shape.S,
+                0, self.dev.index, self.stream_ptr))
+            return
         if self.shape.compact:
             self.rs.reconstruct_batch_dev_out(self.shards, self.present, self.rebuilt, shard_len=self.shape.S)
         else:
@@ -351,6 +413,27 @@ class Workload:
         return ok
 
 
+class _Stacked:
+    """[B, rows, S] view of per-shard tensors for the cpu_baseline leg: indexing
+    [:nb, :, :S] stacks the first nb blocks' shards (a copy, after the timed
+    region)."""
+
+    def __init__(self, blocks, lo, hi):
+        self.blocks, self.lo, self.hi = blocks, lo, hi
+        self.shape = (len(blocks), hi - lo, blocks[0][lo].numel() if blocks else 0)
+
+    def __getitem__(self, idx):
+        nb = range(len(self.blocks))[idx[0]] if isinstance(idx, tuple) else range(len(self.blocks))[idx]
+        rest = idx[1:] if isinstance(idx, tuple) else ()
+        st = torch.stack([torch.stack(self.blocks[b][self.lo:self.hi]) for b in nb])
+        return st[(slice(None),) + rest] if rest else st
+
+
+def _native_check(rc):
+    if rc != 0:
+        raise RuntimeError(f"shmr_ec call failed: {_native.lib().shmr_ec_status_name(rc).decode()}")
+
+
 def device_identity(dev, rank):
     props = torch.cuda.get_device_properties(dev)
     return {"rank": rank, "device": dev.index,
@@ -398,11 +481,15 @@ def report(args, shape, world, ranks, elapsed, step_ms, ramp_steps, process_mode
             "tuning": shape.tuning,
             "memory": ("physically contiguous VRAM (shmr_ec_device_alloc)" if args.contig
                        else "torch caching allocator (hipMalloc)"),
-            "shard_pitch_bytes": shape.pitch,
+            "shard_pitch_bytes": None if args.layout == "ptrs" else shape.pitch,
             "rebuild_out": (None if shape.erasures is None else
+                            "a fresh buffer per None shard, named by the pointer table (crate semantics)"
+                            if args.layout == "ptrs" else
                             "compact [blocks][erasures][pitch] output (crate semantics: a fresh buffer per None "
                             "shard)" if shape.compact else "in place, in the erased shards' own slots"),
-            "shard_layout": ("contiguous shards (the reference's block buffer)" if shape.pitch == shape.S else
+            "shard_layout": ("every shard a separate torch allocation, named by a pointer table (shmr_ec_*_ptrs_dev: "
+                             "the crate's Vec<u8> per shard)" if args.layout == "ptrs" else
+                             "contiguous shards (the reference's block buffer)" if shape.pitch == shape.S else
                              f"shard slots of {shape.pitch} B for {shape.S} B shards"
                              + (" (one 4 KiB page past the 4 KiB-aligned size for a power-of-two stride, "
                                 "DESIGN.md section 4)" if shape.pitch - shape.S >= 4096 else " (4 KiB-aligned)")),
@@ -572,6 +659,8 @@ def traffic_key(args) -> str:
     "+contig" for --pitch-pad 0 on a power-of-two shard, "+inplace" for a
     decode rebuilt in place (the compact output is the default)."""
     key = args.config
+    if args.layout == "ptrs":
+        return key + "+ptrs"
     if args.pitch_align == 1:
         key += "+packed"
     elif args.pitch_pad == 0:

@@ -179,6 +179,26 @@ int shmr_ec_reconstruct_batch_dev_out(shmr_ec_t* rs, const uint8_t* d_shards, si
                                       size_t out_shard_pitch, size_t out_block_pitch, int device,
                                       void* stream);
 
+/* Device-resident shards that live anywhere -- the crate's own argument shape
+ * (ReedSolomon::encode(&mut [Vec<u8>]) at block.rs:427 over shards that
+ * block.rs:408-419 copies into a Vec each; reconstruct(&mut [Option<Vec<u8>>])
+ * at block.rs:560, every None rebuilt into a fresh buffer, :556-565), batched.
+ * d_shards is a HOST array of nblocks x total DEVICE pointers:
+ * d_shards[b*total + i] is shard i of block b, shard_len bytes, any alignment
+ * (16-byte aligned shards take the vector kernels; otherwise the device's
+ * verified unaligned access mode, else byte-granular).  The table is copied
+ * before the call returns (the caller may reuse it) and uploaded on `stream`;
+ * stream-ordered and graph-capturable as the calls above.
+ * encode: shards [0, data) in, [data, total) overwritten with parity; every
+ * pointer non-NULL.
+ * reconstruct: present = nblocks x total host flags; absent shards point at
+ * caller buffers that receive the rebuilt bytes (absent parity may be NULL
+ * with data_only != 0); validation and errors as shmr_ec_reconstruct_batch_dev. */
+int shmr_ec_encode_ptrs_dev(shmr_ec_t* rs, uint8_t* const* d_shards, size_t nblocks, size_t shard_len,
+                            int device, void* stream);
+int shmr_ec_reconstruct_ptrs_dev(shmr_ec_t* rs, uint8_t* const* d_shards, const uint8_t* present,
+                                 size_t nblocks, size_t shard_len, int data_only, int device, void* stream);
+
 /* ---- host-buffer batches over one or more GPUs ---------------------------- *
  * Blocks held in HOST memory (the Block Cache / shard file buffers), whole
  * blocks round-robin across `devices` (block b -> devices[b % ndev]); per

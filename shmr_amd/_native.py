@@ -59,6 +59,9 @@ SIGNATURES = [
      [ctypes.c_void_p, ctypes.c_void_p, _sz, _sz, _u8p, _sz, _sz, ctypes.c_int, ctypes.c_void_p, _sz, _sz,
       ctypes.c_int, ctypes.c_void_p]),
     ("shmr_ec_device_init", ctypes.c_int, [ctypes.c_int]),
+    ("shmr_ec_encode_ptrs_dev", ctypes.c_int, [ctypes.c_void_p, _u8pp, _sz, _sz, ctypes.c_int, ctypes.c_void_p]),
+    ("shmr_ec_reconstruct_ptrs_dev", ctypes.c_int,
+     [ctypes.c_void_p, _u8pp, _u8p, _sz, _sz, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     ("shmr_ec_encode_blocks_host", ctypes.c_int,
      [ctypes.c_void_p, _u8pp, _sz, _sz, ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     ("shmr_ec_reconstruct_blocks_host", ctypes.c_int,

@@ -497,6 +497,93 @@ int shmr_ec_reconstruct_batch_dev_out(shmr_ec_t* rs, const uint8_t* d_shards, si
     });
 }
 
+// ---- device-resident shards anywhere: shard-pointer tables --------------------------
+// The crate's own shape (block.rs:408-427: every shard its own Vec<u8>; :556-565:
+// every None shard rebuilt into a fresh buffer) on device memory.  The host
+// table d_shards[b * total + i] is copied into a pinned slot of the device's
+// pointer ring and uploaded on the caller's stream (inside a capture: into
+// permanent arena memory, which every replay re-reads).
+static int ptrs_dev(shmr_ec_t* rs, uint8_t* const* d_shards, const uint8_t* present, size_t nblocks,
+                    size_t shard_len, int data_only, int device, void* stream_, core::OpClass op) {
+    return guarded([&]() -> int {
+        if (!rs || !d_shards) return SHMR_EC_INVALID_ARGUMENT;
+        if (op == core::kDecode && !present) return SHMR_EC_INVALID_ARGUMENT;
+        if (nblocks == 0) return SHMR_EC_OK;
+        if (shard_len == 0) return SHMR_EC_EMPTY_SHARD;
+        Codec& c = *rs->codec;
+        const unsigned k = c.k(), t = k + c.p();
+        int rc = SHMR_EC_OK;
+        if (op == core::kDecode && (rc = core::validate_presence(c, present, nblocks))) return rc;
+        bool aligned = true;   // every shard the launch touches 16-byte aligned
+        for (size_t b = 0; b < nblocks; ++b)
+            for (unsigned i = 0; i < t; ++i) {
+                const uint8_t* p = d_shards[b * t + i];
+                // absent parity under data_only is neither read nor written
+                const bool needed = op == core::kEncode || present[b * t + i] || i < k || !data_only;
+                if (!p) {
+                    if (needed) return SHMR_EC_INVALID_ARGUMENT;
+                    continue;
+                }
+                aligned = aligned && (uintptr_t(p) & 15u) == 0;
+            }
+        rc = core::check_device(device);
+        if (rc) return rc;
+        core::DeviceScope scope(device);
+        if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
+        const hipStream_t stream = static_cast<hipStream_t>(stream_);
+        rc = core::device_init(device, stream);
+        if (rc) return rc;
+        auto run = [&](const uint8_t* d_tab, size_t b0, size_t n) -> int {
+            core::Layout L{nullptr, nullptr, 0, 0, 0, 0, 0};
+            L.d_ptrs = reinterpret_cast<const uint64_t*>(d_tab);
+            L.total = t;
+            L.ptrs_aligned = aligned;
+            if (op == core::kEncode) return core::encode_on_device(c, device, L, n, shard_len, stream);
+            return core::reconstruct_on_device(c, device, L, present + b0 * t, n, shard_len, data_only != 0, stream);
+        };
+        static_assert(sizeof(uint8_t*) == sizeof(uint64_t), "64-bit device pointers");
+        if (core::stream_capturing(stream)) {
+            const size_t bytes = nblocks * t * sizeof(uint64_t);
+            uint8_t *h = nullptr, *d = nullptr;
+            rc = core::arena_alloc(device, bytes, true, &h, &d);
+            if (rc) return rc;
+            std::memcpy(h, d_shards, bytes);
+            if (hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream) != hipSuccess) {
+                (void)hipGetLastError();
+                return SHMR_EC_DEVICE_ERROR;
+            }
+            return run(d, 0, nblocks);
+        }
+        core::UploadRing* ring = core::UploadRing::for_device(device, &rc, core::UploadRing::kPointers);
+        if (!ring) return rc;
+        const size_t per_chunk = core::UploadRing::kSlotBytes / (sizeof(uint64_t) * t);
+        for (size_t b0 = 0; b0 < nblocks; b0 += per_chunk) {
+            const size_t n = std::min(per_chunk, nblocks - b0);
+            uint8_t *hslot = nullptr, *dslot = nullptr;
+            int slot = -1;
+            rc = ring->acquire(&hslot, &dslot, &slot);
+            if (rc) return rc;
+            std::memcpy(hslot, d_shards + b0 * t, n * t * sizeof(uint64_t));
+            rc = ring->upload(slot, n * t * sizeof(uint64_t), stream);
+            if (rc == SHMR_EC_OK) rc = run(dslot, b0, n);
+            const int rc2 = ring->release_after(slot, stream);
+            if (rc) return rc;
+            if (rc2) return rc2;
+        }
+        return SHMR_EC_OK;
+    });
+}
+
+int shmr_ec_encode_ptrs_dev(shmr_ec_t* rs, uint8_t* const* d_shards, size_t nblocks, size_t shard_len, int device,
+                            void* stream) {
+    return ptrs_dev(rs, d_shards, nullptr, nblocks, shard_len, 0, device, stream, core::kEncode);
+}
+
+int shmr_ec_reconstruct_ptrs_dev(shmr_ec_t* rs, uint8_t* const* d_shards, const uint8_t* present, size_t nblocks,
+                                 size_t shard_len, int data_only, int device, void* stream) {
+    return ptrs_dev(rs, d_shards, present, nblocks, shard_len, data_only, device, stream, core::kDecode);
+}
+
 // ---- host-buffer batches over one or more GPUs -------------------------------------
 static int host_batch(shmr_ec_t* rs, uint8_t* const* host_shards, const uint8_t* present, size_t nblocks,
                       size_t shard_len, int data_only, const int* devices, int ndev, core::OpClass op) {

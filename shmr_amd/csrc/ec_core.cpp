@@ -660,13 +660,14 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
     // buffer, shard i at i * S) take the same vector kernels as aligned ones
     // where the device serves unaligned 16-byte accesses (verified once per
     // device at init; every access still covers only the lane's own bytes),
-    // else the realigning kernel below.  Mapped host shards never do: the
-    // probe covered device memory only.
+    // else the realigning kernel below (pitch layouts; misaligned device
+    // shard-pointer tables then take the byte-granular kernel).  Mapped host
+    // shards never do: the probe covered device memory only.
     const bool out16 = aligned16(uintptr_t(L.out_base)) && aligned16(L.out_bpitch) && aligned16(L.out_spitch);
     const bool aligned16_all =
         ptrs ? L.ptrs_aligned
              : aligned16(uintptr_t(L.in_base)) && aligned16(L.in_bpitch) && aligned16(L.in_spitch) && out16;
-    const bool aligned = aligned16_all || (!ptrs && !L.host_mapped && unaligned_vector(dev));
+    const bool aligned = aligned16_all || (!L.host_mapped && unaligned_vector(dev));
     for (uint32_t row0 = 0; row0 < plan.m; row0 += kern::kMaxRowsPerLaunch) {
         const uint32_t rows = std::min<uint32_t>(kern::kMaxRowsPerLaunch, plan.m - row0);
         count_device(dev, kDevLaunches);
@@ -850,7 +851,11 @@ int reconstruct_on_device(Codec& c, int dev, const Layout& L, const uint8_t* pre
         // no dependent table loads in the kernel prologue.
         {
             std::vector<kern::Seg> segs;
-            bool fits = segs_supported(kDecode, c.k(), L.host_mapped, L.d_ptrs != nullptr, L.compact);
+            // (device shard-pointer tables restage every tile anyway, and their
+            // segment form is compiled only for the mapped-host policy: they take
+            // the table launch with the device policy's loads)
+            bool fits = !(L.d_ptrs && !L.host_mapped) &&
+                        segs_supported(kDecode, c.k(), L.host_mapped, L.d_ptrs != nullptr, L.compact);
             for (size_t i = 0; i < grp.blocks.size() && fits;) {
                 size_t e = i + 1;
                 const uint32_t st = e < grp.blocks.size() ? grp.blocks[e] - grp.blocks[i] : 1;

@@ -300,6 +300,97 @@ class ReedSolomon:
             self._h, ctypes.c_void_p(shards.data_ptr()), shards.stride(1), shards.stride(0), _ptr(pr), B, L,
             int(data_only), ctypes.c_void_p(out.data_ptr()), out.stride(1), out.stride(0), dev, stream))
 
+    # -- device-resident shards anywhere (shard-pointer tables) ----------------------
+    def _dev_table(self, blocks, need_buffer):
+        """Per-block lists of 1-D contiguous uint8 GPU tensors (None allowed
+        where ``need_buffer(b, i)`` is false) -> (tensors kept alive, shard
+        length, device index, ctypes pointer table).  Crate check order per
+        shard list: shard count, EmptyShard, IncorrectShardSize."""
+        import torch
+        t = self.total_shard_count()
+        for blk in blocks:
+            if len(blk) != t:
+                raise Error(-1 if len(blk) < t else -2)          # TooFewShards / TooManyShards
+        L, dev = 0, None
+        for blk in blocks:
+            for s in blk:
+                if s is None:
+                    continue
+                if not isinstance(s, torch.Tensor) or s.dtype != torch.uint8 or not s.is_cuda:
+                    raise TypeError("shards must be torch.uint8 tensors on the GPU (or None)")
+                if not s.is_contiguous():
+                    raise TypeError("shard bytes must be contiguous")
+                if dev is None:
+                    L, dev = s.numel(), s.device.index
+                elif s.device.index != dev:
+                    raise ValueError("every shard of a call must be on one GPU")
+        if blocks and L == 0:
+            raise Error(-11)                                     # EmptyShard
+        flat = []
+        for b, blk in enumerate(blocks):
+            for i, s in enumerate(blk):
+                if s is None:
+                    if need_buffer(b, i):
+                        raise ValueError(f"block {b} shard {i} needs a buffer")
+                    flat.append(None)
+                elif s.numel() != L:
+                    raise Error(-9)                              # IncorrectShardSize
+                else:
+                    flat.append(s)
+        ptrs = (_u8p * max(len(flat), 1))(*[(_u8p() if s is None else ctypes.cast(s.data_ptr(), _u8p)) for s in flat])
+        return flat, L, (dev if dev is not None else torch.cuda.current_device()), ptrs
+
+    def encode_ptrs_dev(self, blocks, device: Optional[int] = None) -> None:
+        """``ReedSolomon::encode`` (reference src/vfs/block.rs:427) for many blocks whose
+        shards are separate GPU buffers -- the crate's shape, where every shard is its
+        own ``Vec<u8>`` (block.rs:408-419).  blocks: per-block lists of ``total``
+        1-D uint8 tensors of one length (data in, parity overwritten).  Enqueued on
+        torch's current stream of their device."""
+        keep, L, dev, ptrs = self._dev_table(blocks, lambda b, i: True)
+        import torch
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        _check(self._L.shmr_ec_encode_ptrs_dev(self._h, ptrs, len(blocks), L,
+                                               dev if device is None else int(device), stream))
+        del keep
+
+    def reconstruct_ptrs_dev(self, blocks, data_only: bool = False, device: Optional[int] = None) -> None:
+        """``ReedSolomon::reconstruct`` / ``reconstruct_data`` (block.rs:560) for many
+        blocks of separate GPU shard buffers, with the crate's semantics: every
+        ``None`` entry becomes a fresh buffer holding the rebuilt shard
+        (block.rs:556-565); absent parity stays ``None`` with ``data_only``.  Blocks
+        with every shard present are left alone; a block with fewer than
+        ``data`` present shards fails the whole call before any launch."""
+        import torch
+        t, k = self.total_shard_count(), self.data_shard_count()
+        for blk in blocks:
+            if len(blk) != t:
+                raise Error(-1 if len(blk) < t else -2)
+        present = np.array([[s is not None for s in blk] for blk in blocks], dtype=np.uint8).reshape(len(blocks), t)
+        for row in present:
+            if row.sum() != t and row.sum() < k:
+                raise Error(-10)                                 # TooFewShardsPresent
+        live = [s for blk in blocks for s in blk if s is not None]
+        if not live:
+            return
+        L, dev0 = live[0].numel(), live[0].device
+        # the crate allocates each None shard (vec![0; len]); here: a fresh GPU buffer
+        fresh = [list(blk) for blk in blocks]
+        for b, blk in enumerate(fresh):
+            if present[b].all():
+                continue
+            for i in range(t):
+                if blk[i] is None and not (data_only and i >= k):
+                    blk[i] = torch.zeros(L, dtype=torch.uint8, device=dev0)
+        keep, L, dev, ptrs = self._dev_table(fresh, lambda b, i: not (data_only and i >= k))
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        _check(self._L.shmr_ec_reconstruct_ptrs_dev(self._h, ptrs, _ptr(present), len(blocks), L, int(data_only),
+                                                    dev if device is None else int(device), stream))
+        for b, blk in enumerate(blocks):
+            for i in range(t):
+                if blk[i] is None and fresh[b][i] is not None:
+                    blk[i] = fresh[b][i]
+        del keep
+
     def _host_ptrs(self, blocks):
         t = self.total_shard_count()
         if isinstance(blocks, np.ndarray):

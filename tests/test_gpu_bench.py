@@ -33,7 +33,9 @@ def run_bench(*args):
 @pytest.mark.gpu
 @pytest.mark.parametrize("config,blocks,extra", [("encode83", 16, ()), ("decode83", 16, ()), ("codec104", 4, ()),
                                                 ("decode83", 16, ("--rebuild-out", "inplace")),
-                                                ("codec104", 4, ("--rebuild-out", "inplace"))])
+                                                ("codec104", 4, ("--rebuild-out", "inplace")),
+                                                ("encode83", 16, ("--layout", "ptrs")),
+                                                ("decode104", 4, ("--layout", "ptrs"))])
 def test_bench_line_contract(gpu, config, blocks, extra):
     d = run_bench("--config", config, "--blocks", str(blocks), *extra)
     assert KEYS <= set(d)
@@ -48,7 +50,7 @@ def test_bench_line_contract(gpu, config, blocks, extra):
     assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0 and c["sample"]
     if config == "encode83":
         assert c["gpu_parity_bit_exact_on_sample"] is True
-    elif config == "decode83":
+    elif config in ("decode83", "decode104"):
         assert c["gpu_rebuilt_bit_exact_on_sample"] is True
     else:
         assert r["round_trip_bit_exact"] is True
