@@ -26,3 +26,8 @@ KEY=encode104+packed BENCH_EXTRA="--pitch-align 1" bash "$D/profile.sh" "$T" enc
 KEY=decode104+packed BENCH_EXTRA="--pitch-align 1" bash "$D/profile.sh" "$T" decode104 64 $((64 * 12 * 1677722))
 KEY=encode83+contig BENCH_EXTRA="--pitch-pad 0" bash "$D/profile.sh" "$T" encode83 512 2952790016
 KEY=decode83+contig BENCH_EXTRA="--pitch-pad 0" bash "$D/profile.sh" "$T" decode83 512 2415919104
+# round 3: every shard its own allocation, named by a pointer table (the crate's shape, --layout ptrs)
+KEY=encode83+ptrs BENCH_EXTRA="--layout ptrs" bash "$D/profile.sh" "$T" encode83 512 2952790016
+KEY=decode83+ptrs BENCH_EXTRA="--layout ptrs" bash "$D/profile.sh" "$T" decode83 512 2415919104
+KEY=encode104+ptrs BENCH_EXTRA="--layout ptrs" bash "$D/profile.sh" "$T" encode104 64 $((64 * 14 * 1677722))
+KEY=decode104+ptrs BENCH_EXTRA="--layout ptrs" bash "$D/profile.sh" "$T" decode104 64 $((64 * 12 * 1677722))
