@@ -41,6 +41,7 @@ struct Tuning {
     std::atomic<int> peel{kAuto};
     std::atomic<int> wave_run{kAuto};
     std::atomic<int> st_align{kAuto};
+    std::atomic<int> xcd{kAuto};
 };
 Tuning g_tune[2];   // [kEncode], [kDecode]
 std::atomic<int> g_bounce_kib{kBounceKibDefault};
@@ -203,7 +204,8 @@ int set_tuning(const char* key, int value) {
             {"chunks", kAuto}, {"nt_load", kAuto}, {"nt_store", kAuto}, {"occ8", 0},
             {"grid", -1},      {"diag", 0},        {"threads", 256},    {"depth", kAuto},   {"wgs_per_cu", kAuto},
             {"occ", kAuto},    {"early", kAuto},   {"spre", kAuto},     {"fuse_tail", kAuto},
-            {"glds", kAuto},   {"serial", kAuto},   {"sc1_store", kAuto}, {"realign", kAuto}, {"peel", kAuto}, {"wave_run", kAuto}, {"st_align", kAuto}};
+            {"glds", kAuto},   {"serial", kAuto},   {"sc1_store", kAuto}, {"realign", kAuto}, {"peel", kAuto}, {"wave_run", kAuto}, {"st_align", kAuto},
+            {"xcd", kAuto}};
         const auto it = kDefaults.find(k);
         return (it != kDefaults.end() && it->second == value) ? SHMR_EC_OK : SHMR_EC_INVALID_ARGUMENT;
     }
@@ -256,6 +258,8 @@ int set_tuning(const char* key, int value) {
             T.wave_run = value == kAuto ? kAuto : (value != 0);
         } else if (k == "st_align") {
             T.st_align = value == kAuto ? kAuto : (value != 0);
+        } else if (k == "xcd") {
+            T.xcd = value == kAuto ? kAuto : (value != 0);
         } else {
             return SHMR_EC_INVALID_ARGUMENT;
         }
@@ -294,6 +298,7 @@ int get_tuning(const char* key) {
     if (k == "peel") return T.peel;
     if (k == "wave_run") return T.wave_run;
     if (k == "st_align") return T.st_align;
+    if (k == "xcd") return T.xcd;
     return SHMR_EC_INVALID_ARGUMENT;
 }
 
@@ -318,6 +323,7 @@ kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_m
     if (T.serial.load() != kAuto) v.serial = T.serial.load() != 0;
     if (T.sc1_store.load() != kAuto) v.sc1_store = T.sc1_store.load() != 0;
     if (T.peel.load() != kAuto) v.peel = T.peel.load() != 0;
+    if (T.xcd.load() != kAuto) v.xcd = T.xcd.load() != 0;
     // U = 2 slots in wave-contiguous runs on device memory: RS(10,4) packed
     // encode +1.9 points (misaligned parity stores +2.2), aligned +0.1 - 0.4,
     // 4-erasure rebuild +0.8 (profiles/r03/r03k/); the realigning, LDS-DMA

@@ -98,6 +98,7 @@ struct Variant {
     bool peel = false;       // depth-2 ring with the tail peeled (no look-ahead load past the last shard)
     bool wave_run = false;   // U > 1 slots in wave-contiguous runs
     bool st_align = false;   // misaligned output rows: aligned stores realigned across lanes (tools)
+    bool xcd = false;        // XCD-grouped tile order: neighbouring tiles on one XCD's L2 (tools)
 };
 
 // rows in [1, kMaxRowsPerLaunch].  mode 0: full tiles, every shard base

@@ -493,7 +493,15 @@ __device__ __forceinline__ void store_run_aligned(uint8_t* p, const u32x4 (&v)[U
     X(2, kNtLoad | kSc1Store | kDepth2 | kPeel) \
     X(2, kNtLoad | kSc1Store | kDepth2 | kFuse | kPeel) \
     X(2, kNtLoad | kSc1Store | kDepth2 | kSegs | kPeel) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse | kPeel)
+    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial | kWaveRun | kXcd) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial | kWaveRun | kXcd) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kPeel | kXcd) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kPeel | kXcd) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse | kPeel | kXcd) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kPeel | kXcd) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kXcd) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kXcd)
 
 template <int R>
 hipError_t dispatch_tools(const ApplyArgs& a, const Variant& v, int grid_cap, hipStream_t s) {

@@ -71,6 +71,13 @@ constexpr int kWaveRun = 1 << 26;
 // (each lane's chunk realigned with the previous lane's by a DPP wavefront
 // shift; the run's two partial chunks by masked narrow stores)
 constexpr int kStAlign = 1 << 27;
+// tools: XCD-grouped tile order for one-workgroup-per-tile grids.  Dispatch
+// puts workgroup w on XCD w % 8; with w -> tile (w % 8) * q + w / 8 (q = ntiles
+// / 8) each XCD walks one contiguous eighth of the tiles in order, so
+// neighbouring column tiles of a block meet in the same L2 -- the cache lines
+// a misaligned shard's tile boundaries share are fetched (and partial-line
+// stores merged) once instead of on two XCDs
+constexpr int kXcd = 1 << 28;
 // Bits 12-15: occupancy target in waves per SIMD (0 = compiler's choice);
 // the register allocator must then fit 512 / target VGPRs.
 constexpr int kOccShift = 12;
@@ -692,6 +699,19 @@ __device__ __forceinline__ TileRef tile_ref(const ApplyArgs& a, uint64_t tile) {
     return TileRef{j, tile - j * tpb, false};
 }
 
+// First grid tile of this workgroup (kXcd: XCD-grouped, one workgroup per tile).
+template <int F>
+__device__ __forceinline__ uint64_t first_tile(const ApplyArgs& a) {
+    uint64_t w = blockIdx.x;
+    if constexpr ((F & kXcd) != 0) {
+        if (uint64_t(gridDim.x) == a.ntiles) {
+            const uint64_t q = a.ntiles >> 3;
+            if (w < (q << 3)) w = (w & 7u) * q + (w >> 3);
+        }
+    }
+    return w;
+}
+
 // The second __launch_bounds__ argument is amdgpu_waves_per_eu (minimum).
 template <int R, int U, int MODE, int F>
 __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) void gf_apply_kernel(const ApplyArgs a) {
@@ -703,7 +723,7 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
     if constexpr ((F & (kEarly | kSPre)) != 0) {
         const uint64_t tb = uint64_t(TH) * 16 * U;
         bool first = true;
-        for (uint64_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+        for (uint64_t tile = first_tile<F>(a); tile < a.ntiles; tile += gridDim.x) {
             const TileRef tr = tile_ref<F>(a, tile);
             const uint64_t j = tr.j, cc = tr.cc;
             uint64_t blk;
@@ -748,7 +768,7 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
         __syncthreads();
     }
     const uint64_t tb = uint64_t(TH) * 16 * U;
-    for (uint64_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    for (uint64_t tile = first_tile<F>(a); tile < a.ntiles; tile += gridDim.x) {
         const TileRef tr = tile_ref<F>(a, tile);
         const uint64_t j = tr.j, cc = tr.cc;
         const uint8_t* plan = a.plan;
@@ -824,7 +844,7 @@ inline int variant_flags(const Variant& v) {
            (v.spre ? kSPre : 0) | (v.fuse_tail ? kFuse : 0) | (v.ptrs ? kPtrs : 0) | (v.segs ? kSegs : 0) |
            (v.glds ? kGlds : 0) | (v.serial ? kSerial : 0) | (v.sc1_store ? kSc1Store : 0) |
            (v.realign ? kRealign : 0) | (v.peel ? kPeel : 0) | (v.wave_run ? kWaveRun : 0) |
-           (v.st_align ? kStAlign : 0);
+           (v.st_align ? kStAlign : 0) | (v.xcd ? kXcd : 0);
 }
 
 }  // namespace
