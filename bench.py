@@ -201,7 +201,10 @@ class Shape:
         self.erasures = -erasures if self.codec else erasures
         self.compact = self.erasures is not None and args.rebuild_out == "compact"
         rows = p if self.erasures is None else self.erasures
-        self.tuning = shmr_amd.describe_variant(0 if self.erasures is None else 2 if self.compact else 1, k, rows)
+        mode = 0 if self.erasures is None else 2 if self.compact else 1
+        if args.layout == "ptrs":
+            mode = 3 if self.erasures is None else 4
+        self.tuning = shmr_amd.describe_variant(mode, k, rows)
         if self.codec:
             self.tuning = f"encode: {shmr_amd.describe_variant(False, k, p)}; reconstruct: {self.tuning}"
         # HBM layout: shard i of block b at (b*k + i) * pitch with pitch = S

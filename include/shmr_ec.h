@@ -304,7 +304,8 @@ int shmr_ec_get_tuning(const char* key);
 
 /* Writes the kernel variant that a launch of `rows` output rows over
  * `data_shards` inputs would use (encode: decode=0, reconstruct in place:
- * decode=1, reconstruct into a compact output: decode=2). */
+ * decode=1, reconstruct into a compact output: decode=2; over 16-byte aligned
+ * device shard-pointer tables, *_ptrs_dev: encode 3, reconstruct 4). */
 int shmr_ec_describe_variant(int decode, uint32_t data_shards, uint32_t rows, char* buf, size_t len);
 
 /* Decode-matrix LRU statistics of the (data, parity) codec (crate cache

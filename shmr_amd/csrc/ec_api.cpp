@@ -165,10 +165,12 @@ int shmr_ec_get_tuning(const char* key) {
 
 int shmr_ec_describe_variant(int decode, uint32_t data_shards, uint32_t rows, char* buf, size_t len) {
     if (!buf || len == 0 || rows == 0) return SHMR_EC_INVALID_ARGUMENT;
-    if (decode < 0 || decode > 2) return SHMR_EC_INVALID_ARGUMENT;
-    const core::OpClass op = decode ? core::kDecode : core::kEncode;
-    const auto v = core::resolve_variant(op, data_shards, std::min<uint32_t>(rows, shmr::kern::kMaxRowsPerLaunch),
-                                         false, decode == 2);
+    if (decode < 0 || decode > 4) return SHMR_EC_INVALID_ARGUMENT;
+    const core::OpClass op = (decode == 1 || decode == 2 || decode == 4) ? core::kDecode : core::kEncode;
+    const uint32_t r = std::min<uint32_t>(rows, shmr::kern::kMaxRowsPerLaunch);
+    // 3 / 4: encode / reconstruct over device shard-pointer tables (aligned shards)
+    const auto v = decode >= 3 ? core::launch_variant(op, data_shards, r, false, true, false, false)
+                               : core::resolve_variant(op, data_shards, r, false, decode == 2);
     auto lean = v;   // the full-tile kernel without fused tails must always exist
     lean.fuse_tail = false;
     const bool compiled = shmr::kern::variant_compiled(lean) && (!v.fuse_tail || shmr::kern::variant_compiled(v));

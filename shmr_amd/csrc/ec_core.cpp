@@ -361,12 +361,29 @@ hipError_t sync_stream(hipStream_t stream) {
 
 kern::Variant launch_variant(OpClass op, unsigned k, unsigned rows, bool host_mapped, bool ptrs, bool segs,
                              bool compact) {
-    kern::Variant v = resolve_variant(op, k, rows, host_mapped, compact && !ptrs);
+    // Device-memory shard-pointer tables (shmr_ec_*_ptrs_dev): every rebuilt
+    // shard is a buffer of its own, so reconstructs take the compact form's
+    // store policy (sc1, no residency cap)
+    const bool dev_ptrs = ptrs && !host_mapped;
+    kern::Variant v = resolve_variant(op, k, rows, host_mapped, (compact && !ptrs) || (dev_ptrs && op == kDecode));
     v.ptrs = ptrs;
     v.segs = segs;
     if (ptrs) {
-        v.early = v.spre = v.glds = false;   // only the plain LDS-staged tile reads pointer tables
-        if (g_tune[op].serial.load() == kAuto) v.serial = false;   // the policy's serial goes with early
+        v.spre = v.glds = false;   // the plain and the early-prologue tiles read pointer tables
+        const Tuning& T = g_tune[op];
+        if (host_mapped) {         // the mapped policy: the plain LDS-staged tile
+            v.early = false;
+            if (T.serial.load() == kAuto) v.serial = false;   // the policy's serial goes with early
+        } else if (T.early.load() == kAuto) {
+            // Measured on separate torch allocations per shard (tools/tune.py --ptrs,
+            // profiles/r03/ptrs/): the early prologue, whose first loads take their
+            // addresses from scalar loads of the block's table row, wins for RS(8,3)
+            // encode (+1.8 points) and for reconstructs with sc1 stores (RS(8,3) +3.4,
+            // RS(10,4) +8.2 over the plain tile with nontemporal stores); RS(10,4)
+            // encode loses 1.5 with it
+            v.early = op == kDecode || k <= 8;
+            if (!v.early && T.serial.load() == kAuto) v.serial = false;
+        }
         kern::Variant lean = v;
         lean.fuse_tail = false;
         if (!kern::variant_compiled(lean)) {   // tuned knobs without a pointer-table build: the mapped policy
@@ -691,7 +708,8 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
         // sc1 stores are raw buffer stores: a 2 GiB resource per output row,
         // and 16-byte aligned outputs only (the unaligned-access probe covers
         // the global instructions); otherwise nontemporal global stores
-        if (var.sc1_store && (len >= (uint64_t(1) << 31) - 4096 || ptrs || !out16)) {
+        if (var.sc1_store &&
+            (len >= (uint64_t(1) << 31) - 4096 || L.host_mapped || (ptrs ? !L.ptrs_aligned : !out16))) {
             var.sc1_store = false;
             var.nt_store = true;
         }

@@ -76,6 +76,20 @@ namespace {
     X(1, kNtLoad | kNtStore | kDepth2 | kPtrs) \
     X(2, kNtLoad | kNtStore | kDepth2 | kPtrs | kWaveRun) \
     X(1, kNtLoad | kNtStore | kDepth2 | kPtrs | kPeel) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kFuse | kPtrs) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kPtrs | kWaveRun) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kPtrs) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPtrs) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial | kWaveRun | kPtrs) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial | kWaveRun | kPtrs) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kPtrs | kPeel) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kFuse | kPtrs | kPeel) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kPtrs | kPeel | kWaveRun) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kFuse | kPtrs | kPeel | kWaveRun) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kPtrs | kPeel) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPtrs | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kPtrs | kPeel | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPtrs | kPeel | kWaveRun) \
     X(2, kNtLoad | kNtStore | kDepth2 | kPtrs | kPeel | kWaveRun) \
     X(1, kNtLoad | kSc1Store | kDepth2 | kPeel) \
     X(2, kNtLoad | kSc1Store | kDepth2 | kPeel | kWaveRun) \

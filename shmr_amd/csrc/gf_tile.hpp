@@ -111,6 +111,7 @@ struct Tab {
 // (s_load, lgkmcnt) even though the kernel stores through other pointers --
 // generic loads would be vector loads on the vmcnt queue of the data stream.
 typedef __attribute__((address_space(4))) const uint32_t cu32;
+typedef __attribute__((address_space(4))) const uint64_t cu64;
 template <class T>
 __device__ __forceinline__ const T* as_const(const void* p) {
     return (const T*)(uintptr_t)p;
@@ -566,9 +567,12 @@ struct StageRegs {
 // scalar loads of the prologue).
 typedef __attribute__((address_space(1))) const u32x4 gu32x4;
 typedef __attribute__((address_space(1))) const uint16_t gu16;
+typedef __attribute__((address_space(1))) const uint64_t gu64;
 
-template <int R>
-__device__ __forceinline__ void stage_issue(const ApplyArgs& a, const uint8_t* plan, StageRegs& s) {
+// PTRS (kernels compiled with kPtrs): shard offsets are absolute addresses
+// from block blk's row of the shard-pointer table (in/out bases are 0).
+template <int R, bool PTRS>
+__device__ __forceinline__ void stage_issue(const ApplyArgs& a, const uint8_t* plan, uint64_t blk, StageRegs& s) {
     const uint32_t k = a.k, i = threadIdx.x;
     const uint32_t n16 = k * R * 2;
     const uint32_t ic = i < n16 ? i : n16 - 1;
@@ -576,13 +580,21 @@ __device__ __forceinline__ void stage_issue(const ApplyArgs& a, const uint8_t* p
     const uint32_t t = e / R, r = e - t * R;
     s.tab = ((const gu32x4*)(uintptr_t)(plan + a.tab_off))[(size_t(t) * a.m + a.row0 + r) * 2 + half];
     const gu16* in_idx = (const gu16*)(uintptr_t)(plan + 8);
-    s.in_off = uint64_t(in_idx[i < k ? i : k - 1]) * a.in_spitch;
-    s.out_off = uint64_t(in_idx[k + a.row0 + (i < uint32_t(R) ? i : R - 1)] - a.out_bias) * a.out_spitch;
+    const uint32_t ti = in_idx[i < k ? i : k - 1];
+    const uint32_t to = in_idx[k + a.row0 + (i < uint32_t(R) ? i : R - 1)];
+    if constexpr (PTRS) {
+        const gu64* bp = (const gu64*)(uintptr_t)(a.shard_ptrs + blk * a.total);
+        s.in_off = bp[ti];
+        s.out_off = bp[to];
+    } else {
+        s.in_off = uint64_t(ti) * a.in_spitch;
+        s.out_off = uint64_t(to - a.out_bias) * a.out_spitch;
+    }
 }
 
-template <int R, int TH>
+template <int R, int TH, bool PTRS>
 __device__ __forceinline__ void stage_commit(const ApplyArgs& a, const uint8_t* plan, uint8_t* smem, Ctx& c,
-                                             const StageRegs& s) {
+                                             const StageRegs& s, uint64_t blk) {
     const uint32_t k = a.k, i = threadIdx.x;
     u32x4* s_tab = reinterpret_cast<u32x4*>(smem);
     uint64_t* s_in_off = reinterpret_cast<uint64_t*>(smem + size_t(k) * R * 32);
@@ -599,7 +611,8 @@ __device__ __forceinline__ void stage_commit(const ApplyArgs& a, const uint8_t* 
         const uint32_t t = e / R, r = e - t * R;
         s_tab[j] = ptab[(size_t(t) * a.m + a.row0 + r) * 2 + half];
     }
-    for (uint32_t t = i + TH; t < k; t += TH) s_in_off[t] = uint64_t(in_idx[t]) * a.in_spitch;
+    for (uint32_t t = i + TH; t < k; t += TH)
+        s_in_off[t] = PTRS ? a.shard_ptrs[blk * a.total + in_idx[t]] : uint64_t(in_idx[t]) * a.in_spitch;
     c.s_tab = s_tab;
     c.s_in_off = s_in_off;
     c.s_out_off = s_out_off;
@@ -607,28 +620,36 @@ __device__ __forceinline__ void stage_commit(const ApplyArgs& a, const uint8_t* 
 
 template <int R, int U, int MODE, int F>
 __device__ __forceinline__ void early_tile(const ApplyArgs& a, const uint8_t* plan, uint8_t* smem, bool first,
-                                           const uint8_t* ib, uint8_t* ob, uint64_t col0) {
+                                           const uint8_t* ib, uint8_t* ob, uint64_t col0, uint64_t blk) {
     constexpr int TH = threads_of<F>();
     constexpr int NB = depth_of<F>();
+    // shard-pointer tables (device memory): the first loads' addresses come
+    // from scalar loads of the block's table row, like the plan's in_idx
+    constexpr bool PTRS = (F & kPtrs) != 0;
     const uint32_t k = a.k;
     const uint64_t len = a.len;
     const uint32_t tid = threadIdx.x;
     const uint16_t* in_idx = reinterpret_cast<const uint16_t*>(plan + 8);
     StageRegs sr;
-    stage_issue<R>(a, plan, sr);
+    stage_issue<R, PTRS>(a, plan, blk, sr);
     __builtin_amdgcn_sched_barrier(0);
     u32x4 ring[NB][U];
 #pragma unroll
     for (int i = 0; i < NB - 1; ++i) {
         const uint32_t t = uint32_t(i) < k ? uint32_t(i) : k - 1;
-        const uint8_t* base = ib + uint64_t(plan_u16(in_idx, t)) * a.in_spitch;
+        const uint8_t* base;
+        if constexpr (PTRS)
+            base = reinterpret_cast<const uint8_t*>(
+                uintptr_t(as_const<cu64>(a.shard_ptrs + blk * a.total)[plan_u16(in_idx, t)]));
+        else
+            base = ib + uint64_t(plan_u16(in_idx, t)) * a.in_spitch;
 #pragma unroll
         for (int u = 0; u < U; ++u) ring[i][u] = ld<MODE, F>(base, col0 + slot_chunk<U, TH, F>(u, tid) * 16, len);
     }
     __builtin_amdgcn_sched_barrier(0);
     if (!first) lds_barrier();   // the previous tile's LDS readers are done
     Ctx c{};
-    stage_commit<R, TH>(a, plan, smem, c, sr);
+    stage_commit<R, TH, PTRS>(a, plan, smem, c, sr, blk);
     lds_barrier();
     __builtin_amdgcn_sched_barrier(0);
 
@@ -751,9 +772,9 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
                     spre_tile<R, U, MODE, F, false>(a, plan, ib, ob, col);
                 }
             } else if ((F & kFuse) != 0 && MODE == 0 && tr.tail) {
-                early_tile<R, U, 1, F>(a, plan, smem, first, ib, ob, col);
+                early_tile<R, U, 1, F>(a, plan, smem, first, ib, ob, col, blk);
             } else {
-                early_tile<R, U, MODE, F>(a, plan, smem, first, ib, ob, col);
+                early_tile<R, U, MODE, F>(a, plan, smem, first, ib, ob, col, blk);
             }
             first = false;
         }

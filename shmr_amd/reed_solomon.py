@@ -59,7 +59,8 @@ def get_tuning(key: str) -> int:
 def describe_variant(decode, data_shards: int, rows: int) -> str:
     """The kernel variant a launch of this shape uses (after the auto policy).
     decode: 0/False encode, 1/True reconstruct in place, 2 reconstruct into a
-    compact output (reconstruct_batch_dev_out)."""
+    compact output (reconstruct_batch_dev_out); 3 / 4 encode / reconstruct
+    over device shard-pointer tables (encode_ptrs_dev / reconstruct_ptrs_dev)."""
     buf = ctypes.create_string_buffer(256)
     _check(lib().shmr_ec_describe_variant(int(decode), data_shards, rows, buf, 256))
     return buf.value.decode()

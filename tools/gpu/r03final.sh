@@ -5,6 +5,11 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 cp profiles/pmc_traffic.json gpurun_out/pmc_traffic.json
 bash tools/profile_all.sh r03 2 > gpurun_out/profile_all_r03_part2.log 2>&1 || exit $?
+# the per-dispatch traces are merged already (pmc_traffic.json) and would push gpurun_out past
+# the 64 MiB copy-back limit: keep the summaries only
+find gpurun_out -name '*_kernel_trace.csv' -delete
+find gpurun_out -name 'pmc_counter_collection.csv' -delete
+du -sh gpurun_out
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
   > gpurun_out/pytest_gpu_final.log 2>&1 || exit $?
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_final.log 2>&1 || exit $?

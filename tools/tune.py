@@ -57,6 +57,9 @@ def main():
                          "(block.rs:408-419; off 16-byte alignment when S % 16 != 0)")
     ap.add_argument("--compact", action="store_true",
                     help="decode: rebuild into a compact [B][erasures][pitch] output (reconstruct_batch_dev_out)")
+    ap.add_argument("--ptrs", action="store_true",
+                    help="every shard its own torch allocation, named by a pointer table (shmr_ec_*_ptrs_dev; "
+                         "bench.py --layout ptrs); decodes rebuild into separate buffers")
     a = ap.parse_args()
     if a.config in CFG:
         k, p, block, er, B = CFG[a.config]
@@ -69,7 +72,36 @@ def main():
     rs = shmr_amd.ReedSolomon(k, p)
     g = torch.Generator(device=dev)
     g.manual_seed(1)
-    if er == 0 and a.packed:
+    if a.ptrs:
+        import ctypes
+        t = k + p
+        blocks = [[torch.randint(0, 256, (S,), dtype=torch.uint8, device=dev, generator=g) for _ in range(k)]
+                  + [torch.zeros(S, dtype=torch.uint8, device=dev) for _ in range(p)] for _ in range(B)]
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        if er == 0:
+            keep, _, _, tab = rs._dev_table(blocks, lambda b, i: True)
+            algo = B * (k + p) * S
+
+            def run():
+                assert rs._L.shmr_ec_encode_ptrs_dev(rs._h, tab, B, S, 0, stream) == 0
+        else:
+            rs.encode_ptrs_dev(blocks)
+            present = np.ones((B, t), np.uint8)
+            rows = np.arange(B)
+            if er == 1:
+                present[rows, rows % k] = 0
+            else:
+                for j in range(er):
+                    present[rows, (rows + 3 * j) % min(t, 10)] = 0
+            table = [[blk[i] if present[b, i] else torch.zeros(S, dtype=torch.uint8, device=dev) for i in range(t)]
+                     for b, blk in enumerate(blocks)]
+            keep, _, _, tab = rs._dev_table(table, lambda b, i: True)
+            algo = B * (k + er) * S
+            pp = present.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+
+            def run():
+                assert rs._L.shmr_ec_reconstruct_ptrs_dev(rs._h, tab, pp, B, S, 0, 0, stream) == 0
+    elif er == 0 and a.packed:
         t = k + p
         flat = torch.randint(0, 256, (B * t * S,), dtype=torch.uint8, device=dev, generator=g)
         data = flat.as_strided((B, k, S), (t * S, S, 1))
