@@ -337,7 +337,9 @@ enum {
     SHMR_EC_DEV_BLOCKING_CALLS = 6,       /* blocking HIP calls the library made on its own: device
                                              init, plan-arena growth, upload-ring creation and waits
                                              for a ring slot (not the host-buffer calls' final sync) */
-    SHMR_EC_DEV_COUNTERS = 7
+    SHMR_EC_DEV_PTR_TABLE_HITS = 7,       /* *_ptrs_dev tables reused from the device's table cache
+                                             (no upload) */
+    SHMR_EC_DEV_COUNTERS = 8
 };
 int shmr_ec_device_stats(int device, uint64_t* out, size_t n);
 

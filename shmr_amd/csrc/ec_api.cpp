@@ -502,9 +502,10 @@ int shmr_ec_reconstruct_batch_dev_out(shmr_ec_t* rs, const uint8_t* d_shards, si
 // ---- device-resident shards anywhere: shard-pointer tables --------------------------
 // The crate's own shape (block.rs:408-427: every shard its own Vec<u8>; :556-565:
 // every None shard rebuilt into a fresh buffer) on device memory.  The host
-// table d_shards[b * total + i] is copied into a pinned slot of the device's
-// pointer ring and uploaded on the caller's stream (inside a capture: into
-// permanent arena memory, which every replay re-reads).
+// table d_shards[b * total + i] goes up on the caller's stream into the
+// device's pointer-table cache (a table the stream passed before is reused
+// without an upload; a busy cache falls back to the pointer ring); inside a
+// capture it goes to permanent arena memory, which every replay re-reads.
 static int ptrs_dev(shmr_ec_t* rs, uint8_t* const* d_shards, const uint8_t* present, size_t nblocks,
                     size_t shard_len, int data_only, int device, void* stream_, core::OpClass op) {
     return guarded([&]() -> int {
@@ -556,11 +557,25 @@ static int ptrs_dev(shmr_ec_t* rs, uint8_t* const* d_shards, const uint8_t* pres
             }
             return run(d, 0, nblocks);
         }
-        core::UploadRing* ring = core::UploadRing::for_device(device, &rc, core::UploadRing::kPointers);
-        if (!ring) return rc;
+        core::PtrTableCache* cache = core::PtrTableCache::for_device(device, &rc);
+        if (!cache) return rc;
+        core::UploadRing* ring = nullptr;
         const size_t per_chunk = core::UploadRing::kSlotBytes / (sizeof(uint64_t) * t);
         for (size_t b0 = 0; b0 < nblocks; b0 += per_chunk) {
             const size_t n = std::min(per_chunk, nblocks - b0);
+            // a table this stream passed before (same bytes): its device copy, no upload
+            const uint8_t* dtab = nullptr;
+            int entry = -1;
+            rc = cache->lookup(d_shards + b0 * t, n * t * sizeof(uint64_t), stream, &dtab, &entry);
+            if (rc) return rc;
+            if (dtab) {
+                rc = run(dtab, b0, n);
+                const int rc2 = cache->release_after(entry, stream);
+                if (rc) return rc;
+                if (rc2) return rc2;
+                continue;
+            }
+            if (!ring && !(ring = core::UploadRing::for_device(device, &rc, core::UploadRing::kPointers))) return rc;
             uint8_t *hslot = nullptr, *dslot = nullptr;
             int slot = -1;
             rc = ring->acquire(&hslot, &dslot, &slot);

@@ -1075,6 +1075,124 @@ void UploadRing::release_now(int slot) {
 }
 
 // ===========================================================================
+// Shard-pointer table cache
+// ===========================================================================
+PtrTableCache* PtrTableCache::for_device(int dev, int* rc) {
+    static std::mutex mu;
+    static auto* caches = new std::map<int, PtrTableCache*>;   // leaked: in-flight kernels read the entries
+    std::lock_guard<std::mutex> lock(mu);
+    auto& c = (*caches)[dev];
+    if (!c) {
+        c = new PtrTableCache;
+        c->dev_id_ = dev;
+    }
+    *rc = SHMR_EC_OK;
+    return c;
+}
+
+namespace {
+uint64_t fnv1a64(const void* p, size_t bytes) {
+    const uint8_t* b = static_cast<const uint8_t*>(p);
+    uint64_t h = 1469598103934665603ull;
+    size_t i = 0;
+    for (; i + 8 <= bytes; i += 8) {
+        uint64_t w;
+        std::memcpy(&w, b + i, 8);
+        h = (h ^ w) * 1099511628211ull;
+    }
+    for (; i < bytes; ++i) h = (h ^ b[i]) * 1099511628211ull;
+    return h;
+}
+
+bool event_done(hipEvent_t e) {
+    const hipError_t q = hipEventQuery(e);
+    if (q == hipSuccess) return true;
+    (void)hipGetLastError();
+    return false;
+}
+}  // namespace
+
+int PtrTableCache::lookup(const void* tab, size_t bytes, hipStream_t stream, const uint8_t** d_tab, int* entry) {
+    *d_tab = nullptr;
+    *entry = -1;
+    if (bytes > UploadRing::kSlotBytes) return SHMR_EC_OK;
+    const uint64_t h = fnv1a64(tab, bytes);
+    std::lock_guard<std::mutex> lock(mu_);
+    for (int i = 0; i < kEntries; ++i) {
+        Entry& e = e_[i];
+        if (e.valid && e.stream == stream && e.bytes == bytes && e.hash == h && std::memcmp(e.host, tab, bytes) == 0) {
+            // (a stream handle reused after its stream was destroyed: wait on the device)
+            if (!event_done(e.up) && hipStreamWaitEvent(stream, e.up, 0) != hipSuccess) {
+                (void)hipGetLastError();
+                return SHMR_EC_DEVICE_ERROR;
+            }
+            ++e.busy;
+            e.tick = ++tick_;
+            count_device(dev_id_, kDevPtrTableHits);
+            *d_tab = e.dev;
+            *entry = i;
+            return SHMR_EC_OK;
+        }
+    }
+    // miss: a never-used entry, else the least recently used free one whose
+    // pinned copy the last upload has left and whose readers on another
+    // stream are done
+    int victim = -1;
+    for (int i = 0; i < kEntries && victim < 0; ++i)
+        if (!e_[i].host) victim = i;
+    if (victim < 0) {
+        for (int i = 0; i < kEntries; ++i) {
+            Entry& e = e_[i];
+            if (e.busy || !event_done(e.up)) continue;
+            if (e.stream != stream && e.used_armed && !event_done(e.used)) continue;
+            if (victim < 0 || e.tick < e_[victim].tick) victim = i;
+        }
+    }
+    if (victim < 0) return SHMR_EC_OK;   // every entry busy: the caller uses the upload ring
+    Entry& e = e_[victim];
+    if (!e.host) {
+        int rc = arena_alloc(dev_id_, UploadRing::kSlotBytes, false, &e.host, &e.dev);
+        if (rc) return rc;
+        if (hipEventCreateWithFlags(&e.up, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e.used, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            e.host = nullptr;   // the arena block is abandoned (permanent memory)
+            return SHMR_EC_DEVICE_ERROR;
+        }
+    }
+    e.valid = false;
+    std::memcpy(e.host, tab, bytes);
+    if (hipMemcpyAsync(e.dev, e.host, bytes, hipMemcpyHostToDevice, stream) != hipSuccess ||
+        hipEventRecord(e.up, stream) != hipSuccess) {
+        (void)hipGetLastError();
+        return SHMR_EC_DEVICE_ERROR;
+    }
+    e.bytes = bytes;
+    e.hash = h;
+    e.stream = stream;
+    e.valid = true;
+    e.used_armed = false;
+    ++e.busy;
+    e.tick = ++tick_;
+    *d_tab = e.dev;
+    *entry = victim;
+    return SHMR_EC_OK;
+}
+
+int PtrTableCache::release_after(int entry, hipStream_t stream) {
+    std::lock_guard<std::mutex> lock(mu_);
+    Entry& e = e_[entry];
+    --e.busy;
+    if (hipEventRecord(e.used, stream) != hipSuccess) {
+        (void)hipGetLastError();
+        e.valid = false;
+        return SHMR_EC_DEVICE_ERROR;
+    }
+    e.used_armed = true;
+    return SHMR_EC_OK;
+}
+
+// ===========================================================================
 // Staging pool
 // ===========================================================================
 StagingPool& StagingPool::get() {

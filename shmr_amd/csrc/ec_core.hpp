@@ -83,6 +83,7 @@ enum DevCounter {
     kDevUploadRings,
     kDevStagingStreams,
     kDevBlockingCalls,
+    kDevPtrTableHits,
     kDevCounters
 };
 void count_device(int dev, DevCounter c, uint64_t n = 1);
@@ -219,6 +220,41 @@ private:
     int next_ = 0;
     std::mutex mu_;
     std::condition_variable cv_;
+};
+
+// ---- per-device cache of shard-pointer tables (the *_ptrs_dev calls) -------
+// A table passed again with the same bytes on the same stream (a device Block
+// Cache whose shard buffers stay put) is not uploaded again: the launch reads
+// the device copy made by the earlier call, which the stream's order already
+// places before it.  Entries live in permanent arena memory; an entry takes
+// another table only once its upload has left the pinned copy and, for another
+// stream, once its last reader has finished (no host wait: a busy cache sends
+// the call through the upload ring instead).
+class PtrTableCache {
+public:
+    static constexpr int kEntries = 8;
+    static PtrTableCache* for_device(int dev, int* rc);
+    // *d_tab: the device copy of tab[0, bytes), ordered before work enqueued
+    // next on `stream`; nullptr when no entry is free (nothing enqueued).
+    int lookup(const void* tab, size_t bytes, hipStream_t stream, const uint8_t** d_tab, int* entry);
+    // After the launches that read `entry` are enqueued on `stream`.
+    int release_after(int entry, hipStream_t stream);
+
+private:
+    struct Entry {
+        uint8_t* host = nullptr;   // pinned copy (the upload's source)
+        uint8_t* dev = nullptr;
+        size_t bytes = 0;
+        uint64_t hash = 0, tick = 0;
+        hipStream_t stream = nullptr;
+        hipEvent_t up = nullptr, used = nullptr;
+        bool valid = false, used_armed = false;
+        int busy = 0;
+    };
+    int dev_id_ = 0;
+    Entry e_[kEntries];
+    uint64_t tick_ = 0;
+    std::mutex mu_;
 };
 
 // ---- device staging for the single-call host-buffer entry points ---------

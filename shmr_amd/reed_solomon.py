@@ -534,7 +534,7 @@ def path_stats():
 
 
 DEVICE_COUNTERS = ("blocks_encoded", "blocks_reconstructed", "launches", "plan_images", "upload_rings",
-                   "staging_streams", "blocking_calls")
+                   "staging_streams", "blocking_calls", "ptr_table_hits")
 
 
 def device_init(device: int = 0) -> None:

@@ -256,3 +256,61 @@ def test_ptrs_validation(gpu):
     assert np.array_equal(out1.cpu().numpy(), host[0, 1])
     assert rs._L.shmr_ec_reconstruct_ptrs_dev(rs._h, tab, pres.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), 1,
                                               64, 0, 0, None) == -100      # the same without data_only
+
+
+def test_ptrs_table_cache(gpu):
+    """A table passed again on the same stream is reused from the device's
+    table cache (no upload; counter ptr_table_hits), and stays exact when the
+    shards' bytes change between calls; a changed table, or the same table on
+    another stream, is uploaded again; more distinct tables than cache entries
+    cycle through it (and through the ring when busy) without a mismatch."""
+    import torch
+    k, p, S, B = 8, 3, 4096 * 3 + 100, 5
+    t = k + p
+    rs = shmr_amd.ReedSolomon(k, p)
+    shmr_amd.device_init(0)
+    g = torch.Generator(device=gpu).manual_seed(3)
+    sets = [[[torch.empty(S, dtype=torch.uint8, device=gpu) for _ in range(t)] for _ in range(B)] for _ in range(11)]
+
+    def check(blocks):
+        data = np.stack([np.stack([s.cpu().numpy() for s in blk[:k]]) for blk in blocks])
+        want = _parity(k, p, data)
+        for b in range(B):
+            for r in range(p):
+                assert np.array_equal(blocks[b][k + r].cpu().numpy(), want[b, r]), (b, r)
+
+    def fill(blocks):
+        for blk in blocks:
+            for s in blk[:k]:
+                s.copy_(torch.randint(0, 256, (S,), dtype=torch.uint8, device=gpu, generator=g))
+
+    hits = lambda: shmr_amd.device_stats(0)["ptr_table_hits"]  # noqa: E731
+    fill(sets[0])
+    rs.encode_ptrs_dev(sets[0])
+    torch.cuda.synchronize()
+    check(sets[0])
+    h0 = hits()
+    fill(sets[0])                       # same table, new bytes
+    rs.encode_ptrs_dev(sets[0])
+    torch.cuda.synchronize()
+    assert hits() == h0 + 1
+    check(sets[0])
+    fill(sets[1])                       # another table: uploaded
+    rs.encode_ptrs_dev(sets[1])
+    torch.cuda.synchronize()
+    assert hits() == h0 + 1
+    check(sets[1])
+    side = torch.cuda.Stream()
+    fill(sets[0])
+    with torch.cuda.stream(side):      # same table, other stream: its own upload
+        rs.encode_ptrs_dev(sets[0])
+    torch.cuda.synchronize()
+    assert hits() == h0 + 1
+    check(sets[0])
+    for rep in range(3):                # 11 tables > 8 entries, back to back without a sync
+        for s in sets:
+            fill(s)
+            rs.encode_ptrs_dev(s)
+        torch.cuda.synchronize()
+        for s in sets:
+            check(s)
