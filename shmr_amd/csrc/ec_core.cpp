@@ -49,6 +49,9 @@ std::atomic<int> g_mirror_zc{1};
 std::atomic<int> g_ptrs_direct{kPtrsDirectDefault};
 std::atomic<int> g_sync_spin{kSyncSpinDefault};
 std::atomic<int> g_alias_devices{0};   // tools build: alias device IDs (see ec_core.hpp)
+// Reconstructs over device shard-pointer tables take segment launches (plans in
+// the kernel arguments) when they fit; 0 = always the uploaded block/plan table
+std::atomic<int> g_ptrs_segs{1};
 // Misaligned device-resident shards: kAuto = the vector kernels (modes 0 / 1)
 // where the device passed probe_unaligned_vector, else the realigning kernel
 // (mode 3); 0 = always mode 3, 1 = always modes 0 / 1 (tools build only).
@@ -164,6 +167,10 @@ int set_tuning(const char* key, int value) {
         g_mirror_zc = value == kAuto ? 1 : (value != 0);
         return SHMR_EC_OK;
     }
+    if (k == "ptrs_segs") {
+        g_ptrs_segs = value == kAuto ? 1 : (value != 0);
+        return SHMR_EC_OK;
+    }
     if (k == "ptrs_direct") {
         if (value < 0 && value != kAuto) return SHMR_EC_INVALID_ARGUMENT;
         g_ptrs_direct = value == kAuto ? kPtrsDirectDefault : value;
@@ -274,6 +281,7 @@ int get_tuning(const char* key) {
     const Tuning& T = g_tune[first];
     if (k == "bounce_kib") return g_bounce_kib;
     if (k == "mirror_zc") return g_mirror_zc;
+    if (k == "ptrs_segs") return g_ptrs_segs;
     if (k == "ptrs_direct") return g_ptrs_direct;
     if (k == "sync_spin_us") return g_sync_spin;
     if (k == "alias_devices") return g_alias_devices;
@@ -875,10 +883,8 @@ int reconstruct_on_device(Codec& c, int dev, const Layout& L, const uint8_t* pre
         // no dependent table loads in the kernel prologue.
         {
             std::vector<kern::Seg> segs;
-            // (device shard-pointer tables restage every tile anyway, and their
-            // segment form is compiled only for the mapped-host policy: they take
-            // the table launch with the device policy's loads)
-            bool fits = !(L.d_ptrs && !L.host_mapped) &&
+            // (device shard-pointer tables: knob "ptrs_segs")
+            bool fits = (!(L.d_ptrs && !L.host_mapped) || g_ptrs_segs.load() != 0) &&
                         segs_supported(kDecode, c.k(), L.host_mapped, L.d_ptrs != nullptr, L.compact);
             for (size_t i = 0; i < grp.blocks.size() && fits;) {
                 size_t e = i + 1;

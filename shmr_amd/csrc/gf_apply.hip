@@ -90,6 +90,14 @@ namespace {
     X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPtrs | kPeel) \
     X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kPtrs | kPeel | kWaveRun) \
     X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPtrs | kPeel | kWaveRun) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kPtrs | kPeel) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kFuse | kPtrs | kPeel) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kPtrs | kPeel | kWaveRun) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kFuse | kPtrs | kPeel | kWaveRun) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kPtrs | kPeel) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kFuse | kPtrs | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kPtrs | kPeel | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kFuse | kPtrs | kPeel | kWaveRun) \
     X(2, kNtLoad | kNtStore | kDepth2 | kPtrs | kPeel | kWaveRun) \
     X(1, kNtLoad | kSc1Store | kDepth2 | kPeel) \
     X(2, kNtLoad | kSc1Store | kDepth2 | kPeel | kWaveRun) \

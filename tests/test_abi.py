@@ -235,7 +235,7 @@ def test_tuning_api():
     finally:
         shmr_amd.set_tuning(bounce_kib=saved)
     # host-path knobs: set, read back, reset to the measured defaults
-    for knob, value, default in (("ptrs_direct", 0, 16), ("sync_spin_us", 50, 0), ("mirror_zc", 0, 1)):
+    for knob, value, default in (("ptrs_direct", 0, 16), ("sync_spin_us", 50, 0), ("mirror_zc", 0, 1), ("ptrs_segs", 0, 1)):
         shmr_amd.set_tuning(**{knob: value})
         assert shmr_amd.get_tuning(knob) == value
         shmr_amd.set_tuning(**{knob: -2})

@@ -152,7 +152,7 @@ def main():
             else:
                 rs.reconstruct_batch_dev(shards, present, shard_len=S)
     base = {"chunks": 1, "nt_load": 0, "nt_store": 0, "occ8": 0, "grid": -1, "diag": 0, "depth": 3, "wgs_per_cu": 0, "occ": 0, "early": 0, "spre": 0,
-            "threads": 256, "fuse_tail": 0, "glds": 0, "serial": 0, "uvec": -2, "sc1_store": 0, "realign": 0, "peel": 0, "wave_run": 0, "st_align": 0, "xcd": 0}
+            "threads": 256, "fuse_tail": 0, "glds": 0, "serial": 0, "uvec": -2, "sc1_store": 0, "realign": 0, "peel": 0, "wave_run": 0, "st_align": 0, "xcd": 0, "ptrs_segs": 1}
     variants = []
     for spec in a.variants.split(";"):
         kn = dict(base)
