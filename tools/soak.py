@@ -2,8 +2,9 @@
 """Randomised multi-threaded soak of the C ABI on one GPU, every result checked
 against the CPU oracle: per-block encode / reconstruct on pageable and mapped
 buffers (zero-copy, bounce, staged DMA), host batches on pageable arrays
-(pinned mirror) and mapped slabs, and device-resident batches on per-thread
-torch streams -- several (k, p) codecs and shard lengths (aligned, tail,
+(pinned mirror) and mapped slabs, device-resident batches on per-thread
+torch streams, and per-shard device buffers through pointer tables (reused, so
+the device's table cache hits) -- several (k, p) codecs and shard lengths (aligned, tail,
 byte-granular) at once.  Not part of the test suite (minutes of GPU time).
 
     python tools/soak.py [--seconds 120] [--threads 12]
@@ -40,10 +41,11 @@ def worker(tid, deadline, errors, counts):
     rng = np.random.default_rng([tid, 2024])
     stream = torch.cuda.Stream()
     slab = shmr_amd.PinnedBuffer(4 * 24 * 524288)
+    kept = {}   # (shape, set) -> per-shard device buffers reused across calls (pointer-table cache hits)
     while time.time() < deadline and not errors:
         k, p, L = SHAPES[int(rng.integers(0, len(SHAPES)))]
         rs = shmr_amd.ReedSolomon(k, p)
-        op = int(rng.integers(0, 4))
+        op = int(rng.integers(0, 5))
         try:
             if op == 0:        # per-block calls, pageable or mapped
                 mapped = bool(rng.integers(0, 2))
@@ -91,6 +93,34 @@ def worker(tid, deadline, errors, counts):
                     want = oracle_encode(k, p, list(blk[b, :k]))
                     if not all(np.array_equal(blk[b, i], want[i]) for i in range(k, k + p)):
                         errors.append((tid, "mapped batch encode", k, p, L, B))
+            elif op == 4:      # per-shard device buffers (pointer tables), on this thread's stream or the default one
+                key = (k, p, L, int(rng.integers(0, 3)))
+                if key not in kept:
+                    B = int(rng.integers(1, 6))
+                    kept[key] = [[torch.empty(L, dtype=torch.uint8, device="cuda") for _ in range(k + p)]
+                                 for _ in range(B)]
+                blocks = kept[key]
+                B = len(blocks)
+                host = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+                st = stream if rng.integers(0, 4) else torch.cuda.current_stream()
+                with torch.cuda.stream(st):
+                    for b in range(B):
+                        for i in range(k):
+                            blocks[b][i].copy_(torch.from_numpy(host[b, i]).cuda(), non_blocking=False)
+                    rs.encode_ptrs_dev(blocks)
+                    lost = [sorted(rng.choice(k + p, size=int(rng.integers(1, p + 1)), replace=False).tolist())
+                            for _ in range(B)]
+                    partial = [[None if i in lost[b] else blocks[b][i] for i in range(k + p)] for b in range(B)]
+                    rs.reconstruct_ptrs_dev(partial)
+                st.synchronize()
+                for b in range(B):
+                    want = oracle_encode(k, p, list(host[b]))
+                    if not all(np.array_equal(blocks[b][i].cpu().numpy(), want[i]) for i in range(k, k + p)):
+                        errors.append((tid, "ptrs encode", k, p, L, B))
+                        break
+                    if not all(np.array_equal(partial[b][i].cpu().numpy(), want[i]) for i in lost[b]):
+                        errors.append((tid, "ptrs reconstruct", k, p, L, B))
+                        break
             else:              # device-resident batch on this thread's stream: encode, in-place and compact rebuild
                 B = int(rng.integers(1, 9))
                 P = (L + 255) // 256 * 256
@@ -150,7 +180,8 @@ def main():
             last = time.time()
     zc, st = shmr_amd.path_stats()
     print(json.dumps({"ops": sum(counts), "threads": a.threads, "seconds": a.seconds, "errors": errors[:5],
-                      "zero_copy_blocks": zc, "staged_blocks": st}), flush=True)
+                      "zero_copy_blocks": zc, "staged_blocks": st,
+                      "ptr_table_hits": shmr_amd.device_stats(0)["ptr_table_hits"]}), flush=True)
     sys.exit(1 if errors else 0)
 
 
