@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=9)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--pitch-align", type=int, default=256, help="shard pitch alignment (bench.py uses 4096)")
+    ap.add_argument("--ptrs", action="store_true",
+                    help="every shard its own torch allocation, through the *_ptrs_dev calls (bench.py --layout ptrs)")
     a = ap.parse_args()
     k, p, block, er, B = CFG[a.config]
     libs = {"current": load(_native.LIB_PATH)}
@@ -57,7 +59,32 @@ def main():
     g = torch.Generator(device=dev)
     g.manual_seed(7)
     runs = {}
-    if er == 0:
+    if a.ptrs:
+        t = k + p
+        blocks = [[torch.randint(0, 256, (S,), dtype=torch.uint8, device=dev, generator=g) for _ in range(k)]
+                  + [torch.zeros(S, dtype=torch.uint8, device=dev) for _ in range(p)] for _ in range(B)]
+        present = np.ones((B, t), np.uint8)
+        rows = np.arange(B)
+        if er == 1:
+            present[rows, rows % k] = 0
+        elif er:
+            present[rows, rows % 10] = 0
+            present[rows, (rows + 3) % 10] = 0
+        outs = [[torch.zeros(S, dtype=torch.uint8, device=dev) for _ in range(t)] for _ in range(B)]
+        table = [blocks[b][i] if present[b, i] else outs[b][i] for b in range(B) for i in range(t)]
+        tab = (_native._u8p * (B * t))(*[ctypes.cast(x.data_ptr(), _native._u8p) for x in table])
+        pr = present.ctypes.data_as(_native._u8p)
+        algo = B * (k + (er or p)) * S
+        for n, L in libs.items():
+            h = ctypes.c_void_p()
+            assert L.shmr_ec_new(k, p, ctypes.byref(h)) == 0
+
+            def run(L=L, h=h):
+                rc = (L.shmr_ec_encode_ptrs_dev(h, tab, B, S, 0, sp) if er == 0 else
+                      L.shmr_ec_reconstruct_ptrs_dev(h, tab, pr, B, S, 0, 0, sp))
+                assert rc == 0, rc
+            runs[n] = run
+    elif er == 0:
         data = torch.randint(0, 256, (B, k, pitch), dtype=torch.uint8, device=dev, generator=g)
         par = {n: torch.empty((B, p, pitch), dtype=torch.uint8, device=dev) for n in libs}
         algo = B * (k + p) * S
@@ -106,7 +133,7 @@ def main():
             e1.record(st)
             torch.cuda.synchronize()
             times[n].append(e0.elapsed_time(e1) / a.iters)
-    if er == 0:
+    if er == 0 and not a.ptrs:
         for n in par:
             assert torch.equal(par["current"], par[n]), f"outputs differ: {n}"
     for n, ts in times.items():
