@@ -167,6 +167,47 @@ def test_reconstruct_validation_precedes_device_use():
     assert e.value.name == "EmptyShard"
 
 
+def test_ptrs_dev_validation_precedes_device_use():
+    """The pointer-table entry points check their arguments before any device
+    work (no GPU needed): NULL table / presence flags, empty shards, NULL shards
+    a call would touch, too few present shards; a well-formed call without a
+    GPU reports NoDevice (no CPU fallback).  Fake device addresses are never
+    dereferenced on the host."""
+    import ctypes
+    L = _native.lib()
+    rs = shmr_amd.ReedSolomon(4, 2)
+    h = rs._h
+    u8p = _native._u8p
+    fake = [ctypes.cast(ctypes.c_void_p(0x100000 + 0x1000 * i), u8p) for i in range(6)]
+    tab = (u8p * 6)(*fake)
+    pr = np.array([1, 1, 1, 1, 1, 0], np.uint8)
+    prp = pr.ctypes.data_as(u8p)
+    assert L.shmr_ec_encode_ptrs_dev(None, tab, 1, 64, 0, None) == -100
+    assert L.shmr_ec_encode_ptrs_dev(h, None, 1, 64, 0, None) == -100
+    assert L.shmr_ec_encode_ptrs_dev(h, tab, 0, 64, 0, None) == 0           # nothing to do
+    assert L.shmr_ec_encode_ptrs_dev(h, tab, 1, 0, 0, None) == -11          # EmptyShard
+    nulls = (u8p * 6)(*(fake[:5] + [u8p()]))
+    assert L.shmr_ec_encode_ptrs_dev(h, nulls, 1, 64, 0, None) == -100
+    assert L.shmr_ec_reconstruct_ptrs_dev(h, tab, None, 1, 64, 0, 0, None) == -100
+    few = np.array([1, 1, 1, 0, 0, 0], np.uint8)
+    assert L.shmr_ec_reconstruct_ptrs_dev(h, tab, few.ctypes.data_as(u8p), 1, 64, 0, 0, None) == -10
+    # data_only: the absent parity shard may be NULL
+    ok = L.shmr_ec_reconstruct_ptrs_dev(h, nulls, prp, 1, 64, 1, 0, None)
+    assert ok in (0, -101)                  # all data present: nothing to rebuild, no device needed
+    assert L.shmr_ec_reconstruct_ptrs_dev(h, nulls, prp, 1, 64, 0, 0, None) == -100
+    import torch
+    if not torch.cuda.is_available():
+        assert L.shmr_ec_encode_ptrs_dev(h, tab, 1, 64, 0, None) == -101   # NoDevice
+    with pytest.raises(shmr_amd.Error) as e:
+        rs.encode_ptrs_dev([[None] * 5])
+    assert e.value.name == "TooFewShards"
+    with pytest.raises(shmr_amd.Error) as e:
+        rs.reconstruct_ptrs_dev([[None] * 7])
+    assert e.value.name == "TooManyShards"
+    with pytest.raises(TypeError):
+        rs.encode_ptrs_dev([[torch.zeros(64, dtype=torch.uint8) for _ in range(6)]])   # host tensors
+
+
 def test_compute_without_gpu_fails_loudly():
     """No CPU fallback: on a machine without a GPU the compute entry points
     report NoDevice instead of computing anything."""
