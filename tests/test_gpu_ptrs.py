@@ -314,3 +314,45 @@ def test_ptrs_table_cache(gpu):
         torch.cuda.synchronize()
         for s in sets:
             check(s)
+
+
+def test_ptrs_many_shards_and_chunks(gpu):
+    """RS(200,55) (255 shards, the crate's maximum total) over 130 blocks: the
+    pointer table spans two upload chunks (128 blocks per 256 KiB slot); encode,
+    then a reconstruct with random erasures (up to 55 per block, mixed patterns),
+    run twice so the second pass reads both chunks from the table cache."""
+    import ctypes
+    import torch
+    from shmr_amd.reed_solomon import _u8p
+    k, p, S, B = 200, 55, 48, 130
+    t = k + p
+    slot = 64
+    rng = np.random.default_rng(255)
+    arena = torch.zeros(B * t * slot + 64, dtype=torch.uint8, device=gpu)
+    base = arena.data_ptr()
+    addr = np.array([base + (b * t + i) * slot for b in range(B) for i in range(t)], dtype=np.uint64)
+    tab = addr.ctypes.data_as(ctypes.POINTER(_u8p))
+    rs = shmr_amd.ReedSolomon(k, p)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(0).cuda_stream)
+    view = arena[:B * t * slot].view(B, t, slot)
+    for rep in range(2):
+        data = rng.integers(0, 256, (B, k, S), dtype=np.uint8)
+        view[:, :k, :S] = torch.from_numpy(data).to(gpu)
+        hits0 = shmr_amd.device_stats(0)["ptr_table_hits"]
+        assert rs._L.shmr_ec_encode_ptrs_dev(rs._h, tab, B, S, 0, stream) == 0
+        torch.cuda.synchronize()
+        if rep:
+            assert shmr_amd.device_stats(0)["ptr_table_hits"] == hits0 + 2
+        got = view[:, :, :S].cpu().numpy()
+        want = _parity(k, p, data)
+        assert np.array_equal(got[:, k:], want)
+        present = np.ones((B, t), np.uint8)
+        for b in range(B):
+            present[b, rng.choice(t, size=int(rng.integers(1, p + 1)), replace=False)] = 0
+        erased = torch.from_numpy(present == 0).to(gpu)
+        view[erased] = 0xEE
+        rc = rs._L.shmr_ec_reconstruct_ptrs_dev(rs._h, tab, present.ctypes.data_as(_u8p), B, S, 0, 0, stream)
+        assert rc == 0
+        torch.cuda.synchronize()
+        assert np.array_equal(view[:, :, :S].cpu().numpy(), got)
+        assert (view[:, :, S:].cpu().numpy() == 0).all(), "bytes past the shards written"
