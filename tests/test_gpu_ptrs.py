@@ -350,7 +350,8 @@ def test_ptrs_many_shards_and_chunks(gpu):
         for b in range(B):
             present[b, rng.choice(t, size=int(rng.integers(1, p + 1)), replace=False)] = 0
         erased = torch.from_numpy(present == 0).to(gpu)
-        view[erased] = 0xEE
+        shard_bytes = view[:, :, :S]
+        shard_bytes[erased] = 0xEE            # absent shards' bytes (the slot tails stay 0)
         rc = rs._L.shmr_ec_reconstruct_ptrs_dev(rs._h, tab, present.ctypes.data_as(_u8p), B, S, 0, 0, stream)
         assert rc == 0
         torch.cuda.synchronize()
