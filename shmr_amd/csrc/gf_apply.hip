@@ -100,6 +100,14 @@ namespace {
     X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kFuse | kPtrs | kPeel | kWaveRun) \
     X(2, kNtLoad | kNtStore | kDepth2 | kPtrs | kPeel | kWaveRun) \
     X(1, kNtLoad | kSc1Store | kDepth2 | kPeel) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kPeel) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kFuse | kPeel) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kPeel) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kFuse | kPeel) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kPeel) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPeel) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kPeel) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kFuse | kPeel) \
     X(2, kNtLoad | kSc1Store | kDepth2 | kPeel | kWaveRun) \
     X(1, kNtLoad | kSc1Store | kDepth2 | kFuse | kPeel) \
     X(2, kNtLoad | kSc1Store | kDepth2 | kFuse | kPeel | kWaveRun) \

@@ -446,8 +446,6 @@ __device__ __forceinline__ void store_run_aligned(uint8_t* p, const u32x4 (&v)[U
     X(2, kDepth2 | kEarly | kSerial | kFuse) \
     X(1, kNtStore | kDepth2 | kSegs | kFuse) \
     X(1, kDepth2 | kSegs | kFuse) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kPeel) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPeel) \
     X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial | kPeel) \
     X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial | kPeel) \
     X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kSerial | kWaveRun) \
