@@ -716,7 +716,10 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
         }
         // Misaligned output rows (knob "st_align", tools build): aligned
         // stores realigned across lanes in the full tiles
-        if (!out16 && !ptrs && g_tune[op].st_align.load() == 1 && !var.realign) var.st_align = true;
+        if (!out16 && !ptrs && g_tune[op].st_align.load() == 1 && !var.realign) {
+            var.st_align = true;
+            if (op == kDecode) var.early = false;   // measured (and compiled) on the plain rebuild tile
+        }
         // sc1 stores are raw buffer stores: a 2 GiB resource per output row,
         // and 16-byte aligned outputs only (the unaligned-access probe covers
         // the global instructions); otherwise nontemporal global stores
