@@ -1164,14 +1164,16 @@ int PtrTableCache::lookup(const void* tab, size_t bytes, hipStream_t stream, con
     if (victim < 0) return SHMR_EC_OK;   // every entry busy: the caller uses the upload ring
     Entry& e = e_[victim];
     if (!e.host) {
-        int rc = arena_alloc(dev_id_, UploadRing::kSlotBytes, false, &e.host, &e.dev);
-        if (rc) return rc;
+        // (no arena memory or events for a new entry: the caller takes the upload ring)
+        uint8_t *h = nullptr, *d = nullptr;
+        if (arena_alloc(dev_id_, UploadRing::kSlotBytes, false, &h, &d) != SHMR_EC_OK) return SHMR_EC_OK;
         if (hipEventCreateWithFlags(&e.up, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&e.used, hipEventDisableTiming) != hipSuccess) {
             (void)hipGetLastError();
-            e.host = nullptr;   // the arena block is abandoned (permanent memory)
-            return SHMR_EC_DEVICE_ERROR;
+            return SHMR_EC_OK;   // the arena block is abandoned (permanent memory)
         }
+        e.host = h;
+        e.dev = d;
     }
     e.valid = false;
     std::memcpy(e.host, tab, bytes);
