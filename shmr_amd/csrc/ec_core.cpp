@@ -131,10 +131,11 @@ kern::Variant variant_policy(OpClass op, unsigned k, unsigned rows, bool host_ma
         v.sc1_store = true;
         v.nt_store = false;
         v.wgs_per_cu = 0;
-        // with sc1 stores the early prologue pays for 2- and 3-row rebuilds:
-        // RS(10,4) 2 erasures +0.7 / +0.7 / +1.1, RS(8,3) 3 erasures +0.5 / +0.5;
+        // with sc1 stores the early prologue pays for rebuilds of 2+ rows:
+        // RS(10,4) 2 erasures +0.7 / +0.7 / +1.1 (-0.8 on a third box), RS(8,3)
+        // 3 erasures +0.5 / +0.5, RS(10,4) 4 erasures (U = 2) +1.3 / +1.8;
         // RS(8,3) 1 erasure -0.9 (profiles/r03/early_dec/)
-        v.early = rows >= 2 && rows <= 3;
+        v.early = rows >= 2;
     }
     return v;
 }

@@ -108,6 +108,14 @@ namespace {
     X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPeel) \
     X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kPeel) \
     X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kFuse | kPeel) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kPeel | kWaveRun) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kFuse | kPeel | kWaveRun) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kPeel | kWaveRun) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kFuse | kPeel | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kPeel | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPeel | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kPeel | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kFuse | kPeel | kWaveRun) \
     X(2, kNtLoad | kSc1Store | kDepth2 | kPeel | kWaveRun) \
     X(1, kNtLoad | kSc1Store | kDepth2 | kFuse | kPeel) \
     X(2, kNtLoad | kSc1Store | kDepth2 | kFuse | kPeel | kWaveRun) \

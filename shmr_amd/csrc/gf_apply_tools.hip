@@ -512,9 +512,7 @@ __device__ __forceinline__ void store_run_aligned(uint8_t* p, const u32x4 (&v)[U
     X(4, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kPeel | kWaveRun) \
     X(4, kNtLoad | kNtStore | kDepth2 | kSegs | kPeel | kWaveRun) \
     X(1, kNtLoad | kSc1Store | kDepth2 | kSPre | kSegs) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kSPre | kSegs | kFuse) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kFuse | kPeel | kWaveRun) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kPeel | kWaveRun)
+    X(1, kNtLoad | kSc1Store | kDepth2 | kSPre | kSegs | kFuse)
 
 template <int R>
 hipError_t dispatch_tools(const ApplyArgs& a, const Variant& v, int grid_cap, hipStream_t s) {
