@@ -138,12 +138,26 @@ int shmr_ec_reconstruct(shmr_ec_t* rs, uint8_t* const* shards, const size_t* sha
  * a permanent pinned slot) on `stream` and return.  They can be captured into
  * a HIP graph (e.g. torch.cuda.graph) once the device is initialised; a
  * capture that would need the initialisation returns INVALID_ARGUMENT with
- * nothing enqueued.  SHMR_EC_DEV_BLOCKING_CALLS counts the exceptions. */
+ * nothing enqueued, and so does one whose stream state cannot be read (the
+ * legacy null stream while another thread captures in global mode).
+ * SHMR_EC_DEV_BLOCKING_CALLS counts the exceptions. */
 
 /* One-time per-device initialisation (probe of the memory system's unaligned
- * access mode on a private stream, the plan arena in pinned and device
- * memory).  Optional: the first device call does it implicitly.  Blocking. */
+ * access mode on a private stream, the plan arena and a 4 MiB capture reserve
+ * in pinned and device memory).  Optional: the first device call does it
+ * implicitly.  Blocking. */
 int shmr_ec_device_init(int device);
+
+/* Captured calls keep their tables in the device's capture reserve, which a
+ * capture never grows: a captured *_ptrs_dev call needs nblocks * total * 8
+ * bytes, a captured reconstruct of several erasure patterns in more than 32
+ * block runs about 6 bytes per block plus 8 per pattern (each rounded up to
+ * 256 bytes).  A captured call that does not fit returns OUT_OF_MEMORY with
+ * nothing enqueued.  This makes sure one free range of `bytes` exists
+ * (initialising the device if needed; blocking, not inside a capture).  A
+ * captured call's block returns to the reserve when its graph and every
+ * executable graph instantiated from it have been destroyed. */
+int shmr_ec_capture_reserve(int device, size_t bytes);
 
 /* Encode nblocks blocks: data shard i of block b at
  * d_data + b*data_block_pitch + i*data_shard_pitch; parity shard r at
@@ -308,6 +322,20 @@ int shmr_ec_get_tuning(const char* key);
  * device shard-pointer tables, *_ptrs_dev: encode 3, reconstruct 4). */
 int shmr_ec_describe_variant(int decode, uint32_t data_shards, uint32_t rows, char* buf, size_t len);
 
+/* Kernel inventory: every gf_apply kernel instantiation compiled into this
+ * library -- the full-tile kernels the launch policy can select (mode 0, one
+ * per reachable (rows, chunks, flags); the product list is derived from the
+ * policy at compile time) and the partial-tile (mode 1), byte-granular (mode 2)
+ * and realigning (mode 3) kernels per row count -- with the launches each has
+ * served in this process.  Writes min(cap, count) entries and returns the
+ * count (out may be NULL to query it).  flags are the kernel's template flags
+ * (the F of gf_apply_kernel<R, U, MODE, F> in the code object's symbol). */
+typedef struct shmr_ec_kernel_info {
+    uint32_t rows, chunks, mode, flags;
+    uint64_t launches;
+} shmr_ec_kernel_info;
+size_t shmr_ec_kernel_inventory(shmr_ec_kernel_info* out, size_t cap);
+
 /* Decode-matrix LRU statistics of the (data, parity) codec (crate cache
  * semantics, capacity 254). */
 int shmr_ec_cache_stats(const shmr_ec_t* rs, uint64_t* hits, uint64_t* misses);
@@ -339,7 +367,9 @@ enum {
                                              for a ring slot (not the host-buffer calls' final sync) */
     SHMR_EC_DEV_PTR_TABLE_HITS = 7,       /* *_ptrs_dev tables reused from the device's table cache
                                              (no upload) */
-    SHMR_EC_DEV_COUNTERS = 8
+    SHMR_EC_DEV_CAPTURE_TABLES = 8,       /* capture-reserve blocks taken by captured calls */
+    SHMR_EC_DEV_CAPTURE_RELEASED = 9,     /* ... and returned when their graph was destroyed */
+    SHMR_EC_DEV_COUNTERS = 10
 };
 int shmr_ec_device_stats(int device, uint64_t* out, size_t n);
 

@@ -59,6 +59,7 @@ SIGNATURES = [
      [ctypes.c_void_p, ctypes.c_void_p, _sz, _sz, _u8p, _sz, _sz, ctypes.c_int, ctypes.c_void_p, _sz, _sz,
       ctypes.c_int, ctypes.c_void_p]),
     ("shmr_ec_device_init", ctypes.c_int, [ctypes.c_int]),
+    ("shmr_ec_capture_reserve", ctypes.c_int, [ctypes.c_int, _sz]),
     ("shmr_ec_encode_ptrs_dev", ctypes.c_int, [ctypes.c_void_p, _u8pp, _sz, _sz, ctypes.c_int, ctypes.c_void_p]),
     ("shmr_ec_reconstruct_ptrs_dev", ctypes.c_int,
      [ctypes.c_void_p, _u8pp, _u8p, _sz, _sz, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
@@ -81,7 +82,14 @@ SIGNATURES = [
      [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     ("shmr_ec_device_count", ctypes.c_int, []),
     ("shmr_ec_device_stats", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), _sz]),
+    ("shmr_ec_kernel_inventory", _sz, [ctypes.c_void_p, _sz]),
 ]
+
+
+class KernelInfo(ctypes.Structure):
+    """shmr_ec_kernel_info (include/shmr_ec.h)."""
+    _fields_ = [("rows", ctypes.c_uint32), ("chunks", ctypes.c_uint32), ("mode", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32), ("launches", ctypes.c_uint64)]
 
 _libs = {}
 _flavour = "tools" if os.environ.get("SHMR_EC_FLAVOUR") == "tools" else "product"

@@ -168,12 +168,14 @@ int shmr_ec_describe_variant(int decode, uint32_t data_shards, uint32_t rows, ch
     if (decode < 0 || decode > 4) return SHMR_EC_INVALID_ARGUMENT;
     const core::OpClass op = (decode == 1 || decode == 2 || decode == 4) ? core::kDecode : core::kEncode;
     const uint32_t r = std::min<uint32_t>(rows, shmr::kern::kMaxRowsPerLaunch);
-    // 3 / 4: encode / reconstruct over device shard-pointer tables (aligned shards)
-    const auto v = decode >= 3 ? core::launch_variant(op, data_shards, r, false, true, false, false)
-                               : core::resolve_variant(op, data_shards, r, false, decode == 2);
+    // 3 / 4: encode / reconstruct over device shard-pointer tables (aligned
+    // shards); the variant of a shard length with a partial last tile
+    const shmr::kern::LaunchShape s =
+        core::shape_of(op, data_shards, r, false, decode >= 3, false, decode == 2, true, true);
+    const auto v = core::select_variant(op, s);
     auto lean = v;   // the full-tile kernel without fused tails must always exist
     lean.fuse_tail = false;
-    const bool compiled = shmr::kern::variant_compiled(lean) && (!v.fuse_tail || shmr::kern::variant_compiled(v));
+    const bool compiled = shmr::kern::variant_compiled(lean, r) && (!v.fuse_tail || shmr::kern::variant_compiled(v, r));
     std::snprintf(buf, len,
                   "chunks=%d nt_load=%d nt_store=%d occ8=%d threads=%d grid=%d diag=%d depth=%d "
                   "wgs_per_cu=%d occ=%d early=%d spre=%d fuse_tail=%d compiled=%d",
@@ -191,6 +193,11 @@ int shmr_ec_describe_variant(int decode, uint32_t data_shards, uint32_t rows, ch
     return SHMR_EC_OK;
 }
 
+size_t shmr_ec_kernel_inventory(shmr_ec_kernel_info* out, size_t cap) {
+    static_assert(sizeof(shmr_ec_kernel_info) == sizeof(shmr::kern::KernelInfo), "kernel info layout");
+    return shmr::kern::kernel_inventory(reinterpret_cast<shmr::kern::KernelInfo*>(out), out ? cap : 0);
+}
+
 int shmr_ec_cache_stats(const shmr_ec_t* rs, uint64_t* hits, uint64_t* misses) {
     if (!rs) return SHMR_EC_INVALID_ARGUMENT;
     if (hits) *hits = rs->codec->decode_cache_hits();
@@ -205,6 +212,14 @@ int shmr_ec_device_init(int device) {
         const int rc = core::check_device(device);
         if (rc) return rc;
         return core::device_init(device, nullptr);
+    });
+}
+
+int shmr_ec_capture_reserve(int device, size_t bytes) {
+    return guarded([&]() -> int {
+        const int rc = core::check_device(device);
+        if (rc) return rc;
+        return core::capture_reserve(device, bytes);
     });
 }
 
@@ -536,6 +551,17 @@ static int ptrs_dev(shmr_ec_t* rs, uint8_t* const* d_shards, const uint8_t* pres
         const hipStream_t stream = static_cast<hipStream_t>(stream_);
         rc = core::device_init(device, stream);
         if (rc) return rc;
+        // The kernels read each block's row in plan order (input t at [t],
+        // output r at [k + r]): a reconstruct's rows are permuted here, once per
+        // call, so no shard address in the kernel waits on a plan index load.
+        // An encode table is already in plan order.
+        const uint64_t* table = reinterpret_cast<const uint64_t*>(d_shards);
+        std::vector<uint64_t> permuted;
+        if (op == core::kDecode) {
+            permuted.resize(nblocks * t);
+            core::permute_ptr_rows(table, present, nblocks, k, t, data_only != 0, permuted.data());
+            table = permuted.data();
+        }
         auto run = [&](const uint8_t* d_tab, size_t b0, size_t n) -> int {
             core::Layout L{nullptr, nullptr, 0, 0, 0, 0, 0};
             L.d_ptrs = reinterpret_cast<const uint64_t*>(d_tab);
@@ -545,12 +571,14 @@ static int ptrs_dev(shmr_ec_t* rs, uint8_t* const* d_shards, const uint8_t* pres
             return core::reconstruct_on_device(c, device, L, present + b0 * t, n, shard_len, data_only != 0, stream);
         };
         static_assert(sizeof(uint8_t*) == sizeof(uint64_t), "64-bit device pointers");
-        if (core::stream_capturing(stream)) {
+        bool capturing = false;
+        if ((rc = core::capture_state(stream, &capturing))) return rc;
+        if (capturing) {   // a block of the capture reserve, returned when the graph is destroyed
             const size_t bytes = nblocks * t * sizeof(uint64_t);
             uint8_t *h = nullptr, *d = nullptr;
-            rc = core::arena_alloc(device, bytes, true, &h, &d);
+            rc = core::capture_alloc(device, stream, bytes, &h, &d);
             if (rc) return rc;
-            std::memcpy(h, d_shards, bytes);
+            std::memcpy(h, table, bytes);
             if (hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream) != hipSuccess) {
                 (void)hipGetLastError();
                 return SHMR_EC_DEVICE_ERROR;
@@ -566,7 +594,7 @@ static int ptrs_dev(shmr_ec_t* rs, uint8_t* const* d_shards, const uint8_t* pres
             // a table this stream passed before (same bytes): its device copy, no upload
             const uint8_t* dtab = nullptr;
             int entry = -1;
-            rc = cache->lookup(d_shards + b0 * t, n * t * sizeof(uint64_t), stream, &dtab, &entry);
+            rc = cache->lookup(table + b0 * t, n * t * sizeof(uint64_t), stream, &dtab, &entry);
             if (rc) return rc;
             if (dtab) {
                 rc = run(dtab, b0, n);
@@ -580,7 +608,7 @@ static int ptrs_dev(shmr_ec_t* rs, uint8_t* const* d_shards, const uint8_t* pres
             int slot = -1;
             rc = ring->acquire(&hslot, &dslot, &slot);
             if (rc) return rc;
-            std::memcpy(hslot, d_shards + b0 * t, n * t * sizeof(uint64_t));
+            std::memcpy(hslot, table + b0 * t, n * t * sizeof(uint64_t));
             rc = ring->upload(slot, n * t * sizeof(uint64_t), stream);
             if (rc == SHMR_EC_OK) rc = run(dslot, b0, n);
             const int rc2 = ring->release_after(slot, stream);

@@ -10,7 +10,7 @@ namespace shmr {
 namespace core {
 
 // ===========================================================================
-// Tuning.  kAuto knobs follow variant_policy(): the fastest variants measured
+// Tuning.  kAuto knobs follow kern::policy_variant: the fastest variants measured
 // on MI355X per launch shape (tools/tune.py, interleaved A/B in one process;
 // DESIGN.md "Tuning").  set_tuning() pins a knob explicitly.
 // ===========================================================================
@@ -54,91 +54,38 @@ std::atomic<int> g_alias_devices{0};   // tools build: alias device IDs (see ec_
 std::atomic<int> g_ptrs_segs{1};
 // Misaligned device-resident shards: kAuto = the vector kernels (modes 0 / 1)
 // where the device passed probe_unaligned_vector, else the realigning kernel
-// (mode 3); 0 = always mode 3, 1 = always modes 0 / 1 (tools build only).
+// (mode 3); 0 = always mode 3 (what a device that fails the probe runs: exact
+// results, so the product build takes it too -- the kernel sweep test runs the
+// fallback kernels of the product library this way), 1 = always modes 0 / 1
+// (tools build only: wrong on a device without the unaligned mode).
 std::atomic<int> g_uvec{kAuto};
 
-// Measured (tools/tune.py, interleaved A/B in one process): a register ring
-// of depth 2 (one shard of loads in flight per wave) beats depth 3 on every
-// shape -- RS(8,3) encode 80 % vs 78 % of HBM peak (it also frees the VGPRs
-// that lift RS(8,3) from 5 to 6 waves/SIMD), RS(4,2) 78 % vs 77 %, RS(10,4)
-// 71 % vs 70 %, reconstruct RS(8,3) 72 % vs 71 %; deeper rings (5, 9) and
-// occupancy caps lose.  With depth 2, NT loads + NT stores win everywhere;
-// launches of 4 rows use U = 2.  Encodes with k <= 8 (short-lived
-// workgroups) issue their first data loads ahead of the plan staging
-// ("early": RS(4,2) 83 % vs 80 %; -2 % on decode, re-measured with segment
-// launches: RS(8,3) 71.1 vs 72.6 %, RS(10,4) 75.1 vs 76.6 %).  Decodes with temporal stores lose 5-8 points (RS(8,3) 64.8 vs
-// 73.3 %, RS(10,4) 70.7 vs 75.9 %), although a copy-only 8-in/1-out probe
-// preferred them (tools/membench.hip).
-// Scalar-loaded tables ("spre", 7-8 waves/SIMD) lose 3-6 % everywhere.
-// An XCD-grouped tile order (workgroup w -> tile (w % 8) * n/8 + w / 8, each
-// XCD streaming one contiguous eighth) measured within +-2 % and was dropped.
-// Shard lengths that are not a multiple of the tile (RS(10,4):
-// S = 1,677,722) run each block's partial last tile at the HEAD of the
-// full-tile grid ("fuse_tail"): 5.5-5.8 % less time than a second launch of
-// 64 latency-bound workgroups after the full tiles.  Placed at each block's
-// end instead, the slow partial tiles finished last and the fused launch lost
-// 5 %; a concurrent side-stream tail launch lost 3 %; uploading multi-plan
-// tables on a side stream was neutral.  Computing an encode's shard offsets
-// arithmetically (identity plan) instead of reading them from LDS before each
-// look-ahead load measured neutral (-0.2 to -1 %): the LDS round trip hides
-// under the other waves.
-//
-// Zero-copy launches over mapped host memory (the kernel's loads and stores
-// cross PCIe) are bound by the link, not HBM: there plain (temporal) loads
-// measured 72 GB/s of RS(8,3) encode traffic vs 64 with nontemporal loads
-// (tools/pcie_probe.py), and the shard-pointer tile has no early prologue.
-// Single-row reconstructs (one lost shard: RS(8,3) decode) fit 8 waves/SIMD
-// (39 VGPRs); capping residency at 7 workgroups per CU (LDS padding) measured
-// +1.4 to +1.7 points of HBM peak on two boxes (73.9-74.7 vs 72.6-73.0 %;
-// caps of 6, 5, 4 lose; profiles/r02/ab_occ*_decode83.txt).  Neutral for
-// RS(10,4) 2-row decodes and RS(8,3) encodes, so only there.
-//
-// Reconstructs into a compact output (shmr_ec_reconstruct_batch_dev_out: the
-// rebuilt shards of a block written densely to a separate array, the crate's
-// fresh-allocation semantics) store with the sc1 cache policy and no
-// residency cap.  Measured with real parity content, in-place and compact
-// interleaved in one process (profiles/r03/r03c/, r03b/): RS(10,4) 2-erasure
-// rebuilds 81.1 / 81.2 % of peak (two boxes) against 77.4 % with nontemporal
-// stores into the same compact output and 77.5 % in place; RS(8,3) 1-erasure
-// rebuilds sc1 and nontemporal-with-cap within 0.6 point of each other on
-// three boxes (73.7-79.7 %, the box decides).  Plain stores lose 3-6 points.
-kern::Variant variant_policy(OpClass op, unsigned k, unsigned rows, bool host_mapped, bool compact = false) {
-    kern::Variant v;
-    if (op == kDecode && rows == 1 && !host_mapped) v.wgs_per_cu = 7;
-    // U = 2 (8 KiB tiles) for 4-row launches, encode and reconstruct alike: a
-    // 4-erasure RS(10,4) rebuild 73.8 vs 67.8-68.9 % at U = 1, while 2- and
-    // 3-row rebuilds lose 5-7 points at U = 2 (profiles/r02/tune_decode*.txt)
-    v.u = rows >= 4 ? 2 : 1;
-    v.nt_store = true;
-    v.nt_load = !host_mapped;
-    v.depth = 2;
-    // early prologue for k <= 8 (RS(8,3) with de-aliased shard slots +1.2 -
-    // 1.4 points, RS(8,1) / RS(8,2) +2.4, RS(4,2) +1.7 - 2.6; RS(8,3) on the
-    // contiguous 2^19-stride layout -0.3 - 0.6: profiles/r02/pad/); for
-    // 4-row encodes (RS(10,4)) early plus the per-dword math order (fewer live
-    // VGPRs at U = 2): +0 - 1.0 point in interleaved A/Bs
-    // (profiles/r02/tune_encode104_early_serial*.txt); serial loses on RS(8,3)
-    // encode (profiles/r02/tune_encode83_early_serial.txt)
-    v.early = op == kEncode && (k <= 8 || rows >= 4) && !host_mapped;
-    v.serial = op == kEncode && rows >= 4 && !host_mapped;
-    v.fuse_tail = true;   // only where len % tile != 0 (RS(10,4): -5.5 % encode, -5.8 % decode time)
-    // reconstructs peel the shard ring's tail (no look-ahead load past the
-    // last input): RS(8,3) compact +0.9, in place +1.0, RS(10,4) compact +0.5
-    // points; the early-prologue encodes lose with it (RS(8,3) -2.5), so they
-    // keep the clamped look-ahead (profiles/r03/r03h/tune_*_peel.txt)
-    v.peel = op == kDecode && !host_mapped;
-    if (compact && op == kDecode && !host_mapped) {
-        v.sc1_store = true;
-        v.nt_store = false;
-        v.wgs_per_cu = 0;
-        // with sc1 stores the early prologue pays for rebuilds of 2+ rows:
-        // RS(10,4) 2 erasures +0.7 / +0.7 / +1.1 (-0.8 on a third box), RS(8,3)
-        // 3 erasures +0.5 / +0.5, RS(10,4) 4 erasures (U = 2) +1.3 / +1.8;
-        // RS(8,3) 1 erasure -0.9 (profiles/r03/early_dec/)
-        v.early = rows >= 2;
-    }
-    return v;
-}
+// The launch policy itself is kern::policy_variant (gf_apply.hpp): constexpr,
+// so the product library compiles exactly the kernels it can select.  Its
+// measured basis (tools/tune.py, interleaved A/B in one process):
+//  * depth-2 register ring (one shard of loads in flight per wave) beats depth
+//    1 / 3 / 5 / 9 on every shape; nontemporal loads + stores win with it.
+//  * U = 2 (8 KiB tiles) for 4-row launches: 4-erasure RS(10,4) rebuild 73.8
+//    vs 67.8-68.9 % of HBM peak; 2- and 3-row launches lose 5-7 points at U = 2.
+//  * early prologue for encodes with k <= 8 (RS(8,3) on padded slots +1.2 -
+//    1.4 points, RS(4,2) +1.7 - 2.6) and, with the per-dword math order, for
+//    4-row encodes (+1.0 / +0.5 / +1.0 / 0.0 on four boxes).
+//  * partial last tiles at the head of the full-tile grid: -5.5 % (encode) /
+//    -5.8 % (decode) time against a separate tail launch.
+//  * reconstructs peel the ring's tail (no look-ahead load past the last input;
+//    profiles/r03/r03h/).  1-row in-place rebuilds cap residency at 7
+//    workgroups per CU (+1.4 - 1.7 on two boxes).
+//  * rebuilt shards into buffers of their own (compact output, device pointer
+//    tables): sc1 stores, no cap (RS(10,4) 2-erasure 81.1 / 81.2 % vs 77.4 %
+//    with nontemporal stores); the early prologue there only for 4-row
+//    rebuilds (+1.3 / +1.8).  r04 re-judged the 2- and 3-row adoptions of r03
+//    (+0.7 / +0.7 / +1.1 / -0.8 and +0.5 / +0.5: under one point, not repeated
+//    on three boxes) and dropped them.
+//  * mapped host shards (zero-copy across PCIe): temporal loads (72 vs 64 GB/s
+//    of RS(8,3) encode traffic), the plain LDS-staged tile.
+//  * device pointer tables: the early prologue (first loads addressed from
+//    scalar loads of the block's table row) for RS(8,3) encode (+1.8) and
+//    every rebuild (+3.4 / +8.2 with sc1); RS(10,4) encode keeps the plain tile.
 
 bool split_key(const char* key, std::string* k, int* first, int* last) {
     if (!key) return false;
@@ -186,14 +133,14 @@ int set_tuning(const char* key, int value) {
         g_sync_spin = value == kAuto ? kSyncSpinDefault : value;
         return SHMR_EC_OK;
     }
-    if (k == "uvec") {   // not per op class; kAuto only in the product build
+    if (k == "uvec") {   // not per op class; the product build takes kAuto and 0
 #ifdef SHMR_EC_TOOLS
         if (value != kAuto && value != 0 && value != 1) return SHMR_EC_INVALID_ARGUMENT;
+#else
+        if (value != kAuto && value != 0) return SHMR_EC_INVALID_ARGUMENT;
+#endif
         g_uvec = value;
         return SHMR_EC_OK;
-#else
-        return value == kAuto ? SHMR_EC_OK : SHMR_EC_INVALID_ARGUMENT;
-#endif
     }
     if (k == "alias_devices") {   // not per op class; tools build only (see ec_core.hpp)
         const int v = value == kAuto ? 0 : value;
@@ -315,41 +262,97 @@ int get_tuning(const char* key) {
     return SHMR_EC_INVALID_ARGUMENT;
 }
 
-kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_mapped, bool compact) {
+kern::Variant select_variant(OpClass op, const kern::LaunchShape& s) {
+    kern::Variant v = kern::policy_variant(s);
+#ifdef SHMR_EC_TOOLS
+    // Tools build: explicit knobs override the policy (measurement variants).
     const Tuning& T = g_tune[op];
-    kern::Variant v = variant_policy(op, k, rows, host_mapped, compact);
     if (T.u.load() != kAuto) v.u = T.u.load();
     if (T.nt_load.load() != kAuto) v.nt_load = T.nt_load.load() != 0;
     if (T.nt_store.load() != kAuto) v.nt_store = T.nt_store.load() != 0;
     v.occ8 = T.occ8.load() != 0;
-#ifdef SHMR_EC_TOOLS
     v.diag = T.diag.load() != 0;
-#endif
     v.threads = T.threads.load();
     if (T.depth.load() != kAuto) v.depth = T.depth.load();
     if (T.wgs_per_cu.load() != kAuto) v.wgs_per_cu = T.wgs_per_cu.load();
     if (T.occ.load() != kAuto) v.occ = T.occ.load();
     if (T.early.load() != kAuto) v.early = T.early.load() != 0;
     if (T.spre.load() != kAuto) v.spre = T.spre.load() != 0;
-    if (T.fuse_tail.load() != kAuto) v.fuse_tail = T.fuse_tail.load() != 0;
+    if (T.fuse_tail.load() == 0) v.fuse_tail = false;
     if (T.glds.load() != kAuto) v.glds = T.glds.load() != 0;
     if (T.serial.load() != kAuto) v.serial = T.serial.load() != 0;
     if (T.sc1_store.load() != kAuto) v.sc1_store = T.sc1_store.load() != 0;
     if (T.peel.load() != kAuto) v.peel = T.peel.load() != 0;
     if (T.xcd.load() != kAuto) v.xcd = T.xcd.load() != 0;
-    // U = 2 slots in wave-contiguous runs on device memory: RS(10,4) packed
-    // encode +1.9 points (misaligned parity stores +2.2), aligned +0.1 - 0.4,
-    // 4-erasure rebuild +0.8 (profiles/r03/r03k/); the realigning, LDS-DMA
-    // and scalar-table tiles keep their own column maps
     if (T.wave_run.load() != kAuto)
         v.wave_run = T.wave_run.load() != 0;
     else
-        v.wave_run = v.u > 1 && v.nt_load && v.depth == 2 && v.threads == 256 && !v.occ8 && !host_mapped && !v.glds &&
-                     !v.spre;
-    if (v.sc1_store) v.nt_store = false;   // one store policy per kernel
-    if (v.glds) v.early = v.spre = false;   // the LDS-DMA ring is a form of the plain tile
+        v.wave_run = v.u > 1 && v.nt_load && v.depth == 2 && v.threads == 256 && !v.occ8 && !s.host_mapped &&
+                     !v.glds && !v.spre;
+    if (v.sc1_store) v.nt_store = false;        // one store policy per kernel
+    if (v.glds) v.early = v.spre = false;       // the LDS-DMA ring is a form of the plain tile
     if (v.glds || v.depth != 2) v.peel = false;   // peeling is a form of the depth-2 register ring
+    if (s.ptrs) v.spre = v.glds = false;        // the plain and the early tiles read pointer tables
+    if (v.sc1_store && !s.sc1_ok) {
+        v.sc1_store = false;
+        v.nt_store = true;
+    }
+#else
+    (void)op;
+#endif
     return v;
+}
+
+kern::LaunchShape shape_of(OpClass op, unsigned k, unsigned rows, bool host_mapped, bool ptrs, bool segs,
+                           bool compact, bool sc1_ok, bool fused) {
+    kern::LaunchShape s;
+    s.decode = op == kDecode;
+    s.small_k = k <= 8;
+    s.rows = rows;
+    s.host_mapped = host_mapped;
+    s.ptrs = ptrs;
+    s.segs = segs && s.decode;
+    s.compact = compact && s.decode && !ptrs && !host_mapped;
+    s.sc1_ok = sc1_ok && !host_mapped;
+    s.fused = fused;
+    return s;
+}
+
+bool segs_supported(OpClass op, unsigned k, bool host_mapped, bool ptrs, bool compact) {
+#ifdef SHMR_EC_TOOLS
+    for (unsigned rows = 1; rows <= kern::kMaxRowsPerLaunch; ++rows)
+        for (bool sc1_ok : {false, true}) {
+            const kern::LaunchShape s = shape_of(op, k, rows, host_mapped, ptrs, true, compact, sc1_ok, false);
+            if (!kern::variant_compiled(select_variant(op, s), rows)) return false;
+        }
+#else
+    (void)op, (void)k, (void)host_mapped, (void)ptrs, (void)compact;   // every policy shape is compiled
+#endif
+    return true;
+}
+
+void permute_ptr_rows(const uint64_t* src, const uint8_t* present, size_t n, unsigned k, unsigned t, bool data_only,
+                      uint64_t* dst) {
+    for (size_t b = 0; b < n; ++b) {
+        const uint64_t* s = src + b * t;
+        uint64_t* d = dst + b * t;
+        const uint8_t* pr = present ? present + b * t : nullptr;
+        unsigned np = 0;
+        for (unsigned i = 0; pr && i < t; ++i) np += pr[i] ? 1 : 0;
+        if (!pr || np == t) {   // encode (already in plan order), or nothing to rebuild
+            std::memcpy(d, s, size_t(t) * sizeof(uint64_t));
+            continue;
+        }
+        unsigned ni = 0, no = 0;
+        for (unsigned i = 0; i < t; ++i) {
+            if (pr[i]) {
+                if (ni < k) d[ni++] = s[i];   // the first k present shards, in index order
+            } else if (i < k || !data_only) {
+                d[k + no++] = s[i];           // the absent ones, ascending
+            }
+        }
+        for (unsigned j = k + no; j < t; ++j) d[j] = 0;
+    }
 }
 
 int grid_mode(OpClass op) { return g_tune[op].grid.load(); }
@@ -370,51 +373,6 @@ hipError_t sync_stream(hipStream_t stream) {
         } while (std::chrono::steady_clock::now() < until);
     }
     return hipStreamSynchronize(stream);
-}
-
-kern::Variant launch_variant(OpClass op, unsigned k, unsigned rows, bool host_mapped, bool ptrs, bool segs,
-                             bool compact) {
-    // Device-memory shard-pointer tables (shmr_ec_*_ptrs_dev): every rebuilt
-    // shard is a buffer of its own, so reconstructs take the compact form's
-    // store policy (sc1, no residency cap)
-    const bool dev_ptrs = ptrs && !host_mapped;
-    kern::Variant v = resolve_variant(op, k, rows, host_mapped, (compact && !ptrs) || (dev_ptrs && op == kDecode));
-    v.ptrs = ptrs;
-    v.segs = segs;
-    if (ptrs) {
-        v.spre = v.glds = false;   // the plain and the early-prologue tiles read pointer tables
-        const Tuning& T = g_tune[op];
-        if (host_mapped) {         // the mapped policy: the plain LDS-staged tile
-            v.early = false;
-            if (T.serial.load() == kAuto) v.serial = false;   // the policy's serial goes with early
-        } else if (T.early.load() == kAuto) {
-            // Measured on separate torch allocations per shard (tools/tune.py --ptrs,
-            // profiles/r03/ptrs/): the early prologue, whose first loads take their
-            // addresses from scalar loads of the block's table row, wins for RS(8,3)
-            // encode (+1.8 points) and for reconstructs with sc1 stores (RS(8,3) +3.4,
-            // RS(10,4) +8.2 over the plain tile with nontemporal stores); RS(10,4)
-            // encode loses 1.5 with it
-            v.early = op == kDecode || k <= 8;
-            if (!v.early && T.serial.load() == kAuto) v.serial = false;
-        }
-        kern::Variant lean = v;
-        lean.fuse_tail = false;
-        if (!kern::variant_compiled(lean)) {   // tuned knobs without a pointer-table build: the mapped policy
-            v = variant_policy(op, k, rows, true);
-            v.ptrs = true;
-            v.segs = segs;
-        }
-    }
-    return v;
-}
-
-bool segs_supported(OpClass op, unsigned k, bool host_mapped, bool ptrs, bool compact) {
-    for (unsigned rows : {1u, kern::kMaxRowsPerLaunch}) {
-        kern::Variant v = launch_variant(op, k, rows, host_mapped, ptrs, true, compact);
-        v.fuse_tail = false;
-        if (!kern::variant_compiled(v)) return false;
-    }
-    return true;
 }
 
 // ===========================================================================
@@ -472,12 +430,24 @@ struct ArenaChunk {
     size_t cap = 0, used = 0;
 };
 
+// The capture reserve: tables of captured calls, first-fit over chunks of
+// pinned + device memory, each block back on its chunk's free list when the
+// graph that captured it is destroyed (capture_alloc).
+struct CaptureChunk {
+    uint8_t* host = nullptr;
+    uint8_t* dev = nullptr;
+    size_t cap = 0;
+    std::map<size_t, size_t> free_;   // offset -> length, coalesced
+};
+
 struct DeviceState {
     int dev = -1;
     bool uvec = false;             // probe verdict of the physical GPU
     hipStream_t priv = nullptr;    // private stream of init-time work
     std::mutex mu;                 // guards chunks
     std::vector<ArenaChunk> chunks;
+    std::mutex cmu;                // guards cchunks and their free lists
+    std::vector<CaptureChunk*> cchunks;   // leaked with the state (graphs may outlive everything)
 };
 
 std::mutex g_state_mu;                          // serialises device_init
@@ -505,15 +475,84 @@ int add_chunk(DeviceState& ds, size_t bytes) {
     ds.chunks.push_back(c);
     return SHMR_EC_OK;
 }
+
+constexpr size_t kCaptureChunk = size_t(4) << 20;   // the reserve device init creates
+
+// Blocking: pinned + device allocation.  Caller holds ds.cmu (or owns ds).
+int add_capture_chunk(DeviceState& ds, size_t bytes) {
+    auto* c = new CaptureChunk;
+    c->cap = round_up(bytes, kArenaAlign);
+    count_device(ds.dev, kDevBlockingCalls, 2);
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->host), c->cap, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        delete c;
+        return SHMR_EC_OUT_OF_MEMORY;
+    }
+    if (hipMalloc(reinterpret_cast<void**>(&c->dev), c->cap) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipHostFree(c->host);
+        delete c;
+        return SHMR_EC_OUT_OF_MEMORY;
+    }
+    c->free_[0] = c->cap;
+    ds.cchunks.push_back(c);
+    return SHMR_EC_OK;
+}
+
+size_t largest_free_locked(const DeviceState& ds) {
+    size_t best = 0;
+    for (const CaptureChunk* c : ds.cchunks)
+        for (const auto& r : c->free_) best = std::max(best, r.second);
+    return best;
+}
+
+void capture_free_locked(CaptureChunk* c, size_t off, size_t len) {
+    auto it = c->free_.emplace(off, len).first;
+    auto next = std::next(it);
+    if (next != c->free_.end() && it->first + it->second == next->first) {
+        it->second += next->second;
+        c->free_.erase(next);
+    }
+    if (it != c->free_.begin()) {
+        auto prev = std::prev(it);
+        if (prev->first + prev->second == it->first) {
+            prev->second += it->second;
+            c->free_.erase(it);
+        }
+    }
+}
+
+// One captured call's table: returned to the reserve by the destructor of the
+// HIP user object its graph holds (runs on a HIP thread: no HIP calls here).
+struct CaptureBlock {
+    DeviceState* ds;
+    CaptureChunk* c;
+    size_t off, len;
+};
+void release_capture_block(void* p) {
+    auto* b = static_cast<CaptureBlock*>(p);
+    {
+        std::lock_guard<std::mutex> lock(b->ds->cmu);
+        capture_free_locked(b->c, b->off, b->len);
+    }
+    count_device(b->ds->dev, kDevCaptureReleased);
+    delete b;
+}
 }  // namespace
 
-bool stream_capturing(hipStream_t stream) {
+int capture_state(hipStream_t stream, bool* capturing) {
+    *capturing = false;
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(stream, &st) != hipSuccess) {
+    const hipError_t e = hipStreamIsCapturing(stream, &st);
+    if (e != hipSuccess) {
         (void)hipGetLastError();
-        return true;   // unknown: take the capture-safe path
+        // e.g. the legacy null stream while another thread captures in global
+        // mode: the call would join (and break) that capture -- refuse it
+        return e == hipErrorStreamCaptureImplicit ? SHMR_EC_INVALID_ARGUMENT : SHMR_EC_DEVICE_ERROR;
     }
-    return st != hipStreamCaptureStatusNone;
+    if (st == hipStreamCaptureStatusInvalidated) return SHMR_EC_INVALID_ARGUMENT;
+    *capturing = st == hipStreamCaptureStatusActive;
+    return SHMR_EC_OK;
 }
 
 int device_init(int dev, hipStream_t caller) {
@@ -523,7 +562,12 @@ int device_init(int dev, hipStream_t caller) {
     if (state_of(dev)) return SHMR_EC_OK;
     // Init allocates and synchronises: inside a capture it would invalidate
     // the caller's graph, so it is refused there (nothing enqueued).
-    if (caller && stream_capturing(caller)) return SHMR_EC_INVALID_ARGUMENT;
+    if (caller) {
+        bool cap = false;
+        const int rc = capture_state(caller, &cap);
+        if (rc) return rc;
+        if (cap) return SHMR_EC_INVALID_ARGUMENT;
+    }
     DeviceScope scope(dev);
     if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
     auto* ds = new DeviceState;
@@ -537,6 +581,14 @@ int device_init(int dev, hipStream_t caller) {
     int rc = add_chunk(*ds, kArenaChunk);
     if (rc) {
         (void)hipStreamDestroy(ds->priv);
+        delete ds;
+        return rc;
+    }
+    rc = add_capture_chunk(*ds, kCaptureChunk);
+    if (rc) {
+        (void)hipStreamDestroy(ds->priv);
+        (void)hipHostFree(ds->chunks.back().host);
+        (void)hipFree(ds->chunks.back().dev);
         delete ds;
         return rc;
     }
@@ -585,6 +637,69 @@ int arena_alloc(int dev, size_t bytes, bool capturing, uint8_t** host, uint8_t**
     return SHMR_EC_OK;
 }
 
+int capture_reserve(int dev, size_t bytes) {
+    int rc = device_init(dev, nullptr);
+    if (rc) return rc;
+    DeviceState* ds = state_of(dev);
+    bytes = round_up(bytes ? bytes : 1, kArenaAlign);
+    std::lock_guard<std::mutex> lock(ds->cmu);
+    if (largest_free_locked(*ds) >= bytes) return SHMR_EC_OK;
+    DeviceScope scope(dev);
+    if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
+    return add_capture_chunk(*ds, std::max(bytes, kCaptureChunk));
+}
+
+int capture_alloc(int dev, hipStream_t stream, size_t bytes, uint8_t** host, uint8_t** devp) {
+    DeviceState* ds = state_of(dev);
+    if (!ds) return SHMR_EC_INVALID_ARGUMENT;
+    bytes = round_up(bytes ? bytes : 1, kArenaAlign);
+    CaptureChunk* chunk = nullptr;
+    size_t off = 0;
+    {
+        std::lock_guard<std::mutex> lock(ds->cmu);
+        for (CaptureChunk* c : ds->cchunks) {
+            for (auto it = c->free_.begin(); it != c->free_.end(); ++it)
+                if (it->second >= bytes) {
+                    chunk = c;
+                    off = it->first;
+                    const size_t rest = it->second - bytes;
+                    c->free_.erase(it);
+                    if (rest) c->free_[off + bytes] = rest;
+                    break;
+                }
+            if (chunk) break;
+        }
+    }
+    if (!chunk) return SHMR_EC_OUT_OF_MEMORY;   // never grown inside a capture: shmr_ec_capture_reserve
+    count_device(dev, kDevCaptureTables);
+    *host = chunk->host + off;
+    *devp = chunk->dev + off;
+    // Tie the block to the graph being captured: a user object the graph
+    // retains (and every executable graph made from it) returns the block when
+    // the last of them is destroyed.  Without the graph handle the block stays
+    // allocated for the life of the process.
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    hipGraph_t graph = nullptr;
+    const hipGraphNode_t* deps = nullptr;
+    size_t ndeps = 0;
+    if (hipStreamGetCaptureInfo_v2(stream, &st, &id, &graph, &deps, &ndeps) != hipSuccess || !graph) {
+        (void)hipGetLastError();
+        return SHMR_EC_OK;
+    }
+    auto* blk = new CaptureBlock{ds, chunk, off, bytes};
+    hipUserObject_t obj = nullptr;
+    if (hipUserObjectCreate(&obj, blk, release_capture_block, 1, hipUserObjectNoDestructorSync) != hipSuccess) {
+        (void)hipGetLastError();
+        delete blk;
+        return SHMR_EC_OK;
+    }
+    if (hipGraphRetainUserObject(graph, obj, 1, hipGraphUserObjectMove) != hipSuccess) {
+        (void)hipGetLastError();   // the object (and with it the block) is kept for good
+    }
+    return SHMR_EC_OK;
+}
+
 // ---- plan images ---------------------------------------------------------------
 namespace {
 // One plan image on one device ID: a permanent pinned copy and its device
@@ -622,7 +737,9 @@ int upload_plan(PlanDev& pd, hipStream_t stream, bool capturing) {
 }  // namespace
 
 int plan_on_device(Plan& plan, int dev, hipStream_t stream, bool compact, const uint8_t** out) {
-    const bool cap = stream_capturing(stream);
+    bool cap = false;
+    const int crc = capture_state(stream, &cap);
+    if (crc) return crc;
     std::lock_guard<std::mutex> lock(plan.dev_mu);
     void*& slot = plan.dev_image[dev * 2 + (compact ? 1 : 0)];
     auto* pd = static_cast<PlanDev*>(slot);
@@ -707,7 +824,21 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
     for (uint32_t row0 = 0; row0 < plan.m; row0 += kern::kMaxRowsPerLaunch) {
         const uint32_t rows = std::min<uint32_t>(kern::kMaxRowsPerLaunch, plan.m - row0);
         count_device(dev, kDevLaunches);
-        kern::Variant var = launch_variant(op, plan.k, rows, L.host_mapped, ptrs, bs.segs != nullptr, L.compact);
+        // sc1 stores are raw buffer stores: a 2 GiB resource per output row,
+        // and 16-byte aligned outputs only (the unaligned-access probe covers
+        // the global instructions); otherwise nontemporal global stores
+        const bool sc1_ok = len < (uint64_t(1) << 31) - 4096 && !L.host_mapped && (ptrs ? L.ptrs_aligned : out16);
+        kern::LaunchShape shape = shape_of(op, plan.k, rows, L.host_mapped, ptrs, bs.segs != nullptr, L.compact,
+                                           sc1_ok, false);
+        kern::Variant var = select_variant(op, shape);
+        {   // fused tails: the partial last tile of every block leads the full-tile grid
+            const uint64_t tb0 = kern::tile_bytes(var.u, var.threads);
+            if (len >= tb0 && len % tb0 != 0) {
+                shape.fused = true;
+                const kern::Variant fv = select_variant(op, shape);
+                if (fv.fuse_tail && kern::variant_compiled(fv, rows)) var = fv;
+            }
+        }
         // Misaligned shards on a device with unaligned vector access: the
         // policy's kernels as they are, or (knob "realign", tools build) the
         // realigning-load form of the plain tile
@@ -720,14 +851,6 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
         if (!out16 && !ptrs && g_tune[op].st_align.load() == 1 && !var.realign) {
             var.st_align = true;
             if (op == kDecode) var.early = false;   // measured (and compiled) on the plain rebuild tile
-        }
-        // sc1 stores are raw buffer stores: a 2 GiB resource per output row,
-        // and 16-byte aligned outputs only (the unaligned-access probe covers
-        // the global instructions); otherwise nontemporal global stores
-        if (var.sc1_store &&
-            (len >= (uint64_t(1) << 31) - 4096 || L.host_mapped || (ptrs ? !L.ptrs_aligned : !out16))) {
-            var.sc1_store = false;
-            var.nt_store = true;
         }
         const uint64_t tb = kern::tile_bytes(var.u, var.threads);
         kern::ApplyArgs a{};
@@ -778,13 +901,7 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
             continue;
         }
         const uint64_t full = len / tb;
-        // Fused tails: the partial last tile of every block leads the
-        // full-tile grid (one launch), if that instantiation is compiled.
-        bool fused = false;
-        if (var.fuse_tail && full > 0 && len % tb != 0) {
-            kern::Variant fv = var;
-            fused = kern::variant_compiled(fv);
-        }
+        const bool fused = var.fuse_tail && full > 0 && len % tb != 0;
         var.fuse_tail = fused;
         if (full) {
             a.col_base = 0;
@@ -937,15 +1054,18 @@ int reconstruct_on_device(Codec& c, int dev, const Layout& L, const uint8_t* pre
             if (rc) return rc;
         }
         const size_t ptab_bytes = (dplans.size() * sizeof(void*) + 15) & ~size_t(15);
-        if (stream_capturing(stream)) {
-            // Inside a capture the tables must outlive every replay: one
-            // permanent arena block per captured call (never reused).
+        bool capturing = false;
+        rc = capture_state(stream, &capturing);
+        if (rc) return rc;
+        if (capturing) {
+            // Inside a capture the tables must outlive every replay: a block of
+            // the capture reserve, returned when the graph is destroyed.
             const size_t n = grp.blocks.size();
             const size_t list_off = ptab_bytes;
             const size_t pidx_off = (list_off + n * sizeof(uint32_t) + 15) & ~size_t(15);
             const size_t total = pidx_off + n * sizeof(uint16_t);
             uint8_t *h = nullptr, *d = nullptr;
-            rc = arena_alloc(dev, total, true, &h, &d);
+            rc = capture_alloc(dev, stream, total, &h, &d);
             if (rc) return rc;
             std::memcpy(h, dplans.data(), dplans.size() * sizeof(void*));
             std::memcpy(h + list_off, grp.blocks.data(), n * sizeof(uint32_t));
@@ -1157,8 +1277,10 @@ int PtrTableCache::lookup(const void* tab, size_t bytes, hipStream_t stream, con
     if (victim < 0) {
         for (int i = 0; i < kEntries; ++i) {
             Entry& e = e_[i];
+            // (readers on the same stream included: a destroyed stream's handle
+            // may come back for a new stream while its kernels still run)
             if (e.busy || !event_done(e.up)) continue;
-            if (e.stream != stream && e.used_armed && !event_done(e.used)) continue;
+            if (e.used_armed && !event_done(e.used)) continue;
             if (victim < 0 || e.tick < e_[victim].tick) victim = i;
         }
     }

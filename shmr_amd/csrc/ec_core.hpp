@@ -36,15 +36,22 @@ constexpr int kAuto = -2;
 
 int set_tuning(const char* key, int value);
 int get_tuning(const char* key);
-// compact: a reconstruct that writes its rebuilt shards to a separate compact
-// output (shmr_ec_reconstruct_batch_dev_out) rather than into their slots.
-kern::Variant resolve_variant(OpClass op, unsigned k, unsigned rows, bool host_mapped = false, bool compact = false);
-// The full-tile variant a launch uses: resolve_variant plus the launch form
-// (shard-pointer tables, segment table), which selects its own instantiation.
-kern::Variant launch_variant(OpClass op, unsigned k, unsigned rows, bool host_mapped, bool ptrs, bool segs,
-                             bool compact = false);
-// Whether segment launches are compiled for this op's current tuning.
+// The full-tile variant of a launch shape: kern::policy_variant (gf_apply.hpp),
+// plus the tools build's kernel knobs.
+kern::Variant select_variant(OpClass op, const kern::LaunchShape& s);
+kern::LaunchShape shape_of(OpClass op, unsigned k, unsigned rows, bool host_mapped, bool ptrs, bool segs,
+                           bool compact, bool sc1_ok, bool fused);
+// Whether segment launches are compiled for this op's current tuning (always,
+// in the product build).
 bool segs_supported(OpClass op, unsigned k, bool host_mapped, bool ptrs, bool compact = false);
+// Shard-pointer table rows in plan order (kern::ApplyArgs::shard_ptrs): input t
+// at [t], output row r at [k + r].  src / dst: n rows of t entries.  present ==
+// nullptr (encode): the rows are already in plan order and are copied.  A
+// reconstruct's plan reads the first k present shards and writes the absent
+// ones in ascending index (data_only: the absent data shards only;
+// gf256.cpp Codec::reconstruct_plan); rows with every shard present are copied.
+void permute_ptr_rows(const uint64_t* src, const uint8_t* present, size_t n, unsigned k, unsigned t, bool data_only,
+                      uint64_t* dst);
 int grid_mode(OpClass op);
 // Largest block ((k+p) * shard bytes) a pageable single-block call bounces
 // through a mapped buffer instead of per-shard DMA copies (knob "bounce_kib").
@@ -84,6 +91,8 @@ enum DevCounter {
     kDevStagingStreams,
     kDevBlockingCalls,
     kDevPtrTableHits,
+    kDevCaptureTables,
+    kDevCaptureReleased,
     kDevCounters
 };
 void count_device(int dev, DevCounter c, uint64_t n = 1);
@@ -119,8 +128,21 @@ int device_init(int dev, hipStream_t caller = nullptr);
 // Whether misaligned device-resident shards may take the vector kernels (the
 // probe's verdict for the device, or the tools knob "uvec").  Needs the state.
 bool unaligned_vector(int dev);
-// Whether `stream` is being captured into a graph (queries nothing else).
-bool stream_capturing(hipStream_t stream);
+// Whether `stream` is being captured into a graph.  An error (e.g. the legacy
+// null stream while another thread captures in global mode:
+// INVALID_ARGUMENT; an invalidated capture: INVALID_ARGUMENT) is the caller's
+// status -- never taken for either answer.
+int capture_state(hipStream_t stream, bool* capturing);
+// The capture reserve (shmr_ec_capture_reserve): per-device pinned + device
+// memory for the tables of captured calls (shard-pointer tables of *_ptrs_dev,
+// block tables of multi-pattern reconstructs), which every replay re-reads.
+// Device init creates 4 MiB; capture_reserve makes sure one free range of
+// `bytes` exists (blocking; not inside a capture).  capture_alloc never grows
+// it (OUT_OF_MEMORY when no range fits) and ties the block to the graph being
+// captured on `stream`: it returns to the reserve when that graph and every
+// executable graph made from it are destroyed.
+int capture_reserve(int dev, size_t bytes);
+int capture_alloc(int dev, hipStream_t stream, size_t bytes, uint8_t** host, uint8_t** devp);
 
 // Device image of a plan (compact: the compact-output form, Plan::image),
 // written to the device's arena on first use and uploaded on `stream`; later

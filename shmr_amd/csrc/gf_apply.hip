@@ -29,7 +29,10 @@
 // live in gf_apply_tools.hip, linked into the tools build only.
 #include <hip/hip_runtime.h>
 
+#include <array>
+#include <atomic>
 #include <cstring>
+#include <utility>
 
 #include "gf_tile.hpp"
 
@@ -38,129 +41,122 @@ namespace kern {
 
 namespace {
 
-// The variants the tuning policy (ec_core.cpp variant_policy / launch_variant)
-// can select: depth-2 ring, nontemporal stores (sc1 for compact rebuilt-shard
-// outputs), nontemporal loads unless the shards are mapped host memory, U = 1
-// or 2, with the early prologue, fused tails, shard-pointer tables and segment
-// launches as launch forms.  An unsupported combination returns
-// hipErrorInvalidValue (the C ABI reports SHMR_EC_INVALID_ARGUMENT).
-#define SHMR_VARIANTS_PRODUCT(X) \
-    X(1, kNtLoad | kNtStore | kDepth2) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kWaveRun) \
-    X(1, kNtStore | kDepth2) \
-    X(2, kNtStore | kDepth2) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kEarly) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kWaveRun) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kFuse) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kWaveRun) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kWaveRun) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial | kWaveRun) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial | kWaveRun) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kPeel) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kPeel) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kPeel | kWaveRun) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kPeel | kWaveRun) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kPeel) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kPeel | kWaveRun) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kFuse | kPeel) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kPeel | kWaveRun) \
-    X(1, kNtStore | kDepth2 | kPtrs) \
-    X(2, kNtStore | kDepth2 | kPtrs) \
-    X(1, kNtStore | kDepth2 | kPtrs | kFuse) \
-    X(2, kNtStore | kDepth2 | kPtrs | kFuse) \
-    X(1, kNtStore | kDepth2 | kPtrs | kSegs) \
-    X(1, kNtStore | kDepth2 | kPtrs | kSegs | kFuse) \
-    X(2, kNtStore | kDepth2 | kPtrs | kSegs) \
-    X(2, kNtStore | kDepth2 | kPtrs | kSegs | kFuse) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kPtrs) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kPtrs | kWaveRun) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kPtrs | kPeel) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kFuse | kPtrs) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kPtrs | kWaveRun) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kPtrs) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPtrs) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial | kWaveRun | kPtrs) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial | kWaveRun | kPtrs) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kPtrs | kPeel) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kFuse | kPtrs | kPeel) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kPtrs | kPeel | kWaveRun) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kFuse | kPtrs | kPeel | kWaveRun) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kPtrs | kPeel) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPtrs | kPeel) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kPtrs | kPeel | kWaveRun) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPtrs | kPeel | kWaveRun) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kPtrs | kPeel) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kFuse | kPtrs | kPeel) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kPtrs | kPeel | kWaveRun) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kFuse | kPtrs | kPeel | kWaveRun) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kPtrs | kPeel) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kFuse | kPtrs | kPeel) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kPtrs | kPeel | kWaveRun) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kFuse | kPtrs | kPeel | kWaveRun) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kPtrs | kPeel | kWaveRun) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kPeel) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kPeel) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kFuse | kPeel) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kPeel) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kFuse | kPeel) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kPeel) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPeel) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kPeel) \
-    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kFuse | kPeel) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kPeel | kWaveRun) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kFuse | kPeel | kWaveRun) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kPeel | kWaveRun) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kFuse | kPeel | kWaveRun) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kPeel | kWaveRun) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPeel | kWaveRun) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kPeel | kWaveRun) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kFuse | kPeel | kWaveRun) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kPeel | kWaveRun) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kFuse | kPeel) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kFuse | kPeel | kWaveRun) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kPeel) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse | kPeel) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs | kPeel | kWaveRun) \
-    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse | kPeel | kWaveRun)
+// ---- the product instantiation list, derived from the launch policy --------
+// Every valid LaunchShape (gf_apply.hpp) is mapped through policy_variant at
+// compile time; the distinct (rows, U, flags) keys are the full-tile (MODE 0)
+// kernels of the product library.  A kernel nothing can launch is therefore
+// never compiled, and a shape's kernel always exists.  The tools build adds
+// its measurement variants (gf_apply_tools.hip).
+struct Key {
+    int rows = 0, u = 0, flags = 0;
+};
+constexpr int kMaxKeys = 256;
+struct KeyList {
+    Key k[kMaxKeys] = {};
+    int n = 0;
+};
 
-template <int R>
-hipError_t dispatch_full(const ApplyArgs& a, const Variant& v, int grid_cap, hipStream_t s) {
+constexpr LaunchShape shape_at(unsigned i) {
+    LaunchShape s;
+    s.decode = i & 1;
+    s.small_k = (i >> 1) & 1;
+    s.host_mapped = (i >> 2) & 1;
+    s.ptrs = (i >> 3) & 1;
+    s.segs = (i >> 4) & 1;
+    s.compact = (i >> 5) & 1;
+    s.sc1_ok = (i >> 6) & 1;
+    s.fused = (i >> 7) & 1;
+    s.rows = 1 + (i >> 8);
+    return s;
+}
+constexpr unsigned kShapes = 256 * kMaxRowsPerLaunch;
+
+constexpr KeyList product_keys() {
+    KeyList L;
+    for (unsigned i = 0; i < kShapes; ++i) {
+        const LaunchShape s = shape_at(i);
+        if (!shape_valid(s)) continue;
+        const Variant v = policy_variant(s);
+        const Key key{int(s.rows), v.u, variant_flags(v)};
+        bool seen = false;
+        for (int j = 0; j < L.n && !seen; ++j)
+            seen = L.k[j].rows == key.rows && L.k[j].u == key.u && L.k[j].flags == key.flags;
+        if (!seen) L.k[L.n++] = key;   // (overflow: not a constant expression -> compile error)
+    }
+    return L;
+}
+constexpr KeyList kProduct = product_keys();
+constexpr int kNumProduct = kProduct.n;
+static_assert(kNumProduct > 0 && kNumProduct < kMaxKeys, "product kernel list");
+
+using LaunchFn = hipError_t (*)(const ApplyArgs&, const Variant&, int, hipStream_t);
+template <size_t... I>
+constexpr std::array<LaunchFn, sizeof...(I)> product_fns(std::index_sequence<I...>) {
+    return {{&launch_one<kProduct.k[I].rows, kProduct.k[I].u, 0, kProduct.k[I].flags>...}};
+}
+constexpr std::array<LaunchFn, kNumProduct> kProductFns = product_fns(std::make_index_sequence<kNumProduct>{});
+
+// Launches served per kernel: [product list][MODE 1, 2, 3 x rows]
+std::atomic<uint64_t> g_launches[kNumProduct + 3 * kMaxRowsPerLaunch];
+
+int product_index(const Variant& v, unsigned rows) {
     const int f = variant_flags(v);
-#define SHMR_F(UU, FL) \
-    if (v.u == UU && f == (FL)) return launch_one<R, UU, 0, FL>(a, v, grid_cap, s);
-    SHMR_VARIANTS_PRODUCT(SHMR_F)
-#undef SHMR_F
+    for (int i = 0; i < kNumProduct; ++i)
+        if (kProduct.k[i].rows == int(rows) && kProduct.k[i].u == v.u && kProduct.k[i].flags == f) return i;
+    return -1;
+}
+
+hipError_t dispatch_full(const ApplyArgs& a, unsigned rows, const Variant& v, int grid_cap, hipStream_t s) {
+    const int i = product_index(v, rows);
+    if (i >= 0) {
+        g_launches[i].fetch_add(1, std::memory_order_relaxed);
+        return kProductFns[size_t(i)](a, v, grid_cap, s);
+    }
 #ifdef SHMR_EC_TOOLS
-    return launch_full_tools(a, R, v, grid_cap, s);
+    return launch_full_tools(a, rows, v, grid_cap, s);
 #else
     return hipErrorInvalidValue;
 #endif
 }
 
+// MODE 1 (partial tail tiles), 2 (byte-granular) and 3 (realigning, for a
+// device without the unaligned access mode): one kernel per row count.
 template <int R>
-hipError_t dispatch(const ApplyArgs& a, const Variant& v, int mode, int grid_cap, hipStream_t s) {
+hipError_t dispatch_mode(const ApplyArgs& a, const Variant& v, int mode, int grid_cap, hipStream_t s) {
+    g_launches[kNumProduct + (mode - 1) * kMaxRowsPerLaunch + (R - 1)].fetch_add(1, std::memory_order_relaxed);
     switch (mode) {
-        case 0: return dispatch_full<R>(a, v, grid_cap, s);
         case 1: return launch_one<R, 1, 1, 0>(a, v, grid_cap, s);
         case 3: return launch_one<R, 1, 3, kNtLoad | kNtStore | kDepth2>(a, v, grid_cap, s);
         default: return launch_one<R, 1, 2, 0>(a, v, grid_cap, s);
     }
 }
+constexpr int kModeFlags[3] = {0, 0, kNtLoad | kNtStore | kDepth2};
 
 }  // namespace
 
-bool variant_compiled(const Variant& v) {
-    const int f = variant_flags(v);
-#define SHMR_F(UU, FL) \
-    if (v.u == UU && f == (FL)) return true;
-    SHMR_VARIANTS_PRODUCT(SHMR_F)
-#undef SHMR_F
+bool variant_compiled(const Variant& v, unsigned rows) {
+    if (product_index(v, rows) >= 0) return true;
 #ifdef SHMR_EC_TOOLS
     return variant_compiled_tools(v);
 #else
     return false;
 #endif
+}
+
+size_t kernel_inventory(KernelInfo* out, size_t cap) {
+    const size_t n = size_t(kNumProduct) + 3 * kMaxRowsPerLaunch;
+    for (size_t i = 0; i < n && out && i < cap; ++i) {
+        KernelInfo& k = out[i];
+        if (i < size_t(kNumProduct)) {
+            k = KernelInfo{uint32_t(kProduct.k[i].rows), uint32_t(kProduct.k[i].u), 0u, uint32_t(kProduct.k[i].flags), 0};
+        } else {
+            const size_t j = i - size_t(kNumProduct);
+            k = KernelInfo{uint32_t(j % kMaxRowsPerLaunch + 1), 1u, uint32_t(j / kMaxRowsPerLaunch + 1),
+                           uint32_t(kModeFlags[j / kMaxRowsPerLaunch]), 0};
+        }
+        k.launches = g_launches[i].load(std::memory_order_relaxed);
+    }
+    return n;
 }
 
 namespace {
@@ -205,12 +201,14 @@ hipError_t probe_unaligned_vector(bool* ok, uint8_t* d_scratch, uint8_t* h_scrat
 
 hipError_t launch_apply(const ApplyArgs& a, unsigned rows, const Variant& v, int mode, int grid_cap,
                         hipStream_t stream) {
+    if (rows < 1 || rows > kMaxRowsPerLaunch) return hipErrorInvalidValue;
+    if (mode == 0) return dispatch_full(a, rows, v, grid_cap, stream);
+    if (mode < 1 || mode > 3) return hipErrorInvalidValue;
     switch (rows) {
-        case 1: return dispatch<1>(a, v, mode, grid_cap, stream);
-        case 2: return dispatch<2>(a, v, mode, grid_cap, stream);
-        case 3: return dispatch<3>(a, v, mode, grid_cap, stream);
-        case 4: return dispatch<4>(a, v, mode, grid_cap, stream);
-        default: return hipErrorInvalidValue;
+        case 1: return dispatch_mode<1>(a, v, mode, grid_cap, stream);
+        case 2: return dispatch_mode<2>(a, v, mode, grid_cap, stream);
+        case 3: return dispatch_mode<3>(a, v, mode, grid_cap, stream);
+        default: return dispatch_mode<4>(a, v, mode, grid_cap, stream);
     }
 }
 

@@ -512,7 +512,91 @@ __device__ __forceinline__ void store_run_aligned(uint8_t* p, const u32x4 (&v)[U
     X(4, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kPeel | kWaveRun) \
     X(4, kNtLoad | kNtStore | kDepth2 | kSegs | kPeel | kWaveRun) \
     X(1, kNtLoad | kSc1Store | kDepth2 | kSPre | kSegs) \
-    X(1, kNtLoad | kSc1Store | kDepth2 | kSPre | kSegs | kFuse)
+    X(1, kNtLoad | kSc1Store | kDepth2 | kSPre | kSegs | kFuse) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial | kPeel | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial | kPeel | kWaveRun)
+
+// The round-3 product list (every row count), so the tools build can still
+// A/B the r03 policy against the current one.
+#define SHMR_VARIANTS_R03(X) \
+    X(1, kNtLoad | kNtStore | kDepth2) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kWaveRun) \
+    X(1, kNtStore | kDepth2) \
+    X(2, kNtStore | kDepth2) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kWaveRun) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kFuse) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kWaveRun) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial | kWaveRun) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kPeel) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kPeel | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kSegs | kFuse | kPeel | kWaveRun) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kPeel | kWaveRun) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kFuse | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kPeel | kWaveRun) \
+    X(1, kNtStore | kDepth2 | kPtrs) \
+    X(2, kNtStore | kDepth2 | kPtrs) \
+    X(1, kNtStore | kDepth2 | kPtrs | kFuse) \
+    X(2, kNtStore | kDepth2 | kPtrs | kFuse) \
+    X(1, kNtStore | kDepth2 | kPtrs | kSegs) \
+    X(1, kNtStore | kDepth2 | kPtrs | kSegs | kFuse) \
+    X(2, kNtStore | kDepth2 | kPtrs | kSegs) \
+    X(2, kNtStore | kDepth2 | kPtrs | kSegs | kFuse) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kPtrs) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kPtrs | kWaveRun) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kPtrs | kPeel) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kFuse | kPtrs) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kPtrs | kWaveRun) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kPtrs) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPtrs) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial | kWaveRun | kPtrs) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial | kWaveRun | kPtrs) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kPtrs | kPeel) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kFuse | kPtrs | kPeel) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kPtrs | kPeel | kWaveRun) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kFuse | kPtrs | kPeel | kWaveRun) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kPtrs | kPeel) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPtrs | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kPtrs | kPeel | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPtrs | kPeel | kWaveRun) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kPtrs | kPeel) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kFuse | kPtrs | kPeel) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kPtrs | kPeel | kWaveRun) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kFuse | kPtrs | kPeel | kWaveRun) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kPtrs | kPeel) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kFuse | kPtrs | kPeel) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kPtrs | kPeel | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kFuse | kPtrs | kPeel | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kPtrs | kPeel | kWaveRun) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kPeel) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kPeel) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kFuse | kPeel) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kPeel) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kFuse | kPeel) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kPeel) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPeel) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kPeel) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kFuse | kPeel) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kPeel | kWaveRun) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kFuse | kPeel | kWaveRun) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kPeel | kWaveRun) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kEarly | kSegs | kFuse | kPeel | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kPeel | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPeel | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kPeel | kWaveRun) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSegs | kFuse | kPeel | kWaveRun) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kPeel | kWaveRun) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kFuse | kPeel) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kFuse | kPeel | kWaveRun) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kPeel) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse | kPeel) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs | kPeel | kWaveRun) \
+    X(2, kNtLoad | kSc1Store | kDepth2 | kSegs | kFuse | kPeel | kWaveRun)
 
 template <int R>
 hipError_t dispatch_tools(const ApplyArgs& a, const Variant& v, int grid_cap, hipStream_t s) {
@@ -520,6 +604,7 @@ hipError_t dispatch_tools(const ApplyArgs& a, const Variant& v, int grid_cap, hi
 #define SHMR_F(UU, FL) \
     if (v.u == UU && f == (FL)) return launch_one<R, UU, 0, FL>(a, v, grid_cap, s);
     SHMR_VARIANTS_TOOLS(SHMR_F)
+    SHMR_VARIANTS_R03(SHMR_F)
 #undef SHMR_F
     return hipErrorInvalidValue;
 }
@@ -541,6 +626,7 @@ bool variant_compiled_tools(const Variant& v) {
 #define SHMR_F(UU, FL) \
     if (v.u == UU && f == (FL)) return true;
     SHMR_VARIANTS_TOOLS(SHMR_F)
+    SHMR_VARIANTS_R03(SHMR_F)
 #undef SHMR_F
     return false;
 }

@@ -24,63 +24,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // mode; checked on the product code object by tests/test_isa.py).
 typedef u32x4 u32x4_u __attribute__((aligned(1)));
 
-// Kernel variant flags (template parameter F).  The values are part of the
-// kernels' mangled names: never renumber.
-constexpr int kNtLoad = 1;       // nontemporal loads
-constexpr int kNtStore = 2;      // nontemporal stores
-constexpr int kOcc8 = 8;         // ask for 8 waves / SIMD (<= 64 VGPRs)
-constexpr int kDiagXor = 16;     // tools: XOR without GF multiply (wrong results)
-constexpr int kTh128 = 32;       // 128-lane workgroups (default 256)
-constexpr int kTh512 = 64;       // 512-lane workgroups
-constexpr int kDepth5 = 128;     // 4 shards of loads in flight (default 2)
-constexpr int kDepth9 = 256;     // 8 shards of loads in flight
-constexpr int kDepth2 = 512;     // 1 shard of loads in flight
-constexpr int kDepth1 = 1024;    // no look-ahead (load, wait, multiply)
-constexpr int kEarly = 1 << 16;  // first data loads issued before the plan's LDS staging completes
-constexpr int kSPre = 1 << 17;   // tools: tables + offsets by scalar loads one shard ahead, no LDS
-constexpr int kFuse = 1 << 18;   // leading partial tiles (ApplyArgs::lead_tails) in a MODE 0 launch; a
-                                 // separate instantiation: the bounds-checked path costs 4-7 VGPRs
-// Launch forms a full-tile (MODE 0) kernel supports only when compiled with
-// the flag, so the lean encode kernel carries none of their code (measured:
-// the runtime checks alone cost the RS(8,3) encode 1.3 %).  The tail and
-// byte-granular kernels (MODE 1, 2) always support both.
-constexpr int kPtrs = 1 << 19;   // shard-pointer tables (ApplyArgs::shard_ptrs)
-constexpr int kSegs = 1 << 20;   // segment launches (ApplyArgs::segs)
-constexpr int kGlds = 1 << 21;   // tools: input ring in LDS filled by LDS-DMA
-// GF math one dword at a time: a scheduling fence after each of a lane's four
-// dwords keeps the scheduler from computing every perm of a 16-byte chunk
-// before the first XOR (48 live temporaries at R = 4), trading ILP inside a
-// wave for registers (more waves per SIMD).
-constexpr int kSerial = 1 << 22;
-// Stores with the sc1 cache policy instead of nontemporal (compact rebuilt-
-// shard outputs: a separate, densely written array; raw buffer stores,
-// store16_row)
-constexpr int kSc1Store = 1 << 23;
-// tools: misaligned shards by aligned loads realigned across lanes (DPP)
-constexpr int kRealign = 1 << 24;
-// tools: the depth-2 ring with its tail peeled -- no look-ahead load past the
-// last shard (the default ring re-reads shard k-1 there: one extra wave load
-// per shard run, an L2 hit) and still no load behind a branch inside the loop
-constexpr int kPeel = 1 << 25;
-// tools: U > 1 slots of a lane in wave-contiguous runs (chunk (w * U + u) *
-// 64 + lane: each wave covers one contiguous U KiB run) instead of
-// workgroup-strided slots (u * TH + tid) -- fewer partial cache lines at run
-// edges when the shards are off alignment
-constexpr int kWaveRun = 1 << 26;
-// tools: full tiles store misaligned output rows with ALIGNED 16-byte stores
-// (each lane's chunk realigned with the previous lane's by a DPP wavefront
-// shift; the run's two partial chunks by masked narrow stores)
-constexpr int kStAlign = 1 << 27;
-// tools: XCD-grouped tile order for one-workgroup-per-tile grids.  Dispatch
-// puts workgroup w on XCD w % 8; with w -> tile (w % 8) * q + w / 8 (q = ntiles
-// / 8) each XCD walks one contiguous eighth of the tiles in order, so
-// neighbouring column tiles of a block meet in the same L2 -- the cache lines
-// a misaligned shard's tile boundaries share are fetched (and partial-line
-// stores merged) once instead of on two XCDs
-constexpr int kXcd = 1 << 28;
-// Bits 12-15: occupancy target in waves per SIMD (0 = compiler's choice);
-// the register allocator must then fit 512 / target VGPRs.
-constexpr int kOccShift = 12;
+// Variant flags (kNtLoad ... kXcd, kOccShift): gf_apply.hpp.
 
 template <int MODE, int F>
 constexpr bool has_ptrs() {
@@ -526,10 +470,10 @@ __device__ __forceinline__ void stage_plan(const ApplyArgs& a, const uint8_t* pl
         const uint32_t t = e / R, r = e - t * R;
         s_tab[i] = ptab[(size_t(t) * a.m + a.row0 + r) * 2 + half];
     }
-    if (PTRS && a.shard_ptrs) {   // absolute shard addresses (in/out bases are 0)
+    if (PTRS && a.shard_ptrs) {   // absolute shard addresses in plan order (in/out bases are 0)
         const uint64_t* bp = a.shard_ptrs + blk * a.total;
-        for (uint32_t t = threadIdx.x; t < k; t += TH) s_in_off[t] = bp[in_idx[t]];
-        for (uint32_t r = threadIdx.x; r < uint32_t(R); r += TH) s_out_off[r] = bp[out_idx[a.row0 + r]];
+        for (uint32_t t = threadIdx.x; t < k; t += TH) s_in_off[t] = bp[t];
+        for (uint32_t r = threadIdx.x; r < uint32_t(R); r += TH) s_out_off[r] = bp[k + a.row0 + r];
     } else {
         for (uint32_t t = threadIdx.x; t < k; t += TH) s_in_off[t] = uint64_t(in_idx[t]) * a.in_spitch;
         for (uint32_t r = threadIdx.x; r < uint32_t(R); r += TH)
@@ -579,14 +523,15 @@ __device__ __forceinline__ void stage_issue(const ApplyArgs& a, const uint8_t* p
     const uint32_t e = ic >> 1, half = ic & 1;
     const uint32_t t = e / R, r = e - t * R;
     s.tab = ((const gu32x4*)(uintptr_t)(plan + a.tab_off))[(size_t(t) * a.m + a.row0 + r) * 2 + half];
-    const gu16* in_idx = (const gu16*)(uintptr_t)(plan + 8);
-    const uint32_t ti = in_idx[i < k ? i : k - 1];
-    const uint32_t to = in_idx[k + a.row0 + (i < uint32_t(R) ? i : R - 1)];
-    if constexpr (PTRS) {
+    const uint32_t ii = i < k ? i : k - 1, ir = a.row0 + (i < uint32_t(R) ? i : R - 1);
+    if constexpr (PTRS) {   // the block's row is in plan order: no index load in front
         const gu64* bp = (const gu64*)(uintptr_t)(a.shard_ptrs + blk * a.total);
-        s.in_off = bp[ti];
-        s.out_off = bp[to];
+        s.in_off = bp[ii];
+        s.out_off = bp[k + ir];
     } else {
+        const gu16* in_idx = (const gu16*)(uintptr_t)(plan + 8);
+        const uint32_t ti = in_idx[ii];
+        const uint32_t to = in_idx[k + ir];
         s.in_off = uint64_t(ti) * a.in_spitch;
         s.out_off = uint64_t(to - a.out_bias) * a.out_spitch;
     }
@@ -612,7 +557,7 @@ __device__ __forceinline__ void stage_commit(const ApplyArgs& a, const uint8_t* 
         s_tab[j] = ptab[(size_t(t) * a.m + a.row0 + r) * 2 + half];
     }
     for (uint32_t t = i + TH; t < k; t += TH)
-        s_in_off[t] = PTRS ? a.shard_ptrs[blk * a.total + in_idx[t]] : uint64_t(in_idx[t]) * a.in_spitch;
+        s_in_off[t] = PTRS ? a.shard_ptrs[blk * a.total + t] : uint64_t(in_idx[t]) * a.in_spitch;
     c.s_tab = s_tab;
     c.s_in_off = s_in_off;
     c.s_out_off = s_out_off;
@@ -624,7 +569,7 @@ __device__ __forceinline__ void early_tile(const ApplyArgs& a, const uint8_t* pl
     constexpr int TH = threads_of<F>();
     constexpr int NB = depth_of<F>();
     // shard-pointer tables (device memory): the first loads' addresses come
-    // from scalar loads of the block's table row, like the plan's in_idx
+    // from scalar loads of the block's table row (plan order: entry t is input t)
     constexpr bool PTRS = (F & kPtrs) != 0;
     const uint32_t k = a.k;
     const uint64_t len = a.len;
@@ -639,8 +584,7 @@ __device__ __forceinline__ void early_tile(const ApplyArgs& a, const uint8_t* pl
         const uint32_t t = uint32_t(i) < k ? uint32_t(i) : k - 1;
         const uint8_t* base;
         if constexpr (PTRS)
-            base = reinterpret_cast<const uint8_t*>(
-                uintptr_t(as_const<cu64>(a.shard_ptrs + blk * a.total)[plan_u16(in_idx, t)]));
+            base = reinterpret_cast<const uint8_t*>(uintptr_t(as_const<cu64>(a.shard_ptrs + blk * a.total)[t]));
         else
             base = ib + uint64_t(plan_u16(in_idx, t)) * a.in_spitch;
 #pragma unroll
@@ -852,20 +796,16 @@ hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStr
     }
     if (grid > a.ntiles) grid = a.ntiles;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL(kern, dim3(uint32_t(grid)), dim3(threads_of<F>()), lds, stream, a);
+    // Launched by name, never through the function-pointer variable `kern`: in
+    // host code a kernel's "address" is its kernel handle (a data object), and
+    // clang's -fsanitize=function (part of -fsanitize=undefined) instruments an
+    // indirect kernel launch with a read of the 8 bytes in front of it --
+    // out of bounds of the handle, which the optimizer then treats as
+    // unreachable: the launch was deleted, leaving only
+    // __hipPushCallConfiguration (no kernel ran, no sanitizer report; DESIGN.md
+    // §3).  tests/test_isa.py checks every instantiation has its launch.
+    hipLaunchKernelGGL((gf_apply_kernel<R, U, MODE, F>), dim3(uint32_t(grid)), dim3(threads_of<F>()), lds, stream, a);
     return hipGetLastError();
-}
-
-// Template flags of a variant (the tools build maps every knob).
-inline int variant_flags(const Variant& v) {
-    return (v.nt_load ? kNtLoad : 0) | (v.nt_store ? kNtStore : 0) | (v.occ8 ? kOcc8 : 0) |
-           (v.diag ? kDiagXor : 0) | (v.threads == 128 ? kTh128 : 0) | (v.threads == 512 ? kTh512 : 0) |
-           (v.depth == 5 ? kDepth5 : 0) | (v.depth == 9 ? kDepth9 : 0) | (v.depth == 2 ? kDepth2 : 0) |
-           (v.depth == 1 ? kDepth1 : 0) | ((v.occ & 15) << kOccShift) | (v.early ? kEarly : 0) |
-           (v.spre ? kSPre : 0) | (v.fuse_tail ? kFuse : 0) | (v.ptrs ? kPtrs : 0) | (v.segs ? kSegs : 0) |
-           (v.glds ? kGlds : 0) | (v.serial ? kSerial : 0) | (v.sc1_store ? kSc1Store : 0) |
-           (v.realign ? kRealign : 0) | (v.peel ? kPeel : 0) | (v.wave_run ? kWaveRun : 0) |
-           (v.st_align ? kStAlign : 0) | (v.xcd ? kXcd : 0);
 }
 
 }  // namespace

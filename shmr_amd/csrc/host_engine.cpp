@@ -316,9 +316,12 @@ int run_mapped(const HostJob& job, const std::vector<uint64_t>& dptrs, bool alig
             int slot = -1;
             rc = ring->acquire(&hslot, &dslot, &slot);
             if (rc) break;
+            // rows in plan order (kern::ApplyArgs::shard_ptrs): reconstructs permuted per block
             uint64_t* tab = reinterpret_cast<uint64_t*>(hslot);
             for (size_t j = 0; j < n; ++j)
-                std::memcpy(tab + j * t, dptrs.data() + mine[c0 + j] * t, t * sizeof(uint64_t));
+                permute_ptr_rows(dptrs.data() + mine[c0 + j] * t,
+                                 job.op == kEncode ? nullptr : job.present + mine[c0 + j] * t, 1, c.k(), t,
+                                 job.data_only, tab + j * t);
             // small launches (few 4 KiB tiles) read the table from the pinned slot
             // itself: no H2D copy in front of the kernel.  Larger ones upload it --
             // every workgroup reads its block's table, and across PCIe that costs

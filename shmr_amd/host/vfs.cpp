@@ -623,7 +623,7 @@ Status VirtualBlock::write(uint64_t pos, const uint8_t* buf, size_t len, size_t*
 }
 
 // block.rs:373-452
-Status VirtualBlock::sync_data(bool force, int device) const {
+Status VirtualBlock::sync_data(bool force, int device, PhaseTimes* times) const {
     if (!force && !st_->should_flush.load()) return std::nullopt;
     if (!st_->shard_loaded.load()) {
         if (auto e = open_handles()) return e;
@@ -648,15 +648,19 @@ Status VirtualBlock::sync_data(bool force, int device) const {
         const size_t n = size_t(topology.data) + topology.parity;
         std::vector<uint8_t*> ptrs(n);
         shard_ptrs(buffer, n, S, ptrs.data());
+        const double tc = times ? now_s() : 0;
         es = r->encode_in_place(ptrs.data(), n, S);   // block.rs:427 (.unwrap() in the reference)
+        if (times) times->codec_s += now_s() - tc;
         if (!es.ok()) {
             restore_tail(buffer, topology, S, tail);
             return ec_error(es.code);
         }
+        const double tw = times ? now_s() : 0;
         parallel_for(std::min(n, nh), 16, [&](size_t i) {   // block.rs:436-439, in parallel
             res[i] = st_->ensure_fd(i, *cfg_);
             if (!res[i]) res[i] = write_path(st_->handles[i].second, ptrs[i], S, opt_.fsync_shards);
         });
+        if (times) times->io_s += now_s() - tw;
         restore_tail(buffer, topology, S, tail);
     } else {
         const size_t copies = topology.kind == BlockTopology::Single ? 1 : std::min<size_t>(topology.n, nh);
@@ -692,7 +696,7 @@ Status VirtualBlock::open_handles() const {
 }
 
 // block.rs:496-584
-Status VirtualBlock::load_block(bool* reconstructed, int device) const {
+Status VirtualBlock::load_block(bool* reconstructed, int device, PhaseTimes* times) const {
     if (reconstructed) *reconstructed = false;
     if (!st_->shard_loaded.load()) {
         if (auto e = open_handles()) return e;
@@ -736,6 +740,7 @@ Status VirtualBlock::load_block(bool* reconstructed, int device) const {
                 odd[i] = o;
             }
         };
+        const double tr = times ? now_s() : 0;
         parallel_for(n, 16, [&](size_t i) {
             if (plan[i] == kRead) read_one(i);
             else if (plan[i] == kPresentUnread) present[i] = 1;
@@ -751,10 +756,13 @@ Status VirtualBlock::load_block(bool* reconstructed, int device) const {
                     }
                 });
         }
+        if (times) times->io_s += now_s() - tr;
         bool missing = false;
         for (size_t i = 0; i < n; ++i) missing |= !present[i] || odd[i];
         if (missing) {
+            const double tc = times ? now_s() : 0;
             es = r->reconstruct_in_place(ptrs.data(), present.data(), n, S, false);   // block.rs:560 (unwrap)
+            if (times) times->codec_s += now_s() - tc;
             if (!es.ok()) return ec_error(es.code);
             if (reconstructed) *reconstructed = true;
         }
@@ -1056,11 +1064,19 @@ Status VirtualFile::sync_data(bool force) {
         // one flush task per block (mod.rs:93-96's par_iter), blocks round-robin over the GPUs
         const size_t nd = std::max<size_t>(1, devices.size());
         std::atomic<size_t> coded{0};
+        std::mutex tmu;
         parallel_for(blocks.size(), 16, [&](size_t i) {
             const VirtualBlock& b = blocks[i];
             const bool dirty = force || b.st_->should_flush.load();
-            results[i] = b.sync_data(force, devices.empty() ? 0 : devices[i % nd]);
+            const double ts = now_s();
+            PhaseTimes pt;
+            results[i] = b.sync_data(force, devices.empty() ? 0 : devices[i % nd], &pt);
             if (!results[i] && dirty && b.topology.kind == BlockTopology::Erasure) ++coded;
+            std::lock_guard<std::mutex> lock(tmu);
+            last_sync.task_write_s += pt.io_s;
+            last_sync.task_codec_s += pt.codec_s;
+            last_sync.task_total_s += now_s() - ts;
+            ++last_sync.tasks;
         });
         last_sync.blocks = coded.load();
         last_sync.total_s = now_s() - t0;
@@ -1205,16 +1221,28 @@ Status VirtualFile::load_blocks(const std::vector<size_t>& block_indices,
         }
         const size_t nd = std::max<size_t>(1, devices.size());
         std::atomic<size_t> rebuilt{0};
+        std::mutex tmu;
         parallel_for(todo.size(), 16, [&](size_t q) {
             const size_t i = todo[q];
             const VirtualBlock& b = blocks[i];
             bool rec = false;
-            results[i] = b.load_block(&rec, devices.empty() ? 0 : devices[i % nd]);
+            const double ts = now_s();
+            PhaseTimes pt;
+            results[i] = b.load_block(&rec, devices.empty() ? 0 : devices[i % nd], &pt);
             if (rec) ++rebuilt;
+            double copy_s = 0;
             if (!results[i] && on_batch && b.topology.kind == BlockTopology::Erasure) {
                 std::lock_guard<std::mutex> lock(b.st_->buf_mu);   // on_batch reads the buffer unlocked
+                const double tc = now_s();
                 on_batch(std::vector<size_t>{i});
+                copy_s = now_s() - tc;
             }
+            std::lock_guard<std::mutex> lock(tmu);
+            last_load.task_read_s += pt.io_s;
+            last_load.task_codec_s += pt.codec_s;
+            last_load.task_copy_s += copy_s;
+            last_load.task_total_s += now_s() - ts;
+            ++last_load.tasks;
         });
         last_load.blocks = rebuilt.load();
         last_load.total_s = now_s() - t0;

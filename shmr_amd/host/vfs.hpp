@@ -144,6 +144,22 @@ struct IoStats {
     double io_s = 0;        // shard-file reads or writes (+ fsync), busy time
     double total_s = 0;     // codec + I/O phase, wall
     size_t blocks = 0;      // Erasure blocks coded
+    // Per-block task mode (mapped Block-Cache buffers with the auto batch: one
+    // task per block on the worker pool, VirtualBlock::sync_data / load_block
+    // each): thread time summed over the tasks.  Tasks run concurrently, so the
+    // sums exceed total_s; their ratios say where a task's time goes.
+    double task_read_s = 0;    // load: shard-file reads into the block's slots
+    double task_write_s = 0;   // flush: shard-file writes (+ fsync)
+    double task_codec_s = 0;   // the block's zero-copy GPU call, PCIe included
+    double task_copy_s = 0;    // VirtualFile::read: copy-out into the caller's buffer
+    double task_total_s = 0;   // whole tasks (the rest: locks, handles, buffer set-up)
+    size_t tasks = 0;
+};
+
+// Phase times of one VirtualBlock::sync_data / load_block call (seconds).
+struct PhaseTimes {
+    double io_s = 0;      // shard-file reads or writes
+    double codec_s = 0;   // the GPU encode / reconstruct call
 };
 
 // VirtualBlock (src/vfs/block.rs:119-634).  Copies share state, like the
@@ -168,7 +184,7 @@ public:
     Status read(uint64_t pos, uint8_t* buf, size_t len, size_t* nread) const;
     Status write(uint64_t pos, const uint8_t* buf, size_t len, size_t* nwritten) const;
     Status sync_data(bool force) const { return sync_data(force, 0); }
-    Status sync_data(bool force, int device) const;   // Erasure encode on that GPU
+    Status sync_data(bool force, int device, PhaseTimes* times = nullptr) const;   // Erasure encode on that GPU
     Status drop_buffer() const;
     Status drop_handles() const;
 
@@ -184,7 +200,7 @@ private:
     Status open_handles() const;
     Status load_block() const { return load_block(nullptr, 0); }
     // *reconstructed (if set): an Erasure block needed a reconstruct (on `device`)
-    Status load_block(bool* reconstructed, int device) const;
+    Status load_block(bool* reconstructed, int device, PhaseTimes* times = nullptr) const;
     size_t shard_size() const;   // S of an Erasure block (mod.rs:16-18)
     std::shared_ptr<State> st_;
     std::shared_ptr<const ShmrFsConfig> cfg_;

@@ -106,6 +106,27 @@ Result run_once(const std::shared_ptr<const ShmrFsConfig>& cfg, uint64_t ino, co
     return r;
 }
 
+// Per-block task mode: where each task's thread time went (ms per block of
+// the best rep, per phase) and the phases' share of the task time.
+std::string tasks_json(const Result& r) {
+    if (!r.load.tasks && !r.sync.tasks) return "";
+    char t[640];
+    auto per = [](double s, size_t n) { return n ? s / double(n) * 1e3 : 0.0; };
+    std::snprintf(t, sizeof t,
+                  "\"per_block_tasks\": {\"unit\": \"ms of thread time per block\", "
+                  "\"sync\": {\"tasks\": %zu, \"encode_call\": %.3f, \"shard_writes\": %.3f, \"other\": %.3f, "
+                  "\"task\": %.3f}, "
+                  "\"read\": {\"tasks\": %zu, \"shard_reads\": %.3f, \"reconstruct_call\": %.3f, \"copy_out\": %.3f, "
+                  "\"other\": %.3f, \"task\": %.3f}, \"read_wall_ms\": %.2f, \"sync_wall_ms\": %.2f}, ",
+                  r.sync.tasks, per(r.sync.task_codec_s, r.sync.tasks), per(r.sync.task_write_s, r.sync.tasks),
+                  per(r.sync.task_total_s - r.sync.task_codec_s - r.sync.task_write_s, r.sync.tasks),
+                  per(r.sync.task_total_s, r.sync.tasks), r.load.tasks, per(r.load.task_read_s, r.load.tasks),
+                  per(r.load.task_codec_s, r.load.tasks), per(r.load.task_copy_s, r.load.tasks),
+                  per(r.load.task_total_s - r.load.task_read_s - r.load.task_codec_s - r.load.task_copy_s, r.load.tasks),
+                  per(r.load.task_total_s, r.load.tasks), r.read_s * 1e3, r.sync_s * 1e3);
+    return t;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -185,14 +206,14 @@ int main(int argc, char** argv) {
             "\"sync_pipeline_GiBps\": %s, \"per_block_sync_GiBps\": %s, \"read_with_erasure_GiBps\": %s, "
             "\"read_reconstruct_GiBps\": %s, \"read_shard_io_GiBps\": %s, \"read_pipeline_GiBps\": %s, "
             "\"reconstructed_blocks\": %zu, \"sync_prepare_ms\": %.2f, \"read_prepare_ms\": %.2f, "
-            "\"read_needed_shards\": %s, \"shard_reads_per_block\": %.2f, \"verified\": true}\n",
+            "\"read_needed_shards\": %s, \"shard_reads_per_block\": %.2f, %s\"verified\": true}\n",
             pinned ? "mapped Block Cache (shmr_ec_host_alloc)" : "pageable", (unsigned long long)(zc1 - zc0),
             (unsigned long long)(st1 - st0), batch_name.c_str(), (unsigned long long)file_mib,
             (unsigned long long)block_mib, int(do_fsync), reps, rate(best.write_s).c_str(), rate(best.sync_s).c_str(),
             rate(best.sync.codec_s).c_str(), rate(best.sync.io_s).c_str(), rate(best.sync.total_s).c_str(),
             rate(best.per_block_sync_s).c_str(), rate(best.read_s).c_str(), rate(best.load.codec_s).c_str(),
             rate(best.load.io_s).c_str(), rate(best.load.total_s).c_str(), best.load.blocks, best.sync.prepare_s * 1e3,
-            best.load.prepare_s * 1e3, needed ? "true" : "false", best.shard_reads_per_block);
+            best.load.prepare_s * 1e3, needed ? "true" : "false", best.shard_reads_per_block, tasks_json(best).c_str());
         std::fflush(stdout);
     }
     return 0;

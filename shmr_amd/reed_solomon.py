@@ -17,10 +17,11 @@ from typing import List, MutableSequence, Optional, Sequence
 
 import numpy as np
 
+from . import _native
 from ._native import _u8p, lib
 
 __all__ = ["Error", "ReedSolomon", "calculate_shard_size", "device_count", "set_tuning", "get_tuning", "describe_variant",
-           "PinnedBuffer", "host_register", "host_unregister", "path_stats", "device_init"]
+           "PinnedBuffer", "host_register", "host_unregister", "path_stats", "device_init", "kernel_inventory", "capture_reserve"]
 
 
 class Error(Exception):
@@ -64,6 +65,19 @@ def describe_variant(decode, data_shards: int, rows: int) -> str:
     buf = ctypes.create_string_buffer(256)
     _check(lib().shmr_ec_describe_variant(int(decode), data_shards, rows, buf, 256))
     return buf.value.decode()
+
+
+def kernel_inventory(flavour: Optional[str] = None) -> list:
+    """Every gf_apply kernel instantiation compiled into the library, with the
+    launches each has served in this process (shmr_ec_kernel_inventory): dicts
+    with rows, chunks, mode (0 full tiles, 1 partial tail, 2 byte-granular,
+    3 realigning) and flags (the kernel's template flags)."""
+    L = _native._load(flavour) if flavour else lib()
+    n = L.shmr_ec_kernel_inventory(None, 0)
+    arr = (_native.KernelInfo * n)()
+    L.shmr_ec_kernel_inventory(ctypes.cast(arr, ctypes.c_void_p), n)
+    return [{"rows": e.rows, "chunks": e.chunks, "mode": e.mode, "flags": e.flags, "launches": e.launches}
+            for e in arr]
 
 
 def _writable_u8(buf) -> np.ndarray:
@@ -534,7 +548,7 @@ def path_stats():
 
 
 DEVICE_COUNTERS = ("blocks_encoded", "blocks_reconstructed", "launches", "plan_images", "upload_rings",
-                   "staging_streams", "blocking_calls", "ptr_table_hits")
+                   "staging_streams", "blocking_calls", "ptr_table_hits", "capture_tables", "capture_released")
 
 
 def device_init(device: int = 0) -> None:
@@ -542,6 +556,13 @@ def device_init(device: int = 0) -> None:
     device-resident entry points make no blocking HIP call and can be
     captured into a graph."""
     _check(lib().shmr_ec_device_init(int(device)))
+
+
+def capture_reserve(bytes_: int, device: int = 0) -> None:
+    """shmr_ec_capture_reserve: make sure one free range of ``bytes_`` exists in
+    the device's capture reserve (the tables of captured calls; a capture never
+    grows it).  Blocking; call it before the capture."""
+    _check(lib().shmr_ec_capture_reserve(int(device), int(bytes_)))
 
 
 def device_stats(device: int) -> dict:

@@ -234,12 +234,17 @@ def test_tuning_api():
                          ("decode.depth", -2), ("occ8", 0), ("uvec", -2)):
         shmr_amd.set_tuning(**{key: default})
     for key, value in (("encode.chunks", 2), ("diag", 1), ("decode.diag", 1), ("depth", 3), ("grid", 0),
-                       ("threads", 512), ("spre", 1), ("occ8", 1), ("uvec", 0), ("uvec", 1)):
+                       ("threads", 512), ("spre", 1), ("occ8", 1), ("uvec", 1)):
         with pytest.raises(shmr_amd.Error) as e:
             shmr_amd.set_tuning(**{key: value})
         assert e.value.name == "InvalidArgument", key
     with pytest.raises(shmr_amd.Error):
         shmr_amd.set_tuning(no_such_knob=1)
+    # uvec=0 (the realigning kernels a device without the unaligned access mode
+    # runs: exact results) is a product knob; uvec=1 stays tools-only
+    shmr_amd.set_tuning(uvec=0)
+    assert shmr_amd.get_tuning("uvec") == 0
+    shmr_amd.set_tuning(uvec=-2)
     assert "diag=0" in shmr_amd.describe_variant(False, 8, 3)
     # the measured policy: 4 output rows -> 2 chunks/lane; NT loads and stores; ring depth 2
     assert "chunks=2" in shmr_amd.describe_variant(False, 10, 4)

@@ -167,3 +167,83 @@ def test_init_refused_inside_capture(gpu):
             assert np.array_equal(parity.cpu().numpy(), want)
         finally:
             shmr_amd.set_tuning(alias_devices=0)
+
+
+def _ptr_table(base, B, t, S):
+    """ctypes table of B x t device pointers into one buffer (shard i of block
+    b at base + (b * t + i) * S)."""
+    import ctypes
+    from shmr_amd.reed_solomon import _u8p
+    addrs = (np.uint64(base) + np.arange(B * t, dtype=np.uint64) * np.uint64(S)).astype(np.uint64)
+    return addrs, addrs.ctypes.data_as(ctypes.POINTER(_u8p))
+
+
+def _wait_released(dev, want, timeout=10.0):
+    import time
+    t0 = time.time()
+    while shmr_amd.device_stats(dev)["capture_released"] < want and time.time() - t0 < timeout:
+        time.sleep(0.01)
+    return shmr_amd.device_stats(dev)["capture_released"]
+
+
+def test_capture_reserve_reused_across_graphs_and_large_capture(gpu):
+    """Captured calls take their tables from the capture reserve and give them
+    back when the graph is destroyed: 120 capture / replay / destroy cycles of a
+    48 KiB pointer table run in the 4 MiB reserve (without the release they
+    would exhaust it after ~85).  A capture larger than the reserve fails with
+    OUT_OF_MEMORY and nothing enqueued; after shmr_ec_capture_reserve it
+    succeeds and replays bit-exact."""
+    import ctypes
+    import gc
+    import torch
+    shmr_amd.device_init(0)
+    stream = torch.cuda.Stream()
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    # repeated captures (RS(4,2), 1000 blocks of 256-byte shards)
+    k, p, S, B = 4, 2, 256, 1000
+    t = k + p
+    rs = shmr_amd.ReedSolomon(k, p)
+    buf = torch.randint(0, 256, (B * t * S,), dtype=torch.uint8, device=gpu)
+    addrs, tab = _ptr_table(buf.data_ptr(), B, t, S)
+    st0 = shmr_amd.device_stats(0)
+    for cycle in range(120):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=stream):
+            rc = rs._L.shmr_ec_encode_ptrs_dev(rs._h, tab, B, S, 0, sp)
+        assert rc == 0, (cycle, shmr_amd.Error(rc).name)
+        if cycle % 40 == 0:
+            buf.view(B, t, S)[:, k:] = 0
+            g.replay()
+            torch.cuda.synchronize()
+            h = buf.view(B, t, S).cpu().numpy()
+            assert np.array_equal(h[:, k:], _oracle_parity(k, p, h[:, :k])), cycle
+        del g
+        gc.collect()
+        torch.cuda.synchronize()
+    st1 = shmr_amd.device_stats(0)
+    assert st1["capture_tables"] - st0["capture_tables"] == 120
+    assert _wait_released(0, st0["capture_released"] + 110) >= st0["capture_released"] + 110
+    # a capture larger than the reserve: RS(10,4), 40,000 blocks = 4.48 MB of pointers
+    k, p, S, B = 10, 4, 256, 40000
+    t = k + p
+    rs = shmr_amd.ReedSolomon(k, p)
+    big = torch.randint(0, 256, (B * t * S,), dtype=torch.uint8, device=gpu)
+    addrs, tab = _ptr_table(big.data_ptr(), B, t, S)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=stream):
+        rc = rs._L.shmr_ec_encode_ptrs_dev(rs._h, tab, B, S, 0, sp)
+    assert shmr_amd.Error(rc).name == "OutOfMemory"
+    del g
+    shmr_amd.capture_reserve(B * t * 8, 0)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=stream):
+        rc = rs._L.shmr_ec_encode_ptrs_dev(rs._h, tab, B, S, 0, sp)
+    assert rc == 0, shmr_amd.Error(rc).name
+    big.view(B, t, S)[:, k:] = 0
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    h = big.view(B, t, S).cpu().numpy()
+    assert np.array_equal(h[:, k:], _oracle_parity(k, p, h[:, :k]))
+    del g
+    gc.collect()

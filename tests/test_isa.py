@@ -104,3 +104,82 @@ def test_misaligned_path_kernels_exist(product_kernels):
     for R in (1, 2, 3, 4):
         assert any(k[0] == R and k[2] == 3 for k in kern), R
         assert any(k[0] == R and k[2] == 2 for k in kern), R
+
+
+def test_inventory_is_the_code_object(product_kernels):
+    """shmr_ec_kernel_inventory (what the library can dispatch, derived from the
+    launch policy at compile time) lists exactly the gf_apply kernels of the
+    product code object -- nothing compiled that the policy cannot select."""
+    import shmr_amd
+    inv = {(e["rows"], e["chunks"], e["mode"], e["flags"]) for e in shmr_amd.kernel_inventory()}
+    assert len(inv) == len(shmr_amd.kernel_inventory())
+    assert set(_apply_kernels(product_kernels)) == inv
+    # modes 1-3: one kernel per row count
+    for mode in (1, 2, 3):
+        assert sorted(r for r, u, m, f in inv if m == mode) == [1, 2, 3, 4]
+    full = [key for key in inv if key[2] == 0]
+    assert all(u == (2 if r == 4 else 1) for r, u, m, f in full), "U = 2 exactly for 4-row launches"
+
+
+def _host_symbols(path):
+    out = subprocess.check_output(["nm", path], text=True)
+    stubs, handles = {}, {}
+    for line in out.splitlines():
+        parts = line.split()
+        if len(parts) != 3 or "gf_apply_kernel" not in parts[2]:
+            continue
+        addr, kind, name = int(parts[0], 16), parts[1], parts[2]
+        m = re.search(r"gf_apply_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E", name)
+        key = tuple(int(x) for x in m.groups())
+        (stubs if "__device_stub__" in name else handles)[key] = (addr, kind)
+    return stubs, handles
+
+
+@pytest.mark.parametrize("flavour", ["product", "tools"])
+def test_kernel_stubs_and_handles_are_distinct(flavour):
+    """Every kernel instantiation has its own host launch stub and its own
+    kernel handle (the address hipLaunchKernel passes and
+    __hipRegisterFunction binds).  Two instantiations sharing either would make
+    one launch run a sibling kernel -- the failure DESIGN.md §3 records for a
+    UBSan build of the kernel TU."""
+    stubs, handles = _host_symbols(_native._PATHS[flavour])
+    assert stubs and set(stubs) == set(handles)
+    assert len({a for a, _ in stubs.values()}) == len(stubs)
+    assert len({a for a, _ in handles.values()}) == len(handles)
+    assert {k for _, k in stubs.values()} <= {"t", "T"} and {k for _, k in handles.values()} <= {"d", "D"}
+
+
+def _launch_protocol(path):
+    """Calls of the HIP launch protocol in the library's own x86 code (outside
+    the compiler's __device_stub__ functions): a launch pushes its
+    configuration (__hipPushCallConfiguration) and the stub's code -- inlined or
+    not -- pops it (__hipPopCallConfiguration) right before hipLaunchKernel."""
+    text = subprocess.check_output(["objdump", "-d", "--no-show-raw-insn", path], text=True)
+    func, push, pop = "", 0, 0
+    for line in text.splitlines():
+        h = re.match(r"^[0-9a-f]+ <(.*)>:", line)
+        if h:
+            func = h.group(1)
+            continue
+        if "__device_stub__" in func or "@plt" in func:
+            continue
+        push += "<__hipPushCallConfiguration@plt>" in line
+        pop += "<__hipPopCallConfiguration@plt>" in line
+    return push, pop
+
+
+@pytest.mark.parametrize("flavour", ["product", "tools"])
+def test_every_launch_reaches_its_kernel(flavour):
+    """Every launch site in the library's host code goes on to launch its
+    kernel.  Guards the failure DESIGN.md §3 records: with -fsanitize=function
+    a kernel launched through a function-pointer variable lost its launch --
+    only __hipPushCallConfiguration was left (no kernel ran, no report),
+    because the sanitizer reads 8 bytes in front of the kernel handle, which
+    the optimizer treats as out of bounds.  gf_tile.hpp launch_one launches by
+    kernel name.  (Measured on a host-UBSan build of gf_apply.hip with the
+    old pointer launch: 132 pushes, 1 pop; with launches by name: 143 / 143.)"""
+    path = _native._PATHS[flavour]
+    out = subprocess.check_output(["nm", path], text=True)
+    handles = [l for l in out.splitlines() if len(l.split()) == 3 and l.split()[1] in "dD" and "gf_apply_kernel" in l]
+    push, pop = _launch_protocol(path)
+    assert push == pop and push >= len(handles) > 0, (push, pop, len(handles))

@@ -25,6 +25,7 @@ from shmr_amd import _native  # noqa: E402
 
 CFG = {"encode83": (8, 3, 4 << 20, 0, 512), "decode83": (8, 3, 4 << 20, 1, 512),
        "encode104": (10, 4, 16 << 20, 0, 64), "decode104": (10, 4, 16 << 20, 2, 64),
+       "decode83e3": (8, 3, 4 << 20, 3, 512),
        "encode42": (4, 2, 1 << 20, 0, 1024)}
 
 
@@ -44,6 +45,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=9)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--pitch-align", type=int, default=256, help="shard pitch alignment (bench.py uses 4096)")
+    ap.add_argument("--compact", action="store_true",
+                    help="decode: rebuild into a compact [B][erasures][pitch] output (shmr_ec_reconstruct_batch_dev_out)")
     ap.add_argument("--ptrs", action="store_true",
                     help="every shard its own torch allocation, through the *_ptrs_dev calls (bench.py --layout ptrs)")
     a = ap.parse_args()
@@ -68,8 +71,8 @@ def main():
         if er == 1:
             present[rows, rows % k] = 0
         elif er:
-            present[rows, rows % 10] = 0
-            present[rows, (rows + 3) % 10] = 0
+            for j in range(er):   # {b, b+3, b+6, ...} mod min(total, 10), as tools/tune.py
+                present[rows, (rows + 3 * j) % min(t, 10)] = 0
         outs = [[torch.zeros(S, dtype=torch.uint8, device=dev) for _ in range(t)] for _ in range(B)]
         table = [blocks[b][i] if present[b, i] else outs[b][i] for b in range(B) for i in range(t)]
         tab = (_native._u8p * (B * t))(*[ctypes.cast(x.data_ptr(), _native._u8p) for x in table])
@@ -105,17 +108,31 @@ def main():
         if er == 1:
             present[rows, rows % k] = 0
         else:
-            present[rows, rows % 10] = 0
-            present[rows, (rows + 3) % 10] = 0
+            for j in range(er):
+                present[rows, (rows + 3 * j) % min(k + p, 10)] = 0
         algo = B * (k + er) * S
         pr = present.ctypes.data_as(_native._u8p)
+        if a.compact:   # real parity content (a zero parity input changes the rate)
+            for n, L in libs.items():
+                h = ctypes.c_void_p()
+                assert L.shmr_ec_new(k, p, ctypes.byref(h)) == 0
+                assert L.shmr_ec_encode_batch_dev(h, ctypes.c_void_p(shards.data_ptr()), pitch, (k + p) * pitch,
+                                                  ctypes.c_void_p(shards.data_ptr() + k * pitch), pitch,
+                                                  (k + p) * pitch, B, S, 0, sp) == 0
+                break
+        outs = {n: torch.zeros((B, er, pitch), dtype=torch.uint8, device=dev) for n in libs}
         for n, L in libs.items():
             h = ctypes.c_void_p()
             assert L.shmr_ec_new(k, p, ctypes.byref(h)) == 0
 
-            def run(L=L, h=h):
-                rc = L.shmr_ec_reconstruct_batch_dev(h, ctypes.c_void_p(shards.data_ptr()), pitch, (k + p) * pitch,
-                                                     pr, B, S, 0, 0, sp)
+            def run(L=L, h=h, out=outs[n]):
+                if a.compact:
+                    rc = L.shmr_ec_reconstruct_batch_dev_out(h, ctypes.c_void_p(shards.data_ptr()), pitch,
+                                                             (k + p) * pitch, pr, B, S, 0,
+                                                             ctypes.c_void_p(out.data_ptr()), pitch, er * pitch, 0, sp)
+                else:
+                    rc = L.shmr_ec_reconstruct_batch_dev(h, ctypes.c_void_p(shards.data_ptr()), pitch,
+                                                         (k + p) * pitch, pr, B, S, 0, 0, sp)
                 assert rc == 0, rc
             runs[n] = run
     t0 = time.perf_counter()
@@ -136,6 +153,9 @@ def main():
     if er == 0 and not a.ptrs:
         for n in par:
             assert torch.equal(par["current"], par[n]), f"outputs differ: {n}"
+    if er and a.compact and not a.ptrs:
+        for n in outs:
+            assert torch.equal(outs["current"], outs[n]), f"outputs differ: {n}"
     for n, ts in times.items():
         med = float(np.median(ts))
         print(json.dumps({"config": a.config, "lib": n, "median_ms": round(med, 4), "min_ms": round(min(ts), 4),

@@ -26,12 +26,11 @@ build)
     SAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer"
     CXXF="-O1 -g -std=c++17 -fPIC -Wall -I$ROOT/include -I$ROOT/shmr_amd/csrc"
     C="$ROOT/shmr_amd/csrc"
-    # The kernel TU gets ASan only: UBSan on the host side of a HIP translation
-    # unit (kernel stubs, fat-binary registration) made the launches produce
-    # wrong parity on the box with byte-identical device ISA, while ASan there
-    # and UBSan on every other TU were clean (tools/abi_check.cpp isolates it).
-    $HIPCC $CXXF -Xarch_host -fsanitize=address -Xarch_host -fno-omit-frame-pointer --offload-arch=gfx950 \
-        -x hip -c "$C/gf_apply.hip" -o "$L/gf_apply.o"
+    # The kernel TU too (r04): UBSan there used to return wrong parity because
+    # -fsanitize=function deleted launches made through a kernel function
+    # pointer; launch_one now launches by kernel name, and
+    # tests/test_isa.py checks every launch site still pops its configuration.
+    $HIPCC $CXXF $SAN --offload-arch=gfx950 -x hip -c "$C/gf_apply.hip" -o "$L/gf_apply.o"
     for f in gf256 ec_core host_engine ec_api; do
         $HIPCC $CXXF $SAN -c "$C/$f.cpp" -o "$L/$f.o"
     done
