@@ -22,6 +22,10 @@ SUBJECTS = {
     # name: (directory prefix, kernel-name filter, algorithmic bytes per dispatch)
     "gf_encode104_slots": ("gf", "gf_apply_kernel<4, 2, 0", 64 * 14 * 1677722),
     "gf_encode104_packed": ("gfpack", "gf_apply_kernel<4, 2, 0", 64 * 14 * 1677722),
+    # r04: the same encode with the peeled ring, and the realigning kernel (MODE 3, knob uvec=0)
+    # on the packed buffer -- it covers the 409 full 4 KiB tiles of each shard (the rest is MODE 2)
+    "gf_encode104_peel": ("gfpeel", "gf_apply_kernel<4, 2, 0", 64 * 14 * 1677722),
+    "gf_encode104_packed_mode3": ("gfpack3", "gf_apply_kernel<4, 1, 3", 64 * 14 * 409 * 4096),
     "xor_10to4_U1": ("xor", "kin_rout<10, 4, 1", 64 * 14 * 1671168),
     "xor_10to4_U2": ("xor", "kin_rout<10, 4, 2", 64 * 14 * 1671168),
 }
