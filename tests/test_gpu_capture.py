@@ -205,6 +205,27 @@ def test_capture_reserve_reused_across_graphs_and_large_capture(gpu):
     rs = shmr_amd.ReedSolomon(k, p)
     buf = torch.randint(0, 256, (B * t * S,), dtype=torch.uint8, device=gpu)
     addrs, tab = _ptr_table(buf.data_ptr(), B, t, S)
+    # two live graphs (torch destroys the captured hipGraph_t right after instantiating it, so the
+    # executable graph alone must keep its table): each replays its own table, not the other's
+    buf2 = torch.randint(0, 256, (B * t * S,), dtype=torch.uint8, device=gpu)
+    _, tab2 = _ptr_table(buf2.data_ptr(), B, t, S)
+    ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+    with torch.cuda.graph(ga, stream=stream):
+        assert rs._L.shmr_ec_encode_ptrs_dev(rs._h, tab, B, S, 0, sp) == 0
+    with torch.cuda.graph(gb, stream=stream):
+        assert rs._L.shmr_ec_encode_ptrs_dev(rs._h, tab2, B, S, 0, sp) == 0
+    for g, mine, other in ((ga, buf, buf2), (gb, buf2, buf)):
+        mine.view(B, t, S)[:, k:] = 0
+        other.view(B, t, S)[:, k:] = 0
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        h = mine.view(B, t, S).cpu().numpy()
+        assert np.array_equal(h[:, k:], _oracle_parity(k, p, h[:, :k]))
+        assert not other.view(B, t, S)[:, k:].any().item(), "a graph ran another graph's table"
+    del ga, gb
+    gc.collect()
+    torch.cuda.synchronize()
     st0 = shmr_amd.device_stats(0)
     for cycle in range(120):
         g = torch.cuda.CUDAGraph()

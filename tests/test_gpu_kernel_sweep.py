@@ -82,7 +82,9 @@ def _patterns(k, t, rows, segs):
 
 def _dev_views(gpu, arr, misalign_one):
     """Separate GPU buffers per shard (slices of one arena); one shard off
-    16-byte alignment when misalign_one."""
+    16-byte alignment when misalign_one: the last shard of block 1, which no
+    erasure pattern here removes (a removed shard would be replaced by a fresh,
+    aligned buffer)."""
     import torch
     Bn, t, L = arr.shape
     slot = (L + 64 + 255) // 256 * 256
@@ -91,7 +93,7 @@ def _dev_views(gpu, arr, misalign_one):
     for b in range(Bn):
         row = []
         for i in range(t):
-            off = (b * t + i) * slot + (3 if misalign_one and b == 1 and i == 0 else 0)
+            off = (b * t + i) * slot + (3 if misalign_one and b == 1 and i == t - 1 else 0)
             v = arena[off:off + L]
             v.copy_(torch.from_numpy(np.ascontiguousarray(arr[b, i])).to(gpu))
             row.append(v)
