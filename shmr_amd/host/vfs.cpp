@@ -1065,7 +1065,7 @@ Status VirtualFile::sync_data(bool force) {
         const size_t nd = std::max<size_t>(1, devices.size());
         std::atomic<size_t> coded{0};
         std::mutex tmu;
-        parallel_for(blocks.size(), 16, [&](size_t i) {
+        parallel_for(blocks.size(), per_block_tasks, [&](size_t i) {
             const VirtualBlock& b = blocks[i];
             const bool dirty = force || b.st_->should_flush.load();
             const double ts = now_s();
@@ -1222,7 +1222,7 @@ Status VirtualFile::load_blocks(const std::vector<size_t>& block_indices,
         const size_t nd = std::max<size_t>(1, devices.size());
         std::atomic<size_t> rebuilt{0};
         std::mutex tmu;
-        parallel_for(todo.size(), 16, [&](size_t q) {
+        parallel_for(todo.size(), per_block_tasks, [&](size_t q) {
             const size_t i = todo[q];
             const VirtualBlock& b = blocks[i];
             bool rec = false;

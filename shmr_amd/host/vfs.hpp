@@ -238,6 +238,9 @@ public:
     // memory bandwidth and pipelining measured slower.
     static constexpr size_t kAutoBatch = ~size_t(0);
     size_t pipeline_batch_bytes = kAutoBatch;
+    // Concurrent per-block tasks of the mapped-buffer flush / load (the
+    // reference's rayon fan-out, mod.rs:93-96; the worker pool has 32 threads).
+    size_t per_block_tasks = 16;
 
     // read (mod.rs:137-180): the blocks the range touches are loaded in one
     // batched call (load_blocks) and copied out as the reference's chunk loop

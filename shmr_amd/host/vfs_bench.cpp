@@ -50,6 +50,7 @@ Result run_once(const std::shared_ptr<const ShmrFsConfig>& cfg, uint64_t ino, co
     vf.populate(cfg);
     vf.block_size = block_bytes;
     vf.pipeline_batch_bytes = batch_bytes;
+    if (const char* e = std::getenv("SHMR_VFS_TASKS")) vf.per_block_tasks = std::strtoull(e, nullptr, 10);
     for (size_t i = 0; i < nblk; ++i) {
         VirtualBlock b;
         DIE_IF(VirtualBlock::create(ino, i + 1, cfg, block_bytes, BlockTopology::erasure(1, 8, 3), &b));
@@ -206,14 +207,16 @@ int main(int argc, char** argv) {
             "\"sync_pipeline_GiBps\": %s, \"per_block_sync_GiBps\": %s, \"read_with_erasure_GiBps\": %s, "
             "\"read_reconstruct_GiBps\": %s, \"read_shard_io_GiBps\": %s, \"read_pipeline_GiBps\": %s, "
             "\"reconstructed_blocks\": %zu, \"sync_prepare_ms\": %.2f, \"read_prepare_ms\": %.2f, "
-            "\"read_needed_shards\": %s, \"shard_reads_per_block\": %.2f, %s\"verified\": true}\n",
+            "\"read_needed_shards\": %s, \"shard_reads_per_block\": %.2f, \"per_block_task_threads\": %s, "
+            "%s\"verified\": true}\n",
             pinned ? "mapped Block Cache (shmr_ec_host_alloc)" : "pageable", (unsigned long long)(zc1 - zc0),
             (unsigned long long)(st1 - st0), batch_name.c_str(), (unsigned long long)file_mib,
             (unsigned long long)block_mib, int(do_fsync), reps, rate(best.write_s).c_str(), rate(best.sync_s).c_str(),
             rate(best.sync.codec_s).c_str(), rate(best.sync.io_s).c_str(), rate(best.sync.total_s).c_str(),
             rate(best.per_block_sync_s).c_str(), rate(best.read_s).c_str(), rate(best.load.codec_s).c_str(),
             rate(best.load.io_s).c_str(), rate(best.load.total_s).c_str(), best.load.blocks, best.sync.prepare_s * 1e3,
-            best.load.prepare_s * 1e3, needed ? "true" : "false", best.shard_reads_per_block, tasks_json(best).c_str());
+            best.load.prepare_s * 1e3, needed ? "true" : "false", best.shard_reads_per_block,
+            std::getenv("SHMR_VFS_TASKS") ? std::getenv("SHMR_VFS_TASKS") : "16", tasks_json(best).c_str());
         std::fflush(stdout);
     }
     return 0;

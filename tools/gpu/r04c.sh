@@ -37,3 +37,9 @@ cd $R
 python3 tools/counter_table.py $O/pmc --json $O/counters_encode104_r04.json > $O/counters_encode104_r04.md || exit $?
 find $O -name '*_kernel_trace.csv' -size +2M -delete
 echo done-counters
+# config 5: per-block task concurrency of the mapped-buffer read / flush (default 16)
+mkdir -p /tmp/vb
+for n in 24 32 16; do
+  SHMR_VFS_TASKS=$n timeout -k 10 400 shmr_amd/_lib/shmr_vfs_bench /tmp/vb 256 4 0 3 > $O/e2e_vf_tasks$n.jsonl 2> $O/e2e_vf_tasks$n.err || exit $?
+done
+echo done-e2e
