@@ -124,6 +124,22 @@ int shmr_ec_encode(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_le
 int shmr_ec_reconstruct(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_lens,
                         const uint8_t* present, size_t nshards, int data_only);
 
+/* Asynchronous forms of shmr_ec_encode / shmr_ec_reconstruct (same arguments,
+ * validation and errors, returned by the start call), so a Block Cache can
+ * overlap its file I/O or copies with the GPU: when every shard the call
+ * touches lies in mapped memory, the kernels are enqueued and the start call
+ * returns with *op pending; on every other path the work is complete when it
+ * returns.  While *op is pending the caller may read -- not write -- the input
+ * shards (encode: shards [0, data); reconstruct: the present ones) and must not
+ * touch the output shards.  shmr_ec_op_wait(op) waits for the work, frees op
+ * and returns SHMR_EC_OK or a device error; on a start error *op is NULL. */
+typedef struct shmr_ec_op shmr_ec_op_t;
+int shmr_ec_encode_start(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_lens, size_t nshards,
+                         shmr_ec_op_t** op);
+int shmr_ec_reconstruct_start(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_lens,
+                              const uint8_t* present, size_t nshards, int data_only, shmr_ec_op_t** op);
+int shmr_ec_op_wait(shmr_ec_op_t* op);
+
 /* ---- device-resident batched entry points ------------------------------ *
  * All pointers are device pointers on `device`; `stream` is a hipStream_t
  * (NULL = the null stream).  Block b's shard i lives at

@@ -83,6 +83,11 @@ SIGNATURES = [
     ("shmr_ec_device_count", ctypes.c_int, []),
     ("shmr_ec_device_stats", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), _sz]),
     ("shmr_ec_kernel_inventory", _sz, [ctypes.c_void_p, _sz]),
+    ("shmr_ec_encode_start", ctypes.c_int,
+     [ctypes.c_void_p, _u8pp, ctypes.POINTER(_sz), _sz, ctypes.POINTER(ctypes.c_void_p)]),
+    ("shmr_ec_reconstruct_start", ctypes.c_int,
+     [ctypes.c_void_p, _u8pp, ctypes.POINTER(_sz), _u8p, _sz, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    ("shmr_ec_op_wait", ctypes.c_int, [ctypes.c_void_p]),
 ]
 
 

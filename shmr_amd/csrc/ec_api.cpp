@@ -337,7 +337,10 @@ int shmr_ec_host_unregister(void* p) {
 }
 
 // ---- host-buffer encode (ReedSolomon::encode) --------------------------------------
-int shmr_ec_encode(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_lens, size_t nshards) {
+// async != nullptr (shmr_ec_encode_start): shards in mapped memory are coded by
+// kernels left running on *async's stream; every other path finishes here.
+static int encode_impl(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_lens, size_t nshards,
+                       core::Staging** async) {
     return guarded([&]() -> int {
         if (!rs || !shards || !shard_lens) return SHMR_EC_INVALID_ARGUMENT;
         Codec& c = *rs->codec;
@@ -357,7 +360,7 @@ int shmr_ec_encode(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_le
         {   // shards in mapped memory: the kernel encodes them in place (zero-copy)
             const core::HostJob job{c, core::kEncode, false, shards, nullptr, 1, len, 0, 1};
             bool handled = false;
-            rc = core::run_mapped_job(job, &dev, 1, &handled);
+            rc = core::run_mapped_job(job, &dev, 1, &handled, true, async);
             if (handled || rc) return rc;
         }
         if (uint64_t(t) * len <= core::bounce_limit()) {   // pageable, small: one bounce, one launch
@@ -385,8 +388,8 @@ int shmr_ec_encode(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_le
 }
 
 // ---- host-buffer reconstruct (ReedSolomon::reconstruct{,_data}) ---------------------
-int shmr_ec_reconstruct(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_lens, const uint8_t* present,
-                        size_t nshards, int data_only) {
+static int reconstruct_impl(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_lens, const uint8_t* present,
+                            size_t nshards, int data_only, core::Staging** async) {
     return guarded([&]() -> int {
         if (!rs || !shards || !shard_lens || !present) return SHMR_EC_INVALID_ARGUMENT;
         Codec& c = *rs->codec;
@@ -421,7 +424,7 @@ int shmr_ec_reconstruct(shmr_ec_t* rs, uint8_t* const* shards, const size_t* sha
         {   // shards in mapped memory: rebuilt in place by the kernel (zero-copy)
             const core::HostJob job{c, core::kDecode, data_only != 0, shards, present, 1, len, 0, 1};
             bool handled = false;
-            rc = core::run_mapped_job(job, &dev, 1, &handled);
+            rc = core::run_mapped_job(job, &dev, 1, &handled, true, async);
             if (handled || rc) return rc;
         }
         if (uint64_t(t) * len <= core::bounce_limit()) {   // pageable, small: one bounce, one launch
@@ -449,6 +452,62 @@ int shmr_ec_reconstruct(shmr_ec_t* rs, uint8_t* const* shards, const size_t* sha
         SHMR_HIP_TRY(core::sync_stream(s.stream));
         return SHMR_EC_OK;
     });
+}
+
+int shmr_ec_encode(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_lens, size_t nshards) {
+    return encode_impl(rs, shards, shard_lens, nshards, nullptr);
+}
+
+int shmr_ec_reconstruct(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_lens, const uint8_t* present,
+                        size_t nshards, int data_only) {
+    return reconstruct_impl(rs, shards, shard_lens, present, nshards, data_only, nullptr);
+}
+
+// ---- asynchronous single-block calls -----------------------------------------------
+struct shmr_ec_op {
+    core::Staging* s = nullptr;   // pending zero-copy kernels' stream, or none
+};
+
+static int start_op(int rc, core::Staging* s, shmr_ec_op_t** op) {
+    if (rc != SHMR_EC_OK) {
+        if (s) (void)core::finish_async(s);
+        return rc;
+    }
+    return guarded([&]() -> int {
+        try {
+            *op = new shmr_ec_op;
+        } catch (...) {
+            if (s) (void)core::finish_async(s);
+            throw;
+        }
+        (*op)->s = s;
+        return SHMR_EC_OK;
+    });
+}
+
+int shmr_ec_encode_start(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_lens, size_t nshards,
+                         shmr_ec_op_t** op) {
+    if (!op) return SHMR_EC_INVALID_ARGUMENT;
+    *op = nullptr;
+    core::Staging* s = nullptr;
+    const int rc = encode_impl(rs, shards, shard_lens, nshards, &s);
+    return start_op(rc, s, op);
+}
+
+int shmr_ec_reconstruct_start(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_lens, const uint8_t* present,
+                              size_t nshards, int data_only, shmr_ec_op_t** op) {
+    if (!op) return SHMR_EC_INVALID_ARGUMENT;
+    *op = nullptr;
+    core::Staging* s = nullptr;
+    const int rc = reconstruct_impl(rs, shards, shard_lens, present, nshards, data_only, &s);
+    return start_op(rc, s, op);
+}
+
+int shmr_ec_op_wait(shmr_ec_op_t* op) {
+    if (!op) return SHMR_EC_INVALID_ARGUMENT;
+    const int rc = op->s ? guarded([&] { return core::finish_async(op->s); }) : SHMR_EC_OK;
+    delete op;
+    return rc;
 }
 
 // ---- device-resident batches --------------------------------------------------------

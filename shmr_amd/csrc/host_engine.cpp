@@ -280,7 +280,8 @@ bool map_job(const HostJob& job, std::vector<uint64_t>* dptrs, bool* aligned) {
 
 // Zero-copy: per device, the blocks' shard-pointer tables go up through the
 // device's pointer ring and the kernels run on the host buffers in place.
-int run_mapped(const HostJob& job, const std::vector<uint64_t>& dptrs, bool aligned, const int* devices, int ndev) {
+int run_mapped(const HostJob& job, const std::vector<uint64_t>& dptrs, bool aligned, const int* devices, int ndev,
+               Staging** async) {
     Codec& c = job.codec;
     const unsigned t = c.k() + c.p();
     std::vector<int> results(size_t(ndev), SHMR_EC_OK);
@@ -347,7 +348,12 @@ int run_mapped(const HostJob& job, const std::vector<uint64_t>& dptrs, bool alig
             const int rc2 = ring->release_after(slot, stream);
             if (rc == SHMR_EC_OK) rc = rc2;
         }
-        if (sync_stream(stream) != hipSuccess && rc == SHMR_EC_OK) rc = SHMR_EC_DEVICE_ERROR;
+        if (async && rc == SHMR_EC_OK) {   // the caller waits (finish_async)
+            *async = lease.s;
+            lease.s = nullptr;
+        } else if (sync_stream(stream) != hipSuccess && rc == SHMR_EC_OK) {
+            rc = SHMR_EC_DEVICE_ERROR;
+        }
         result = rc;
     };
     std::vector<std::thread> th;
@@ -468,8 +474,17 @@ int run_bounced_job(const HostJob& job, int device) {
     return rc;
 }
 
-int run_mapped_job(const HostJob& job, const int* devices, int ndev, bool* handled, bool count) {
+int finish_async(Staging* s) {
+    StagingLease lease;
+    lease.s = s;
+    DeviceScope scope(s->dev);
+    if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
+    return sync_stream(s->stream) == hipSuccess ? SHMR_EC_OK : SHMR_EC_DEVICE_ERROR;
+}
+
+int run_mapped_job(const HostJob& job, const int* devices, int ndev, bool* handled, bool count, Staging** async) {
     *handled = false;
+    if (async && ndev != 1) return SHMR_EC_INVALID_ARGUMENT;
     if (job.op == kDecode) {
         const int rc = validate_presence(job.codec, job.present, job.nblocks);
         if (rc) return rc;
@@ -479,7 +494,7 @@ int run_mapped_job(const HostJob& job, const int* devices, int ndev, bool* handl
     if (!map_job(job, &dptrs, &aligned)) return SHMR_EC_OK;
     *handled = true;
     if (count) count_blocks(true, job.nblocks);
-    return run_mapped(job, dptrs, aligned, devices, ndev);
+    return run_mapped(job, dptrs, aligned, devices, ndev, async);
 }
 
 int copy_threads_default() {

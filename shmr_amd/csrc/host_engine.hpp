@@ -31,7 +31,13 @@ int run_host_job(const HostJob& job, const int* devices, int ndev);
 
 // Zero-copy only: *handled = false (and nothing runs) unless every shard the
 // job touches is mapped.  Used by the single-block entry points.
-int run_mapped_job(const HostJob& job, const int* devices, int ndev, bool* handled, bool count = true);
+// async (one device only): the kernels are enqueued and *async receives the
+// staging stream they run on, not synchronised -- the caller waits on it and
+// releases it (finish_async); nothing is kept when the job is not handled.
+int run_mapped_job(const HostJob& job, const int* devices, int ndev, bool* handled, bool count = true,
+                   Staging** async = nullptr);
+// Waits for an async mapped job's stream and returns it to the pool.
+int finish_async(Staging* s);
 
 // Pageable single-block job through a pooled mapped bounce buffer: the input
 // shards are memcpy'd in, the kernel runs zero-copy on the bounce buffer, the

@@ -22,6 +22,27 @@ struct EcStatus {
     const char* name() const { return shmr_ec_status_name(code); }
 };
 
+// A pending shmr_ec_encode_start / shmr_ec_reconstruct_start; waits on
+// destruction if wait() was not called.
+class EcOp {
+public:
+    EcOp() = default;
+    EcOp(const EcOp&) = delete;
+    EcOp& operator=(const EcOp&) = delete;
+    ~EcOp() {
+        if (op_) (void)shmr_ec_op_wait(op_);
+    }
+    EcStatus wait() {
+        shmr_ec_op_t* o = op_;
+        op_ = nullptr;
+        return EcStatus{o ? shmr_ec_op_wait(o) : SHMR_EC_OK};
+    }
+    shmr_ec_op_t** out() { return &op_; }
+
+private:
+    shmr_ec_op_t* op_ = nullptr;
+};
+
 class ReedSolomon {
 public:
     // ReedSolomon::new(data_shards, parity_shards)
@@ -72,6 +93,18 @@ public:
         std::vector<size_t> lens(n);
         for (size_t i = 0; i < n; ++i) lens[i] = present[i] ? len : 0;
         return EcStatus{shmr_ec_reconstruct(h_, shards, lens.data(), present, n, data_only)};
+    }
+    // The same, started: the GPU work may still run when they return (mapped
+    // shards); op->wait() completes it.  Inputs may be read meanwhile.
+    EcStatus encode_start(uint8_t* const* shards, size_t n, size_t len, EcOp* op) const {
+        std::vector<size_t> lens(n, len);
+        return EcStatus{shmr_ec_encode_start(h_, shards, lens.data(), n, op->out())};
+    }
+    EcStatus reconstruct_start(uint8_t* const* shards, const uint8_t* present, size_t n, size_t len, bool data_only,
+                               EcOp* op) const {
+        std::vector<size_t> lens(n);
+        for (size_t i = 0; i < n; ++i) lens[i] = present[i] ? len : 0;
+        return EcStatus{shmr_ec_reconstruct_start(h_, shards, lens.data(), present, n, data_only, op->out())};
     }
 
 private:

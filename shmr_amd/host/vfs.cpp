@@ -648,19 +648,37 @@ Status VirtualBlock::sync_data(bool force, int device, PhaseTimes* times) const 
         const size_t n = size_t(topology.data) + topology.parity;
         std::vector<uint8_t*> ptrs(n);
         shard_ptrs(buffer, n, S, ptrs.data());
+        // block.rs:427 (.unwrap() in the reference).  Started: with mapped Block-
+        // Cache buffers the GPU still runs when it returns, and the data shard
+        // files (the encode's inputs, never written by it) go out meanwhile;
+        // the parity files after the wait.  block.rs:436-439 writes all k+p.
         const double tc = times ? now_s() : 0;
-        es = r->encode_in_place(ptrs.data(), n, S);   // block.rs:427 (.unwrap() in the reference)
-        if (times) times->codec_s += now_s() - tc;
+        EcOp op;
+        es = r->encode_start(ptrs.data(), n, S, &op);
+        if (es.ok()) {
+            const size_t k = topology.data, nw = std::min(n, nh);
+            const double tw = times ? now_s() : 0;
+            parallel_for(std::min(k, nw), 16, [&](size_t i) {
+                res[i] = st_->ensure_fd(i, *cfg_);
+                if (!res[i]) res[i] = write_path(st_->handles[i].second, ptrs[i], S, opt_.fsync_shards);
+            });
+            const double tw2 = times ? now_s() : 0;
+            es = op.wait();
+            if (times) times->codec_s += now_s() - tc - (tw2 - tw), times->io_s += tw2 - tw;
+            if (es.ok() && nw > k) {
+                const double tp = times ? now_s() : 0;
+                parallel_for(nw - k, 16, [&](size_t j) {
+                    const size_t i = k + j;
+                    res[i] = st_->ensure_fd(i, *cfg_);
+                    if (!res[i]) res[i] = write_path(st_->handles[i].second, ptrs[i], S, opt_.fsync_shards);
+                });
+                if (times) times->io_s += now_s() - tp;
+            }
+        }
         if (!es.ok()) {
             restore_tail(buffer, topology, S, tail);
             return ec_error(es.code);
         }
-        const double tw = times ? now_s() : 0;
-        parallel_for(std::min(n, nh), 16, [&](size_t i) {   // block.rs:436-439, in parallel
-            res[i] = st_->ensure_fd(i, *cfg_);
-            if (!res[i]) res[i] = write_path(st_->handles[i].second, ptrs[i], S, opt_.fsync_shards);
-        });
-        if (times) times->io_s += now_s() - tw;
         restore_tail(buffer, topology, S, tail);
     } else {
         const size_t copies = topology.kind == BlockTopology::Single ? 1 : std::min<size_t>(topology.n, nh);
@@ -696,7 +714,8 @@ Status VirtualBlock::open_handles() const {
 }
 
 // block.rs:496-584
-Status VirtualBlock::load_block(bool* reconstructed, int device, PhaseTimes* times) const {
+Status VirtualBlock::load_block(bool* reconstructed, int device, PhaseTimes* times,
+                                const std::function<void(const uint8_t*)>* during) const {
     if (reconstructed) *reconstructed = false;
     if (!st_->shard_loaded.load()) {
         if (auto e = open_handles()) return e;
@@ -761,8 +780,20 @@ Status VirtualBlock::load_block(bool* reconstructed, int device, PhaseTimes* tim
         for (size_t i = 0; i < n; ++i) missing |= !present[i] || odd[i];
         if (missing) {
             const double tc = times ? now_s() : 0;
-            es = r->reconstruct_in_place(ptrs.data(), present.data(), n, S, false);   // block.rs:560 (unwrap)
-            if (times) times->codec_s += now_s() - tc;
+            double td = 0;
+            if (during && *during) {   // copies of the present shards overlap the GPU work
+                EcOp op;
+                es = r->reconstruct_start(ptrs.data(), present.data(), n, S, false, &op);   // block.rs:560
+                if (es.ok()) {
+                    const double t1 = now_s();
+                    (*during)(present.data());
+                    td = now_s() - t1;
+                    es = op.wait();
+                }
+            } else {
+                es = r->reconstruct_in_place(ptrs.data(), present.data(), n, S, false);   // block.rs:560 (unwrap)
+            }
+            if (times) times->codec_s += now_s() - tc - td, times->overlap_s += td;
             if (!es.ok()) return ec_error(es.code);
             if (reconstructed) *reconstructed = true;
         }
@@ -930,6 +961,29 @@ Status VirtualFile::read(uint64_t pos, uint8_t* buf, size_t len, size_t* nread) 
     std::map<size_t, std::vector<size_t>> early_of;   // block -> early run indices
     for (size_t i = 0; i < early.size(); ++i) early_of[early[i].blk].push_back(i);
     std::vector<uint8_t> copied(early.size(), 0);
+    // Pieces of a run still to copy after its block's reconstruct: a run whose
+    // block was rebuilt by a per-block task had its bytes in present data
+    // shards copied while the GPU rebuilt the rest (during_rebuild).
+    std::vector<std::vector<std::pair<uint64_t, size_t>>> rest(early.size());
+    std::vector<uint8_t> split(early.size(), 0);
+    auto during_rebuild = [&](size_t bi, const uint8_t* present) {
+        auto it = early_of.find(bi);
+        if (it == early_of.end()) return;
+        const VirtualBlock& b = blocks[bi];
+        const uint64_t S = b.shard_size(), k = b.topology.data;
+        const auto& data = b.st_->buffer;   // locked by the load task (this thread)
+        for (size_t q : it->second) {
+            const ReadRun& r = early[q];
+            if (data.size() < r.block_pos + r.len || S == 0) continue;
+            for (uint64_t p0 = r.block_pos, end = r.block_pos + r.len; p0 < end;) {
+                const uint64_t s = p0 / S, p1 = std::min(end, (s + 1) * S);
+                if (s < k && present[s]) std::memcpy(buf + r.off + (p0 - r.block_pos), data.data() + p0, p1 - p0);
+                else rest[q].emplace_back(p0, size_t(p1 - p0));
+                p0 = p1;
+            }
+            split[q] = 1;
+        }
+    };
     auto on_batch = [&](const std::vector<size_t>& loaded) {
         std::vector<size_t> todo;
         for (size_t bi : loaded) {
@@ -942,11 +996,16 @@ Status VirtualFile::read(uint64_t pos, uint8_t* buf, size_t len, size_t* nread) 
             const ReadRun& r = early[todo[q]];
             const auto& data = blocks[r.blk].st_->buffer;
             if (data.size() < r.block_pos + r.len) return;   // not as planned: the plan below copies it
-            std::memcpy(buf + r.off, data.data() + r.block_pos, r.len);
+            if (split[todo[q]]) {
+                for (const auto& pc : rest[todo[q]])
+                    std::memcpy(buf + r.off + (pc.first - r.block_pos), data.data() + pc.first, pc.second);
+            } else {
+                std::memcpy(buf + r.off, data.data() + r.block_pos, r.len);
+            }
             copied[todo[q]] = 1;
         });
     };
-    if (auto e = load_blocks(blocks_for_range(pos, len), on_batch)) return e;
+    if (auto e = load_blocks(blocks_for_range(pos, len), on_batch, during_rebuild)) return e;
     uint64_t c = 0;
     size_t done = 0;
     std::vector<ReadRun> runs = plan_read_runs(blocks, chunk_size, block_size, pos, len,
@@ -1208,7 +1267,8 @@ Status VirtualFile::sync_data(bool force) {
 // Batched load_block (block.rs:496-584) over several blocks: the same rules
 // per block, one reconstruct call per (k, p, S) for the blocks with erasures.
 Status VirtualFile::load_blocks(const std::vector<size_t>& block_indices,
-                                const std::function<void(const std::vector<size_t>&)>& on_batch) {
+                                const std::function<void(const std::vector<size_t>&)>& on_batch,
+                                const DuringRebuild& during_rebuild) {
     last_load = IoStats{};
     const double t0 = now_s();
     std::vector<Status> results(blocks.size());
@@ -1228,9 +1288,11 @@ Status VirtualFile::load_blocks(const std::vector<size_t>& block_indices,
             bool rec = false;
             const double ts = now_s();
             PhaseTimes pt;
-            results[i] = b.load_block(&rec, devices.empty() ? 0 : devices[i % nd], &pt);
+            std::function<void(const uint8_t*)> during;
+            if (during_rebuild) during = [&, i](const uint8_t* present) { during_rebuild(i, present); };
+            results[i] = b.load_block(&rec, devices.empty() ? 0 : devices[i % nd], &pt, &during);
             if (rec) ++rebuilt;
-            double copy_s = 0;
+            double copy_s = pt.overlap_s;
             if (!results[i] && on_batch && b.topology.kind == BlockTopology::Erasure) {
                 std::lock_guard<std::mutex> lock(b.st_->buf_mu);   // on_batch reads the buffer unlocked
                 const double tc = now_s();

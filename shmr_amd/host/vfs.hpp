@@ -158,8 +158,9 @@ struct IoStats {
 
 // Phase times of one VirtualBlock::sync_data / load_block call (seconds).
 struct PhaseTimes {
-    double io_s = 0;      // shard-file reads or writes
-    double codec_s = 0;   // the GPU encode / reconstruct call
+    double io_s = 0;        // shard-file reads or writes (flush: those not overlapped with the encode)
+    double codec_s = 0;     // the GPU encode / reconstruct call, minus work overlapped with it
+    double overlap_s = 0;   // load: the during-rebuild callback (copies overlapping the GPU work)
 };
 
 // VirtualBlock (src/vfs/block.rs:119-634).  Copies share state, like the
@@ -200,7 +201,11 @@ private:
     Status open_handles() const;
     Status load_block() const { return load_block(nullptr, 0); }
     // *reconstructed (if set): an Erasure block needed a reconstruct (on `device`)
-    Status load_block(bool* reconstructed, int device, PhaseTimes* times = nullptr) const;
+    // during (if set): called while the block's reconstruct runs, with the
+    // presence flags (mapped buffers: the kernel is still running; otherwise
+    // after it finished)
+    Status load_block(bool* reconstructed, int device, PhaseTimes* times = nullptr,
+                      const std::function<void(const uint8_t*)>* during = nullptr) const;
     size_t shard_size() const;   // S of an Erasure block (mod.rs:16-18)
     std::shared_ptr<State> st_;
     std::shared_ptr<const ShmrFsConfig> cfg_;
@@ -264,8 +269,14 @@ public:
     // each pipeline batch as soon as they are loaded (while later batches load);
     // it may read those blocks' buffers without locking -- load_blocks holds
     // their locks until every on_batch call has returned.
+    // during_rebuild (per-block tasks only), if set, is called by a block's load
+    // task while its zero-copy reconstruct runs on the GPU, with the block
+    // index and the shard presence flags: the present shards' bytes in the
+    // buffer are final then (the kernel only reads them) and may be copied.
+    using DuringRebuild = std::function<void(size_t blk, const uint8_t* present)>;
     Status load_blocks(const std::vector<size_t>& block_indices,
-                       const std::function<void(const std::vector<size_t>&)>& on_batch = {});
+                       const std::function<void(const std::vector<size_t>&)>& on_batch = {},
+                       const DuringRebuild& during_rebuild = {});
     Status drop_buffers() const;
     Status drop_handles() const;
     Status replace_block(size_t block_idx, VirtualBlock new_block);

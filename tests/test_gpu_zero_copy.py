@@ -223,3 +223,66 @@ def test_register_errors(gpu):
     import ctypes
     assert lib().shmr_ec_host_unregister(ctypes.c_void_p(12345)) == -100   # never registered
     assert lib().shmr_ec_host_register(None, 10) == -100
+
+
+def _start(rs, fn, shards, present=None, data_only=False):
+    """shmr_ec_encode_start / shmr_ec_reconstruct_start through ctypes: (rc, op)."""
+    import ctypes
+    from shmr_amd.reed_solomon import _ptr, _u8p
+    n = len(shards)
+    L = next(len(s) for s in shards if s is not None)
+    ptrs = (_u8p * n)(*[(_ptr(s) if s is not None else _u8p()) for s in shards])
+    lens = (ctypes.c_size_t * n)(*[(L if s is not None and (present is None or present[i]) else 0)
+                                   for i, s in enumerate(shards)])
+    op = ctypes.c_void_p()
+    if fn == "encode":
+        rc = rs._L.shmr_ec_encode_start(rs._h, ptrs, lens, n, ctypes.byref(op))
+    else:
+        pr = np.ascontiguousarray(present, dtype=np.uint8)
+        rc = rs._L.shmr_ec_reconstruct_start(rs._h, ptrs, lens, _ptr(pr), n, int(data_only), ctypes.byref(op))
+    return rc, op
+
+
+@pytest.mark.parametrize("mapped", [True, False])
+def test_started_encode_and_reconstruct(gpu, mapped):
+    """shmr_ec_encode_start / shmr_ec_reconstruct_start + shmr_ec_op_wait (the
+    Block Cache's overlap of shard-file writes and copy-outs with the GPU
+    work): mapped shards run zero-copy and the inputs may be read while the
+    op is pending; pageable shards finish inside the start call.  Bytes equal
+    the oracle's; validation errors come from the start call with no op."""
+    k, p, S = 8, 3, 3 * 4096 + 100
+    rng = np.random.default_rng(31 + int(mapped))
+    rs = shmr_amd.ReedSolomon(k, p)
+    if mapped:
+        keep, blocks = pinned_blocks(rng, k, p, S, 1)
+        sh = blocks[0]
+    else:
+        sh = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)] + [np.zeros(S, np.uint8) for _ in range(p)]
+    want = oracle_parity(k, p, sh[:k])
+    with Delta() as d:
+        rc, op = _start(rs, "encode", sh)
+        assert rc == 0 and op.value
+        snapshot = [s.copy() for s in sh[:k]]          # reading the inputs meanwhile is allowed
+        assert rs._L.shmr_ec_op_wait(op) == 0
+    assert (d.zero_copy, d.staged) == ((1, 0) if mapped else (0, 1))
+    assert all(np.array_equal(a, b) for a, b in zip(snapshot, sh[:k]))
+    for r in range(p):
+        assert np.array_equal(sh[k + r], want[r]), r
+    full = [s.copy() for s in sh]
+    present = np.ones(k + p, np.uint8)
+    present[[1, 6, 9]] = 0
+    for i in (1, 6, 9):
+        sh[i][:] = 0xEE
+    rc, op = _start(rs, "reconstruct", sh, present)
+    assert rc == 0 and op.value
+    assert rs._L.shmr_ec_op_wait(op) == 0
+    for i in range(k + p):
+        assert np.array_equal(sh[i], full[i]), i
+    # all present: a completed op; too few present: the crate's error, no op
+    rc, op = _start(rs, "reconstruct", sh, np.ones(k + p, np.uint8))
+    assert rc == 0 and rs._L.shmr_ec_op_wait(op) == 0
+    few = np.ones(k + p, np.uint8)
+    few[:4] = 0
+    rc, op = _start(rs, "reconstruct", sh, few)
+    assert shmr_amd.Error(rc).name == "TooFewShardsPresent" and not op.value
+    assert shmr_amd.Error(rs._L.shmr_ec_op_wait(None)).name == "InvalidArgument"

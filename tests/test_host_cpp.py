@@ -83,7 +83,11 @@ def test_library_exports():
     assert os.path.exists(lib)
     nm = subprocess.run(["nm", "-D", "--undefined-only", lib], capture_output=True, text=True, check=True).stdout
     used = {l.split()[-1] for l in nm.splitlines() if "shmr_ec_" in l}
-    assert {"shmr_ec_new", "shmr_ec_encode", "shmr_ec_reconstruct", "shmr_ec_encode_blocks_host"} <= used
+    # VirtualBlock::sync_data starts the encode and writes the data shard files
+    # while it runs (shmr_ec_encode_start / shmr_ec_op_wait); load_block
+    # reconstructs synchronously, or started when a copy-out overlaps it
+    assert {"shmr_ec_new", "shmr_ec_encode_start", "shmr_ec_op_wait", "shmr_ec_reconstruct",
+            "shmr_ec_reconstruct_start", "shmr_ec_encode_blocks_host"} <= used
 
 
 # --------------------------------------------------------------------------- GPU

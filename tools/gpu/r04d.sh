@@ -12,11 +12,11 @@ find gpurun_out -name '*_kernel_trace.csv' -delete
 find gpurun_out -name 'pmc_counter_collection.csv' -delete
 if [ "$PART" = 1 ]; then
   cp gpurun_out/pmc_traffic.json profiles/pmc_traffic.json   # (the box's copy) bench lines then match traffic
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
-    > $O/pytest_gpu_final.log 2>&1 || exit $?
-  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_final.log 2>&1 || exit $?
   for c in encode83 decode83 encode104 decode104 encode42 codec104; do
     timeout -k 10 300 python bench.py --config $c >> $O/bench_final.jsonl 2>> $O/bench_final.err || exit $?
   done
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_final.log 2>&1 || exit $?
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+    > $O/pytest_gpu_final.log 2>&1 || exit $?
 fi
 echo done-final-$PART
