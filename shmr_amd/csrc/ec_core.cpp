@@ -154,7 +154,7 @@ int set_tuning(const char* key, int value) {
     }
 #ifndef SHMR_EC_TOOLS
     // Product build: the kernel variant of every launch is the measured policy
-    // (variant_policy), the same for every caller in the process.  Kernel knobs
+    // (kern::policy_variant), the same for every caller in the process.  Kernel knobs
     // exist to take measurements and live in the tools build
     // (libshmr_ec_tools.so); here a knob may only be "set" to its default.
     // In particular "diag" (XOR-only, wrong results) is refused.

@@ -1292,7 +1292,7 @@ Status VirtualFile::load_blocks(const std::vector<size_t>& block_indices,
             if (during_rebuild) during = [&, i](const uint8_t* present) { during_rebuild(i, present); };
             results[i] = b.load_block(&rec, devices.empty() ? 0 : devices[i % nd], &pt, &during);
             if (rec) ++rebuilt;
-            double copy_s = pt.overlap_s;
+            double copy_s = 0;
             if (!results[i] && on_batch && b.topology.kind == BlockTopology::Erasure) {
                 std::lock_guard<std::mutex> lock(b.st_->buf_mu);   // on_batch reads the buffer unlocked
                 const double tc = now_s();
@@ -1303,6 +1303,7 @@ Status VirtualFile::load_blocks(const std::vector<size_t>& block_indices,
             last_load.task_read_s += pt.io_s;
             last_load.task_codec_s += pt.codec_s;
             last_load.task_copy_s += copy_s;
+            last_load.task_overlap_s += pt.overlap_s;
             last_load.task_total_s += now_s() - ts;
             ++last_load.tasks;
         });

@@ -151,7 +151,8 @@ struct IoStats {
     double task_read_s = 0;    // load: shard-file reads into the block's slots
     double task_write_s = 0;   // flush: shard-file writes (+ fsync)
     double task_codec_s = 0;   // the block's zero-copy GPU call, PCIe included
-    double task_copy_s = 0;    // VirtualFile::read: copy-out into the caller's buffer
+    double task_copy_s = 0;    // VirtualFile::read: copy-out into the caller's buffer (after the load)
+    double task_overlap_s = 0; // VirtualFile::read: copy-out of present shards while the GPU rebuilds
     double task_total_s = 0;   // whole tasks (the rest: locks, handles, buffer set-up)
     size_t tasks = 0;
 };

@@ -111,19 +111,23 @@ Result run_once(const std::shared_ptr<const ShmrFsConfig>& cfg, uint64_t ino, co
 // the best rep, per phase) and the phases' share of the task time.
 std::string tasks_json(const Result& r) {
     if (!r.load.tasks && !r.sync.tasks) return "";
-    char t[640];
+    char t[768];
     auto per = [](double s, size_t n) { return n ? s / double(n) * 1e3 : 0.0; };
     std::snprintf(t, sizeof t,
                   "\"per_block_tasks\": {\"unit\": \"ms of thread time per block\", "
                   "\"sync\": {\"tasks\": %zu, \"encode_call\": %.3f, \"shard_writes\": %.3f, \"other\": %.3f, "
                   "\"task\": %.3f}, "
-                  "\"read\": {\"tasks\": %zu, \"shard_reads\": %.3f, \"reconstruct_call\": %.3f, \"copy_out\": %.3f, "
-                  "\"other\": %.3f, \"task\": %.3f}, \"read_wall_ms\": %.2f, \"sync_wall_ms\": %.2f}, ",
+                  "\"read\": {\"tasks\": %zu, \"shard_reads\": %.3f, \"reconstruct_call\": %.3f, "
+                  "\"copy_out_during_rebuild\": %.3f, \"copy_out\": %.3f, \"other\": %.3f, \"task\": %.3f}, "
+                  "\"read_wall_ms\": %.2f, \"sync_wall_ms\": %.2f}, ",
                   r.sync.tasks, per(r.sync.task_codec_s, r.sync.tasks), per(r.sync.task_write_s, r.sync.tasks),
                   per(r.sync.task_total_s - r.sync.task_codec_s - r.sync.task_write_s, r.sync.tasks),
                   per(r.sync.task_total_s, r.sync.tasks), r.load.tasks, per(r.load.task_read_s, r.load.tasks),
-                  per(r.load.task_codec_s, r.load.tasks), per(r.load.task_copy_s, r.load.tasks),
-                  per(r.load.task_total_s - r.load.task_read_s - r.load.task_codec_s - r.load.task_copy_s, r.load.tasks),
+                  per(r.load.task_codec_s, r.load.tasks), per(r.load.task_overlap_s, r.load.tasks),
+                  per(r.load.task_copy_s, r.load.tasks),
+                  per(r.load.task_total_s - r.load.task_read_s - r.load.task_codec_s - r.load.task_overlap_s -
+                          r.load.task_copy_s,
+                      r.load.tasks),
                   per(r.load.task_total_s, r.load.tasks), r.read_s * 1e3, r.sync_s * 1e3);
     return t;
 }
