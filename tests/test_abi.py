@@ -461,3 +461,43 @@ def test_device_list_and_stats_api():
         assert T.shmr_ec_set_tuning(b"alias_devices", 33) == -100
         assert T.shmr_ec_set_tuning(b"alias_devices", 0) == 0
     assert L.shmr_ec_get_tuning(b"alias_devices") == 0
+
+
+def test_pointer_table_rows_follow_the_plan():
+    """Pointer tables go to the kernels in plan order (input t at [t], output
+    row r at [k + r], ec_core permute_ptr_rows): for random presence patterns
+    the permuted row names exactly the shards of the reconstruct plan the
+    library runs (shmr_ec_reconstruct_plan: the crate's first k present shards,
+    then the absent ones -- absent parity only without data_only), and encode
+    rows stay as given.  CPU only (the host side of *_ptrs_dev and of the
+    zero-copy mapped path)."""
+    L = _native.lib()
+    fn = L["_ZN4shmr4core16permute_ptr_rowsEPKmPKhmjjbPm"]   # shmr::core::permute_ptr_rows
+    fn.restype = None
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint, ctypes.c_uint, ctypes.c_bool,
+                   ctypes.c_void_p]
+    rng = np.random.default_rng(404)
+    for k, p in ((4, 2), (8, 3), (10, 4), (3, 5), (17, 7)):
+        t = k + p
+        rs = shmr_amd.ReedSolomon(k, p)
+        n = 40
+        src = (np.arange(n * t, dtype=np.uint64) + np.uint64(1 << 40)) * np.uint64(16)
+        present = np.ones((n, t), np.uint8)
+        for b in range(1, n):   # block 0 keeps every shard
+            lost = rng.choice(t, size=int(rng.integers(1, p + 1)), replace=False)
+            present[b, lost] = 0
+        for data_only in (False, True):
+            dst = np.zeros(n * t, np.uint64)
+            fn(src.ctypes.data, present.ctypes.data, n, k, t, data_only, dst.ctypes.data)
+            row = dst.reshape(n, t)
+            assert np.array_equal(row[0], src[:t])
+            for b in range(1, n):
+                in_idx, out_idx, _ = rs.reconstruct_plan(present[b].astype(bool), data_only=data_only)
+                base = src[b * t:(b + 1) * t]
+                assert np.array_equal(row[b, :k], base[list(in_idx)]), (k, p, b)
+                m = len(out_idx)
+                assert np.array_equal(row[b, k:k + m], base[list(out_idx)]), (k, p, b)
+                assert not row[b, k + m:].any()
+        enc = np.zeros(n * t, np.uint64)
+        fn(src.ctypes.data, None, n, k, t, False, enc.ctypes.data)
+        assert np.array_equal(enc, src)
