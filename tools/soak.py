@@ -3,8 +3,10 @@
 against the CPU oracle: per-block encode / reconstruct on pageable and mapped
 buffers (zero-copy, bounce, staged DMA), host batches on pageable arrays
 (pinned mirror) and mapped slabs, device-resident batches on per-thread
-torch streams, and per-shard device buffers through pointer tables (reused, so
-the device's table cache hits) -- several (k, p) codecs and shard lengths (aligned, tail,
+torch streams, per-shard device buffers through pointer tables (reused, so
+the device's table cache hits), started per-block calls (shmr_ec_*_start) and
+pointer-table encodes captured into graphs and destroyed again (the capture
+reserve) -- several (k, p) codecs and shard lengths (aligned, tail,
 byte-granular) at once.  Not part of the test suite (minutes of GPU time).
 
     python tools/soak.py [--seconds 120] [--threads 12]
@@ -45,7 +47,7 @@ def worker(tid, deadline, errors, counts):
     while time.time() < deadline and not errors:
         k, p, L = SHAPES[int(rng.integers(0, len(SHAPES)))]
         rs = shmr_amd.ReedSolomon(k, p)
-        op = int(rng.integers(0, 5))
+        op = int(rng.integers(0, 7))
         try:
             if op == 0:        # per-block calls, pageable or mapped
                 mapped = bool(rng.integers(0, 2))
@@ -93,6 +95,54 @@ def worker(tid, deadline, errors, counts):
                     want = oracle_encode(k, p, list(blk[b, :k]))
                     if not all(np.array_equal(blk[b, i], want[i]) for i in range(k, k + p)):
                         errors.append((tid, "mapped batch encode", k, p, L, B))
+            elif op == 5:      # started per-block calls (shmr_ec_*_start + shmr_ec_op_wait), mapped or pageable
+                import ctypes
+                from shmr_amd.reed_solomon import _ptr, _u8p
+                mapped = bool(rng.integers(0, 2))
+                if mapped:
+                    arr = slab.array[:(k + p) * L].reshape(k + p, L)
+                    shards = [arr[i] for i in range(k + p)]
+                else:
+                    shards = [np.zeros(L, np.uint8) for _ in range(k + p)]
+                for i in range(k):
+                    shards[i][:] = rng.integers(0, 256, L, dtype=np.uint8)
+                tab = (_u8p * (k + p))(*[_ptr(x) for x in shards])
+                lens = (ctypes.c_size_t * (k + p))(*([L] * (k + p)))
+                h = ctypes.c_void_p()
+                assert rs._L.shmr_ec_encode_start(rs._h, tab, lens, k + p, ctypes.byref(h)) == 0
+                assert rs._L.shmr_ec_op_wait(h) == 0
+                want = oracle_encode(k, p, shards[:k])
+                if not all(np.array_equal(shards[i], want[i]) for i in range(k, k + p)):
+                    errors.append((tid, "encode_start", k, p, L, mapped))
+                present = np.ones(k + p, np.uint8)
+                present[rng.choice(k + p, size=int(rng.integers(1, p + 1)), replace=False)] = 0
+                for i in np.flatnonzero(present == 0):
+                    shards[i][:] = 0xEE
+                    lens[i] = 0
+                assert rs._L.shmr_ec_reconstruct_start(rs._h, tab, lens, _ptr(present), k + p, 0, ctypes.byref(h)) == 0
+                assert rs._L.shmr_ec_op_wait(h) == 0
+                if not all(np.array_equal(shards[i], want[i]) for i in range(k + p)):
+                    errors.append((tid, "reconstruct_start", k, p, L, mapped))
+            elif op == 6:      # a pointer-table encode captured into a graph (capture reserve), replayed, destroyed
+                B = int(rng.integers(1, 5))
+                blocks = [[torch.zeros(L, dtype=torch.uint8, device="cuda") for _ in range(k + p)] for _ in range(B)]
+                host = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+                with torch.cuda.stream(stream):
+                    for b in range(B):
+                        for i in range(k):
+                            blocks[b][i].copy_(torch.from_numpy(host[b, i]).cuda())
+                stream.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=stream, capture_error_mode="thread_local"):
+                    rs.encode_ptrs_dev(blocks)
+                g.replay()
+                stream.synchronize()
+                for b in range(B):
+                    want = oracle_encode(k, p, list(host[b]))
+                    if not all(np.array_equal(blocks[b][i].cpu().numpy(), want[i]) for i in range(k, k + p)):
+                        errors.append((tid, "captured ptrs encode", k, p, L, B))
+                        break
+                del g
             elif op == 4:      # per-shard device buffers (pointer tables), on this thread's stream or the default one
                 key = (k, p, L, int(rng.integers(0, 3)))
                 if key not in kept:
@@ -181,7 +231,9 @@ def main():
     zc, st = shmr_amd.path_stats()
     print(json.dumps({"ops": sum(counts), "threads": a.threads, "seconds": a.seconds, "errors": errors[:5],
                       "zero_copy_blocks": zc, "staged_blocks": st,
-                      "ptr_table_hits": shmr_amd.device_stats(0)["ptr_table_hits"]}), flush=True)
+                      "ptr_table_hits": shmr_amd.device_stats(0)["ptr_table_hits"],
+                      "capture_tables": shmr_amd.device_stats(0)["capture_tables"],
+                      "capture_released": shmr_amd.device_stats(0)["capture_released"]}), flush=True)
     sys.exit(1 if errors else 0)
 
 
