@@ -39,6 +39,62 @@ def oracle_encode(k, p, data):
     return sh
 
 
+class CaptureGate:
+    """Graph captures (op 6) against the legacy default stream: torch work on the
+    null stream (op 4's default-stream branch, the .cpu() reads and allocations
+    outside a stream context in ops 3-4) synchronises implicitly with every
+    stream and would join -- and invalidate -- another thread's capture (a
+    HIP / CUDA rule, not the library's).  Captures run exclusively against ops
+    3-4; the host-buffer ops (0-2, 5), which use only the library's own
+    non-blocking streams, run alongside them."""
+
+    def __init__(self):
+        self.cv = threading.Condition()
+        self.readers = 0
+        self.writer = False
+
+    def shared(self):
+        gate = self
+
+        class _S:
+            def __enter__(self):
+                with gate.cv:
+                    gate.cv.wait_for(lambda: not gate.writer)
+                    gate.readers += 1
+
+            def __exit__(self, *exc):
+                with gate.cv:
+                    gate.readers -= 1
+                    gate.cv.notify_all()
+        return _S()
+
+    def exclusive(self):
+        gate = self
+
+        class _X:
+            def __enter__(self):
+                with gate.cv:
+                    gate.cv.wait_for(lambda: not gate.writer and gate.readers == 0)
+                    gate.writer = True
+
+            def __exit__(self, *exc):
+                with gate.cv:
+                    gate.writer = False
+                    gate.cv.notify_all()
+        return _X()
+
+
+GATE = CaptureGate()
+
+
+class _Nothing:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
+
+
 def worker(tid, deadline, errors, counts):
     rng = np.random.default_rng([tid, 2024])
     stream = torch.cuda.Stream()
@@ -48,166 +104,168 @@ def worker(tid, deadline, errors, counts):
         k, p, L = SHAPES[int(rng.integers(0, len(SHAPES)))]
         rs = shmr_amd.ReedSolomon(k, p)
         op = int(rng.integers(0, 7))
+        gate = GATE.exclusive() if op == 6 else GATE.shared() if op in (3, 4) else _Nothing()
         try:
-            if op == 0:        # per-block calls, pageable or mapped
-                mapped = bool(rng.integers(0, 2))
-                if mapped:
-                    arr = slab.array[:(k + p) * L].reshape(k + p, L)
-                    shards = [arr[i] for i in range(k + p)]
-                else:
-                    shards = [np.zeros(L, np.uint8) for _ in range(k + p)]
-                for i in range(k):
-                    shards[i][:] = rng.integers(0, 256, L, dtype=np.uint8)
-                rs.encode(shards)
-                want = oracle_encode(k, p, shards[:k])
-                if not all(np.array_equal(shards[i], want[i]) for i in range(k, k + p)):
-                    errors.append((tid, "encode", k, p, L, mapped))
-                lost = rng.choice(k + p, size=int(rng.integers(1, p + 1)), replace=False)
-                got = [None if i in lost else shards[i].copy() for i in range(k + p)]
-                rs.reconstruct(got)
-                if not all(np.array_equal(got[i], want[i]) for i in range(k + p)):
-                    errors.append((tid, "reconstruct", k, p, L, mapped))
-            elif op == 1:      # host batch on a pageable [B, t, L] array (pinned mirror)
-                B = int(rng.integers(1, 6))
-                blk = np.zeros((B, k + p, L), np.uint8)
-                blk[:, :k] = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
-                rs.encode_blocks_host(blk)
-                full = blk.copy()
-                for b in range(B):
-                    want = oracle_encode(k, p, list(blk[b, :k]))
-                    if not all(np.array_equal(blk[b, i], want[i]) for i in range(k, k + p)):
-                        errors.append((tid, "blocks_host encode", k, p, L, B))
-                present = np.ones((B, k + p), np.uint8)
-                for b in range(B):
-                    present[b, rng.choice(k + p, size=int(rng.integers(1, p + 1)), replace=False)] = 0
-                blk[present == 0] = 0
-                rs.reconstruct_blocks_host(blk, present)
-                if not np.array_equal(blk, full):
-                    errors.append((tid, "blocks_host reconstruct", k, p, L, B))
-            elif op == 2:      # host batch on the mapped slab (zero-copy)
-                B = int(min(4, (slab.nbytes // ((k + p) * L))))
-                if B == 0:
-                    continue
-                blk = slab.array[:B * (k + p) * L].reshape(B, k + p, L)
-                blk[:, :k] = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
-                rs.encode_blocks_host(blk)
-                for b in range(B):
-                    want = oracle_encode(k, p, list(blk[b, :k]))
-                    if not all(np.array_equal(blk[b, i], want[i]) for i in range(k, k + p)):
-                        errors.append((tid, "mapped batch encode", k, p, L, B))
-            elif op == 5:      # started per-block calls (shmr_ec_*_start + shmr_ec_op_wait), mapped or pageable
-                import ctypes
-                from shmr_amd.reed_solomon import _ptr, _u8p
-                mapped = bool(rng.integers(0, 2))
-                if mapped:
-                    arr = slab.array[:(k + p) * L].reshape(k + p, L)
-                    shards = [arr[i] for i in range(k + p)]
-                else:
-                    shards = [np.zeros(L, np.uint8) for _ in range(k + p)]
-                for i in range(k):
-                    shards[i][:] = rng.integers(0, 256, L, dtype=np.uint8)
-                tab = (_u8p * (k + p))(*[_ptr(x) for x in shards])
-                lens = (ctypes.c_size_t * (k + p))(*([L] * (k + p)))
-                h = ctypes.c_void_p()
-                assert rs._L.shmr_ec_encode_start(rs._h, tab, lens, k + p, ctypes.byref(h)) == 0
-                assert rs._L.shmr_ec_op_wait(h) == 0
-                want = oracle_encode(k, p, shards[:k])
-                if not all(np.array_equal(shards[i], want[i]) for i in range(k, k + p)):
-                    errors.append((tid, "encode_start", k, p, L, mapped))
-                present = np.ones(k + p, np.uint8)
-                present[rng.choice(k + p, size=int(rng.integers(1, p + 1)), replace=False)] = 0
-                for i in np.flatnonzero(present == 0):
-                    shards[i][:] = 0xEE
-                    lens[i] = 0
-                assert rs._L.shmr_ec_reconstruct_start(rs._h, tab, lens, _ptr(present), k + p, 0, ctypes.byref(h)) == 0
-                assert rs._L.shmr_ec_op_wait(h) == 0
-                if not all(np.array_equal(shards[i], want[i]) for i in range(k + p)):
-                    errors.append((tid, "reconstruct_start", k, p, L, mapped))
-            elif op == 6:      # a pointer-table encode captured into a graph (capture reserve), replayed, destroyed
-                B = int(rng.integers(1, 5))
-                blocks = [[torch.zeros(L, dtype=torch.uint8, device="cuda") for _ in range(k + p)] for _ in range(B)]
-                host = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
-                with torch.cuda.stream(stream):
-                    for b in range(B):
-                        for i in range(k):
-                            blocks[b][i].copy_(torch.from_numpy(host[b, i]).cuda())
-                stream.synchronize()
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=stream, capture_error_mode="thread_local"):
-                    rs.encode_ptrs_dev(blocks)
-                g.replay()
-                stream.synchronize()
-                for b in range(B):
-                    want = oracle_encode(k, p, list(host[b]))
-                    if not all(np.array_equal(blocks[b][i].cpu().numpy(), want[i]) for i in range(k, k + p)):
-                        errors.append((tid, "captured ptrs encode", k, p, L, B))
-                        break
-                del g
-            elif op == 4:      # per-shard device buffers (pointer tables), on this thread's stream or the default one
-                key = (k, p, L, int(rng.integers(0, 3)))
-                if key not in kept:
+            with gate:
+                if op == 0:        # per-block calls, pageable or mapped
+                    mapped = bool(rng.integers(0, 2))
+                    if mapped:
+                        arr = slab.array[:(k + p) * L].reshape(k + p, L)
+                        shards = [arr[i] for i in range(k + p)]
+                    else:
+                        shards = [np.zeros(L, np.uint8) for _ in range(k + p)]
+                    for i in range(k):
+                        shards[i][:] = rng.integers(0, 256, L, dtype=np.uint8)
+                    rs.encode(shards)
+                    want = oracle_encode(k, p, shards[:k])
+                    if not all(np.array_equal(shards[i], want[i]) for i in range(k, k + p)):
+                        errors.append((tid, "encode", k, p, L, mapped))
+                    lost = rng.choice(k + p, size=int(rng.integers(1, p + 1)), replace=False)
+                    got = [None if i in lost else shards[i].copy() for i in range(k + p)]
+                    rs.reconstruct(got)
+                    if not all(np.array_equal(got[i], want[i]) for i in range(k + p)):
+                        errors.append((tid, "reconstruct", k, p, L, mapped))
+                elif op == 1:      # host batch on a pageable [B, t, L] array (pinned mirror)
                     B = int(rng.integers(1, 6))
-                    kept[key] = [[torch.empty(L, dtype=torch.uint8, device="cuda") for _ in range(k + p)]
-                                 for _ in range(B)]
-                blocks = kept[key]
-                B = len(blocks)
-                host = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
-                st = stream if rng.integers(0, 4) else torch.cuda.current_stream()
-                with torch.cuda.stream(st):
+                    blk = np.zeros((B, k + p, L), np.uint8)
+                    blk[:, :k] = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+                    rs.encode_blocks_host(blk)
+                    full = blk.copy()
                     for b in range(B):
-                        for i in range(k):
-                            blocks[b][i].copy_(torch.from_numpy(host[b, i]).cuda(), non_blocking=False)
-                    rs.encode_ptrs_dev(blocks)
-                    lost = [sorted(rng.choice(k + p, size=int(rng.integers(1, p + 1)), replace=False).tolist())
-                            for _ in range(B)]
-                    partial = [[None if i in lost[b] else blocks[b][i] for i in range(k + p)] for b in range(B)]
-                    rs.reconstruct_ptrs_dev(partial)
-                st.synchronize()
-                for b in range(B):
-                    want = oracle_encode(k, p, list(host[b]))
-                    if not all(np.array_equal(blocks[b][i].cpu().numpy(), want[i]) for i in range(k, k + p)):
-                        errors.append((tid, "ptrs encode", k, p, L, B))
-                        break
-                    if not all(np.array_equal(partial[b][i].cpu().numpy(), want[i]) for i in lost[b]):
-                        errors.append((tid, "ptrs reconstruct", k, p, L, B))
-                        break
-            else:              # device-resident batch on this thread's stream: encode, in-place and compact rebuild
-                B = int(rng.integers(1, 9))
-                P = (L + 255) // 256 * 256
-                with torch.cuda.stream(stream):
-                    d = torch.zeros((B, k + p, P), dtype=torch.uint8, device="cuda")
-                    host = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
-                    d[:, :k, :L] = torch.from_numpy(host).cuda()
-                    rs.encode_batch_dev(d[:, :k], d[:, k:], shard_len=L)
+                        want = oracle_encode(k, p, list(blk[b, :k]))
+                        if not all(np.array_equal(blk[b, i], want[i]) for i in range(k, k + p)):
+                            errors.append((tid, "blocks_host encode", k, p, L, B))
                     present = np.ones((B, k + p), np.uint8)
                     for b in range(B):
                         present[b, rng.choice(k + p, size=int(rng.integers(1, p + 1)), replace=False)] = 0
-                    full = d.clone()
-                    erased = torch.from_numpy(present == 0).cuda()
-                    d[erased] = 0
-                    rs.reconstruct_batch_dev(d, present, shard_len=L)
-                    ok = torch.equal(d[:, :, :L], full[:, :, :L])
-                    # compact rebuild (the crate's fresh-buffer semantics) from a copy
-                    # whose erased slots are poisoned: they must not be read
-                    src = full.clone()
-                    src[erased] = 0xEE
-                    out = torch.zeros((B, int((present == 0).sum(axis=1).max()), P), dtype=torch.uint8, device="cuda")
-                    rs.reconstruct_batch_dev_out(src, present, out, shard_len=L)
-                stream.synchronize()
-                h = full.cpu().numpy()
-                ho = out.cpu().numpy()
-                for b in range(B):
-                    for j, i in enumerate(np.flatnonzero(present[b] == 0)):
-                        if not np.array_equal(ho[b, j, :L], h[b, i, :L]):
-                            errors.append((tid, "batch_dev compact", k, p, L, B))
+                    blk[present == 0] = 0
+                    rs.reconstruct_blocks_host(blk, present)
+                    if not np.array_equal(blk, full):
+                        errors.append((tid, "blocks_host reconstruct", k, p, L, B))
+                elif op == 2:      # host batch on the mapped slab (zero-copy)
+                    B = int(min(4, (slab.nbytes // ((k + p) * L))))
+                    if B == 0:
+                        continue
+                    blk = slab.array[:B * (k + p) * L].reshape(B, k + p, L)
+                    blk[:, :k] = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+                    rs.encode_blocks_host(blk)
+                    for b in range(B):
+                        want = oracle_encode(k, p, list(blk[b, :k]))
+                        if not all(np.array_equal(blk[b, i], want[i]) for i in range(k, k + p)):
+                            errors.append((tid, "mapped batch encode", k, p, L, B))
+                elif op == 5:      # started per-block calls (shmr_ec_*_start + shmr_ec_op_wait), mapped or pageable
+                    import ctypes
+                    from shmr_amd.reed_solomon import _ptr, _u8p
+                    mapped = bool(rng.integers(0, 2))
+                    if mapped:
+                        arr = slab.array[:(k + p) * L].reshape(k + p, L)
+                        shards = [arr[i] for i in range(k + p)]
+                    else:
+                        shards = [np.zeros(L, np.uint8) for _ in range(k + p)]
+                    for i in range(k):
+                        shards[i][:] = rng.integers(0, 256, L, dtype=np.uint8)
+                    tab = (_u8p * (k + p))(*[_ptr(x) for x in shards])
+                    lens = (ctypes.c_size_t * (k + p))(*([L] * (k + p)))
+                    h = ctypes.c_void_p()
+                    assert rs._L.shmr_ec_encode_start(rs._h, tab, lens, k + p, ctypes.byref(h)) == 0
+                    assert rs._L.shmr_ec_op_wait(h) == 0
+                    want = oracle_encode(k, p, shards[:k])
+                    if not all(np.array_equal(shards[i], want[i]) for i in range(k, k + p)):
+                        errors.append((tid, "encode_start", k, p, L, mapped))
+                    present = np.ones(k + p, np.uint8)
+                    present[rng.choice(k + p, size=int(rng.integers(1, p + 1)), replace=False)] = 0
+                    for i in np.flatnonzero(present == 0):
+                        shards[i][:] = 0xEE
+                        lens[i] = 0
+                    assert rs._L.shmr_ec_reconstruct_start(rs._h, tab, lens, _ptr(present), k + p, 0, ctypes.byref(h)) == 0
+                    assert rs._L.shmr_ec_op_wait(h) == 0
+                    if not all(np.array_equal(shards[i], want[i]) for i in range(k + p)):
+                        errors.append((tid, "reconstruct_start", k, p, L, mapped))
+                elif op == 6:      # a pointer-table encode captured into a graph (capture reserve), replayed, destroyed
+                    B = int(rng.integers(1, 5))
+                    blocks = [[torch.zeros(L, dtype=torch.uint8, device="cuda") for _ in range(k + p)] for _ in range(B)]
+                    host = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+                    with torch.cuda.stream(stream):
+                        for b in range(B):
+                            for i in range(k):
+                                blocks[b][i].copy_(torch.from_numpy(host[b, i]).cuda())
+                    stream.synchronize()
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=stream, capture_error_mode="thread_local"):
+                        rs.encode_ptrs_dev(blocks)
+                    g.replay()
+                    stream.synchronize()
+                    for b in range(B):
+                        want = oracle_encode(k, p, list(host[b]))
+                        if not all(np.array_equal(blocks[b][i].cpu().numpy(), want[i]) for i in range(k, k + p)):
+                            errors.append((tid, "captured ptrs encode", k, p, L, B))
                             break
-                for b in range(B):
-                    want = oracle_encode(k, p, list(host[b]))
-                    if not all(np.array_equal(h[b, i, :L], want[i]) for i in range(k, k + p)):
-                        errors.append((tid, "batch_dev encode", k, p, L, B))
-                if not ok:
-                    errors.append((tid, "batch_dev reconstruct", k, p, L, B))
-            counts[tid] += 1
+                    del g
+                elif op == 4:      # per-shard device buffers (pointer tables), on this thread's stream or the default one
+                    key = (k, p, L, int(rng.integers(0, 3)))
+                    if key not in kept:
+                        B = int(rng.integers(1, 6))
+                        kept[key] = [[torch.empty(L, dtype=torch.uint8, device="cuda") for _ in range(k + p)]
+                                     for _ in range(B)]
+                    blocks = kept[key]
+                    B = len(blocks)
+                    host = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+                    st = stream if rng.integers(0, 4) else torch.cuda.current_stream()
+                    with torch.cuda.stream(st):
+                        for b in range(B):
+                            for i in range(k):
+                                blocks[b][i].copy_(torch.from_numpy(host[b, i]).cuda(), non_blocking=False)
+                        rs.encode_ptrs_dev(blocks)
+                        lost = [sorted(rng.choice(k + p, size=int(rng.integers(1, p + 1)), replace=False).tolist())
+                                for _ in range(B)]
+                        partial = [[None if i in lost[b] else blocks[b][i] for i in range(k + p)] for b in range(B)]
+                        rs.reconstruct_ptrs_dev(partial)
+                    st.synchronize()
+                    for b in range(B):
+                        want = oracle_encode(k, p, list(host[b]))
+                        if not all(np.array_equal(blocks[b][i].cpu().numpy(), want[i]) for i in range(k, k + p)):
+                            errors.append((tid, "ptrs encode", k, p, L, B))
+                            break
+                        if not all(np.array_equal(partial[b][i].cpu().numpy(), want[i]) for i in lost[b]):
+                            errors.append((tid, "ptrs reconstruct", k, p, L, B))
+                            break
+                else:              # device-resident batch on this thread's stream: encode, in-place and compact rebuild
+                    B = int(rng.integers(1, 9))
+                    P = (L + 255) // 256 * 256
+                    with torch.cuda.stream(stream):
+                        d = torch.zeros((B, k + p, P), dtype=torch.uint8, device="cuda")
+                        host = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+                        d[:, :k, :L] = torch.from_numpy(host).cuda()
+                        rs.encode_batch_dev(d[:, :k], d[:, k:], shard_len=L)
+                        present = np.ones((B, k + p), np.uint8)
+                        for b in range(B):
+                            present[b, rng.choice(k + p, size=int(rng.integers(1, p + 1)), replace=False)] = 0
+                        full = d.clone()
+                        erased = torch.from_numpy(present == 0).cuda()
+                        d[erased] = 0
+                        rs.reconstruct_batch_dev(d, present, shard_len=L)
+                        ok = torch.equal(d[:, :, :L], full[:, :, :L])
+                        # compact rebuild (the crate's fresh-buffer semantics) from a copy
+                        # whose erased slots are poisoned: they must not be read
+                        src = full.clone()
+                        src[erased] = 0xEE
+                        out = torch.zeros((B, int((present == 0).sum(axis=1).max()), P), dtype=torch.uint8, device="cuda")
+                        rs.reconstruct_batch_dev_out(src, present, out, shard_len=L)
+                    stream.synchronize()
+                    h = full.cpu().numpy()
+                    ho = out.cpu().numpy()
+                    for b in range(B):
+                        for j, i in enumerate(np.flatnonzero(present[b] == 0)):
+                            if not np.array_equal(ho[b, j, :L], h[b, i, :L]):
+                                errors.append((tid, "batch_dev compact", k, p, L, B))
+                                break
+                    for b in range(B):
+                        want = oracle_encode(k, p, list(host[b]))
+                        if not all(np.array_equal(h[b, i, :L], want[i]) for i in range(k, k + p)):
+                            errors.append((tid, "batch_dev encode", k, p, L, B))
+                    if not ok:
+                        errors.append((tid, "batch_dev reconstruct", k, p, L, B))
+                counts[tid] += 1
         except Exception as e:   # surfaced by the main thread
             errors.append((tid, "exception", op, k, p, L, repr(e)))
 
