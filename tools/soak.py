@@ -183,9 +183,12 @@ def worker(tid, deadline, errors, counts):
                         errors.append((tid, "reconstruct_start", k, p, L, mapped))
                 elif op == 6:      # a pointer-table encode captured into a graph (capture reserve), replayed, destroyed
                     B = int(rng.integers(1, 5))
-                    blocks = [[torch.zeros(L, dtype=torch.uint8, device="cuda") for _ in range(k + p)] for _ in range(B)]
                     host = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+                    # allocated and filled on this thread's stream (a fill on the legacy
+                    # stream would race the non-blocking stream's copies)
                     with torch.cuda.stream(stream):
+                        blocks = [[torch.empty(L, dtype=torch.uint8, device="cuda") for _ in range(k + p)]
+                                  for _ in range(B)]
                         for b in range(B):
                             for i in range(k):
                                 blocks[b][i].copy_(torch.from_numpy(host[b, i]).cuda())
