@@ -246,6 +246,7 @@ int shmr_ec_device_alloc(int device, size_t bytes, int contiguous, void** out) {
             core::DeviceScope scope(device);
             if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
             const size_t n = bytes ? bytes : 1;
+            core::RelaxedCapture relaxed;
             e = contiguous ? hipExtMallocWithFlags(out, n, hipDeviceMallocContiguous) : hipMalloc(out, n);
         }
         if (e != hipSuccess) {
@@ -264,7 +265,10 @@ int shmr_ec_device_free(int device, void* p) {
         if (rc) return rc;
         core::DeviceScope scope(device);
         if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
-        return hipFree(p) == hipSuccess ? SHMR_EC_OK : SHMR_EC_DEVICE_ERROR;
+        core::RelaxedCapture relaxed;
+        if (hipFree(p) == hipSuccess) return SHMR_EC_OK;
+        (void)hipGetLastError();
+        return SHMR_EC_DEVICE_ERROR;
     });
 }
 
@@ -278,7 +282,9 @@ int shmr_ec_host_alloc(size_t bytes, void** out) {
         int rc = core::check_device(0);
         if (rc) return rc;
         const size_t n = bytes ? bytes : 1;
+        core::RelaxedCapture relaxed;
         if (hipHostMalloc(out, n, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) {
+            (void)hipGetLastError();
             *out = nullptr;
             return SHMR_EC_OUT_OF_MEMORY;
         }
@@ -301,7 +307,8 @@ int shmr_ec_host_alloc(size_t bytes, void** out) {
 void shmr_ec_host_free(void* p) {
     if (!p) return;
     core::mapped_remove(p);
-    (void)hipHostFree(p);
+    core::RelaxedCapture relaxed;
+    if (hipHostFree(p) != hipSuccess) (void)hipGetLastError();
 }
 
 int shmr_ec_host_register(void* p, size_t bytes) {
@@ -309,6 +316,7 @@ int shmr_ec_host_register(void* p, size_t bytes) {
         if (!p || bytes == 0) return SHMR_EC_INVALID_ARGUMENT;
         int rc = core::check_device(0);
         if (rc) return rc;
+        core::RelaxedCapture relaxed;
         if (hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable) != hipSuccess) {
             (void)hipGetLastError();
             return SHMR_EC_DEVICE_ERROR;
@@ -332,7 +340,10 @@ int shmr_ec_host_register(void* p, size_t bytes) {
 int shmr_ec_host_unregister(void* p) {
     return guarded([&]() -> int {
         if (!p || !core::mapped_remove(p)) return SHMR_EC_INVALID_ARGUMENT;
-        return hipHostUnregister(p) == hipSuccess ? SHMR_EC_OK : SHMR_EC_DEVICE_ERROR;
+        core::RelaxedCapture relaxed;
+        if (hipHostUnregister(p) == hipSuccess) return SHMR_EC_OK;
+        (void)hipGetLastError();
+        return SHMR_EC_DEVICE_ERROR;
     });
 }
 

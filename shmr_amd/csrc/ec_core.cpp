@@ -460,6 +460,7 @@ DeviceState* state_of(int dev) {
 
 // Blocking: pinned + device allocation.  Caller holds ds.mu (or owns ds).
 int add_chunk(DeviceState& ds, size_t bytes) {
+    RelaxedCapture relaxed;
     ArenaChunk c;
     c.cap = std::max(round_up(bytes, kArenaAlign), kArenaChunk);
     count_device(ds.dev, kDevBlockingCalls, 2);
@@ -480,6 +481,7 @@ constexpr size_t kCaptureChunk = size_t(4) << 20;   // the reserve device init c
 
 // Blocking: pinned + device allocation.  Caller holds ds.cmu (or owns ds).
 int add_capture_chunk(DeviceState& ds, size_t bytes) {
+    RelaxedCapture relaxed;
     auto* c = new CaptureChunk;
     c->cap = round_up(bytes, kArenaAlign);
     count_device(ds.dev, kDevBlockingCalls, 2);
@@ -570,6 +572,7 @@ int device_init(int dev, hipStream_t caller) {
     }
     DeviceScope scope(dev);
     if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
+    RelaxedCapture relaxed;
     auto* ds = new DeviceState;
     ds->dev = dev;
     count_device(dev, kDevBlockingCalls);
@@ -722,9 +725,12 @@ int upload_plan(PlanDev& pd, hipStream_t stream, bool capturing) {
         return SHMR_EC_DEVICE_ERROR;
     }
     if (capturing) return SHMR_EC_OK;   // a graph node: same bytes on every replay
-    if (!pd.ready && hipEventCreateWithFlags(&pd.ready, hipEventDisableTiming) != hipSuccess) {
-        (void)hipGetLastError();
-        return SHMR_EC_DEVICE_ERROR;
+    if (!pd.ready) {
+        RelaxedCapture relaxed;
+        if (hipEventCreateWithFlags(&pd.ready, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            return SHMR_EC_DEVICE_ERROR;
+        }
     }
     if (hipEventRecord(pd.ready, stream) != hipSuccess) {
         (void)hipGetLastError();
@@ -1124,6 +1130,7 @@ UploadRing* UploadRing::for_device(int dev, int* rc, Kind kind) {
     std::lock_guard<std::mutex> lock(mu);
     auto& r = (*rings)[{dev, int(kind)}];
     if (!r) {
+        RelaxedCapture relaxed;
         auto* ring = new UploadRing;
         ring->dev_id_ = dev;
         // on failure nothing is kept: the next call retries from scratch
@@ -1132,6 +1139,7 @@ UploadRing* UploadRing::for_device(int dev, int* rc, Kind kind) {
                 if (ring->ev_[i]) (void)hipEventDestroy(ring->ev_[i]);
             if (ring->dev_) (void)hipFree(ring->dev_);
             if (ring->host_) (void)hipHostFree(ring->host_);
+            (void)hipGetLastError();
             delete ring;
             *rc = code;
             return nullptr;
@@ -1290,6 +1298,7 @@ int PtrTableCache::lookup(const void* tab, size_t bytes, hipStream_t stream, con
         // (no arena memory or events for a new entry: the caller takes the upload ring)
         uint8_t *h = nullptr, *d = nullptr;
         if (arena_alloc(dev_id_, UploadRing::kSlotBytes, false, &h, &d) != SHMR_EC_OK) return SHMR_EC_OK;
+        RelaxedCapture relaxed;
         if (hipEventCreateWithFlags(&e.up, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&e.used, hipEventDisableTiming) != hipSuccess) {
             (void)hipGetLastError();
@@ -1348,10 +1357,12 @@ Staging* StagingPool::acquire(int dev, size_t bytes, int* rc) {
             lst.pop_back();
         }
     }
+    RelaxedCapture relaxed;
     if (!s) {
         s = new Staging;
         s->dev = dev;
         if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+            (void)hipGetLastError();
             delete s;
             *rc = SHMR_EC_DEVICE_ERROR;
             return nullptr;
@@ -1359,10 +1370,11 @@ Staging* StagingPool::acquire(int dev, size_t bytes, int* rc) {
         count_device(dev, kDevStagingStreams);
     }
     if (s->cap < bytes) {
-        if (s->dbuf) (void)hipFree(s->dbuf);
+        if (s->dbuf && hipFree(s->dbuf) != hipSuccess) (void)hipGetLastError();
         s->dbuf = nullptr;
         s->cap = 0;
         if (hipMalloc(reinterpret_cast<void**>(&s->dbuf), bytes) != hipSuccess) {
+            (void)hipGetLastError();
             release(s);
             *rc = SHMR_EC_OUT_OF_MEMORY;
             return nullptr;

@@ -114,6 +114,29 @@ private:
     bool ok_ = false;
 };
 
+// Runs the library's own allocation calls (hipMalloc / hipFree / hipHostMalloc /
+// hipHostRegister and their releases, stream and event creation) under the
+// relaxed stream-capture mode, restoring the thread's mode after.  Under the
+// default (global) mode HIP refuses such a call while ANY thread of the
+// process captures a graph -- and the refused call invalidates that capture
+// -- although none of these buffers belongs to a captured sequence.  A
+// caller's own capture is checked separately (capture_state): nothing
+// allocates inside it.
+class RelaxedCapture {
+public:
+    RelaxedCapture() {
+        ok_ = hipThreadExchangeStreamCaptureMode(&prev_) == hipSuccess;
+        if (!ok_) (void)hipGetLastError();
+    }
+    ~RelaxedCapture() {
+        if (ok_) (void)hipThreadExchangeStreamCaptureMode(&prev_);
+    }
+
+private:
+    hipStreamCaptureMode prev_ = hipStreamCaptureModeRelaxed;
+    bool ok_ = false;
+};
+
 // ---- per-device state --------------------------------------------------------
 // Created once per device ID, by the first call that touches the device or by
 // shmr_ec_device_init, synchronously and on a private stream (never the

@@ -132,28 +132,36 @@ struct DevicePipe {
     std::mutex mu;
     StageSet sets[kStageSets];
     int ensure(int dev, size_t dbytes, size_t hbytes) {
+        RelaxedCapture relaxed;
         for (auto& s : sets) {
             if (!s.stream) {
                 if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
-                    hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess)
+                    hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) {
+                    (void)hipGetLastError();
                     return SHMR_EC_DEVICE_ERROR;
+                }
                 count_device(dev, kDevStagingStreams);
             }
             if (s.dcap < dbytes) {
-                if (s.dbuf) (void)hipFree(s.dbuf);
+                if (s.dbuf && hipFree(s.dbuf) != hipSuccess) (void)hipGetLastError();
                 s.dbuf = nullptr;
                 s.dcap = 0;
-                if (hipMalloc(reinterpret_cast<void**>(&s.dbuf), dbytes) != hipSuccess) return SHMR_EC_OUT_OF_MEMORY;
+                if (hipMalloc(reinterpret_cast<void**>(&s.dbuf), dbytes) != hipSuccess) {
+                    (void)hipGetLastError();
+                    return SHMR_EC_OUT_OF_MEMORY;
+                }
                 s.dcap = dbytes;
             }
             if (s.hcap < hbytes) {
-                if (s.hbuf) (void)hipHostFree(s.hbuf);
+                if (s.hbuf && hipHostFree(s.hbuf) != hipSuccess) (void)hipGetLastError();
                 s.hbuf = nullptr;
                 s.hcap = 0;
                 s.hbuf_unified = false;
                 if (hipHostMalloc(reinterpret_cast<void**>(&s.hbuf), hbytes,
-                                  hipHostMallocMapped | hipHostMallocPortable) != hipSuccess)
+                                  hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) {
+                    (void)hipGetLastError();
                     return SHMR_EC_OUT_OF_MEMORY;
+                }
                 s.hcap = hbytes;
                 void* d = nullptr;
                 s.hbuf_unified = hipHostGetDevicePointer(&d, s.hbuf, 0) == hipSuccess && d == s.hbuf;
@@ -416,6 +424,7 @@ public:
                 }
         }
         void* p = nullptr;
+        RelaxedCapture relaxed;
         if (hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) {
             (void)hipGetLastError();
             return nullptr;
@@ -435,7 +444,8 @@ public:
         std::lock_guard<std::mutex> lock(mu_);
         if (free_.size() >= kKeep) {   // keep a bounded pool
             mapped_remove(p);
-            (void)hipHostFree(p);
+            RelaxedCapture relaxed;
+            if (hipHostFree(p) != hipSuccess) (void)hipGetLastError();
             size_.erase(p);
             return;
         }

@@ -268,3 +268,70 @@ def test_capture_reserve_reused_across_graphs_and_large_capture(gpu):
     assert np.array_equal(h[:, k:], _oracle_parity(k, p, h[:, :k]))
     del g
     gc.collect()
+
+
+@pytest.mark.parametrize("mode", ["global", "thread_local"])
+def test_library_allocations_while_another_thread_captures(gpu, mode):
+    """One thread holds a graph capture open while another makes calls that
+    allocate (device / mapped buffers, host registration, a fresh codec's
+    pageable per-block and batch calls that grow the staging buffers).  Under
+    the default capture mode HIP refuses such calls while any thread captures
+    and invalidates that capture; the library makes its own allocations under
+    the relaxed mode, so both sides succeed: every call exact, the capture
+    replays bit-exact (soak finding: tools/soak.py, profiles/r04/s6)."""
+    import threading
+    import torch
+    shmr_amd.device_init(0)
+    k, p, S, B = 8, 3, 65536, 4
+    rs = shmr_amd.ReedSolomon(k, p)
+    data = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=gpu)
+    parity = torch.zeros((B, p, S), dtype=torch.uint8, device=gpu)
+    torch.cuda.synchronize()
+    in_capture, done = threading.Event(), threading.Event()
+    results = {}
+
+    def other():
+        try:
+            assert in_capture.wait(60)
+            dev = shmr_amd.DeviceBuffer(48 << 20)
+            pin = shmr_amd.PinnedBuffer(24 << 20)
+            arr = np.zeros(8 << 20, np.uint8)
+            shmr_amd.host_register(arr)
+            shmr_amd.host_unregister(arr)
+            del dev, pin
+            # a codec and sizes no other test uses: fresh staging and plans
+            k2, p2, L2 = 13, 6, (3 << 20) + 4096
+            rs2 = shmr_amd.ReedSolomon(k2, p2)
+            rng = np.random.default_rng(31)
+            blk = np.zeros((3, k2 + p2, L2), np.uint8)
+            blk[:, :k2] = rng.integers(0, 256, (3, k2, L2), dtype=np.uint8)
+            rs2.encode_blocks_host(blk)
+            want = np.zeros((3, p2, L2), np.uint8)
+            c_oracle.encode_batch(k2, p2, np.ascontiguousarray(blk[:, :k2]), want, 3, L2, 8)
+            results["batch"] = np.array_equal(blk[:, k2:], want)
+            shards = [np.ascontiguousarray(blk[0, i]) for i in range(k2 + p2)]
+            for i in range(k2, k2 + p2):
+                shards[i][:] = 0
+            rs2.encode(shards)
+            results["block"] = all(np.array_equal(shards[k2 + r], want[0, r]) for r in range(p2))
+        except BaseException as e:   # reported by the capturing thread
+            results["error"] = repr(e)
+        finally:
+            done.set()
+
+    th = threading.Thread(target=other)
+    th.start()
+    graph = torch.cuda.CUDAGraph()
+    try:
+        with torch.cuda.graph(graph, stream=torch.cuda.Stream(), capture_error_mode=mode):
+            rs.encode_batch_dev(data, parity)
+            in_capture.set()
+            assert done.wait(120), "the other thread did not finish"
+    finally:
+        in_capture.set()
+        th.join(120)
+    assert "error" not in results, results
+    assert results == {"batch": True, "block": True}, results
+    graph.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(parity.cpu().numpy(), _oracle_parity(k, p, data.cpu().numpy()))
