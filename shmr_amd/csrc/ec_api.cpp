@@ -25,9 +25,11 @@ namespace core = shmr::core;
 namespace {
 // No C++ exception (allocation failure, thread or stream creation) crosses the
 // C ABI: it becomes a status code, so a Rust/C caller never sees an abort.
+// Every entry point runs under the relaxed capture mode (core::RelaxedCapture).
 template <class F>
 int guarded(F&& f) noexcept {
     try {
+        core::RelaxedCapture relaxed;
         return f();
     } catch (const std::bad_alloc&) {
         return SHMR_EC_OUT_OF_MEMORY;

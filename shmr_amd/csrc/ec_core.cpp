@@ -545,7 +545,12 @@ void release_capture_block(void* p) {
 int capture_state(hipStream_t stream, bool* capturing) {
     *capturing = false;
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    // under the mode the caller entered the library with (see RelaxedCapture)
+    const CaptureModeTls& t = capture_mode_tls();
+    hipStreamCaptureMode m = t.caller;
+    const bool swap = t.depth > 0 && hipThreadExchangeStreamCaptureMode(&m) == hipSuccess;
     const hipError_t e = hipStreamIsCapturing(stream, &st);
+    if (swap) (void)hipThreadExchangeStreamCaptureMode(&m);
     if (e != hipSuccess) {
         (void)hipGetLastError();
         // e.g. the legacy null stream while another thread captures in global

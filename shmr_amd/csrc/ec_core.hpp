@@ -114,23 +114,41 @@ private:
     bool ok_ = false;
 };
 
-// Runs the library's own allocation calls (hipMalloc / hipFree / hipHostMalloc /
-// hipHostRegister and their releases, stream and event creation) under the
-// relaxed stream-capture mode, restoring the thread's mode after.  Under the
-// default (global) mode HIP refuses such a call while ANY thread of the
-// process captures a graph -- and the refused call invalidates that capture
-// -- although none of these buffers belongs to a captured sequence.  A
-// caller's own capture is checked separately (capture_state): nothing
-// allocates inside it.
+// Every C-ABI entry point runs under the relaxed stream-capture mode (the
+// calling thread's mode is restored on return).  Under the default (global)
+// mode HIP refuses the library's allocation and synchronisation calls
+// (hipMalloc / hipFree / hipHostMalloc / hipHostRegister, hipStreamSynchronize
+// of its own streams ...) while ANY thread of the process captures a graph --
+// and the refused call invalidates that capture -- although none of them
+// touches a captured stream (measured: profiles/r04/s8, tools/capture_probe_hip.py).
+// The caller's own capture is checked separately, under the mode the caller
+// entered with (capture_state): nothing allocates or synchronises inside it.
+struct CaptureModeTls {
+    int depth = 0;
+    hipStreamCaptureMode caller = hipStreamCaptureModeGlobal;
+};
+inline CaptureModeTls& capture_mode_tls() {
+    static thread_local CaptureModeTls t;
+    return t;
+}
 class RelaxedCapture {
 public:
     RelaxedCapture() {
         ok_ = hipThreadExchangeStreamCaptureMode(&prev_) == hipSuccess;
-        if (!ok_) (void)hipGetLastError();
+        if (!ok_) {
+            (void)hipGetLastError();
+            return;
+        }
+        CaptureModeTls& t = capture_mode_tls();
+        if (t.depth++ == 0) t.caller = prev_;
     }
     ~RelaxedCapture() {
-        if (ok_) (void)hipThreadExchangeStreamCaptureMode(&prev_);
+        if (!ok_) return;
+        --capture_mode_tls().depth;
+        (void)hipThreadExchangeStreamCaptureMode(&prev_);
     }
+    RelaxedCapture(const RelaxedCapture&) = delete;
+    RelaxedCapture& operator=(const RelaxedCapture&) = delete;
 
 private:
     hipStreamCaptureMode prev_ = hipStreamCaptureModeRelaxed;
