@@ -562,6 +562,21 @@ int capture_state(hipStream_t stream, bool* capturing) {
     return SHMR_EC_OK;
 }
 
+int record_mirrored(int dev, hipStream_t stream, hipEvent_t on_caller, hipEvent_t mirror) {
+    DeviceState* ds = state_of(dev);
+    if (!ds) {
+        const int rc = device_init(dev, nullptr);
+        if (rc) return rc;
+        ds = state_of(dev);
+    }
+    if (hipEventRecord(on_caller, stream) != hipSuccess || hipStreamWaitEvent(ds->priv, on_caller, 0) != hipSuccess ||
+        hipEventRecord(mirror, ds->priv) != hipSuccess) {
+        (void)hipGetLastError();
+        return SHMR_EC_DEVICE_ERROR;
+    }
+    return SHMR_EC_OK;
+}
+
 int device_init(int dev, hipStream_t caller) {
     if (dev < 0 || dev >= kMaxDevIds) return SHMR_EC_INVALID_ARGUMENT;
     if (state_of(dev)) return SHMR_EC_OK;
@@ -721,10 +736,11 @@ struct PlanDev {
     size_t bytes = 0;
     enum State { kCaptured, kPending, kDone } state = kCaptured;
     hipStream_t stream = nullptr;
-    hipEvent_t ready = nullptr;
+    hipEvent_t ready = nullptr;    // recorded behind the upload on the caller's stream
+    hipEvent_t mready = nullptr;   // its mirror (record_mirrored): queried and waited on
 };
 
-int upload_plan(PlanDev& pd, hipStream_t stream, bool capturing) {
+int upload_plan(PlanDev& pd, int dev, hipStream_t stream, bool capturing) {
     if (hipMemcpyAsync(pd.dev, pd.host, pd.bytes, hipMemcpyHostToDevice, stream) != hipSuccess) {
         (void)hipGetLastError();
         return SHMR_EC_DEVICE_ERROR;
@@ -732,15 +748,14 @@ int upload_plan(PlanDev& pd, hipStream_t stream, bool capturing) {
     if (capturing) return SHMR_EC_OK;   // a graph node: same bytes on every replay
     if (!pd.ready) {
         RelaxedCapture relaxed;
-        if (hipEventCreateWithFlags(&pd.ready, hipEventDisableTiming) != hipSuccess) {
+        if (hipEventCreateWithFlags(&pd.ready, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&pd.mready, hipEventDisableTiming) != hipSuccess) {
             (void)hipGetLastError();
             return SHMR_EC_DEVICE_ERROR;
         }
     }
-    if (hipEventRecord(pd.ready, stream) != hipSuccess) {
-        (void)hipGetLastError();
-        return SHMR_EC_DEVICE_ERROR;
-    }
+    const int rc = record_mirrored(dev, stream, pd.ready, pd.mready);
+    if (rc) return rc;
     pd.state = PlanDev::kPending;
     pd.stream = stream;
     return SHMR_EC_OK;
@@ -766,16 +781,16 @@ int plan_on_device(Plan& plan, int dev, hipStream_t stream, bool compact, const 
         pd->bytes = img.size();
         slot = pd;
         count_device(dev, kDevPlanImages);
-        const int rc2 = upload_plan(*pd, stream, cap);
+        const int rc2 = upload_plan(*pd, dev, stream, cap);
         if (rc2) return rc2;
     } else if (pd->state == PlanDev::kPending && !cap) {
-        const hipError_t q = hipEventQuery(pd->ready);
+        const hipError_t q = hipEventQuery(pd->mready);
         if (q == hipSuccess) {
             pd->state = PlanDev::kDone;
         } else if (q == hipErrorNotReady) {
             (void)hipGetLastError();
             // still in flight on another stream: order this stream after it
-            if (pd->stream != stream && hipStreamWaitEvent(stream, pd->ready, 0) != hipSuccess) {
+            if (pd->stream != stream && hipStreamWaitEvent(stream, pd->mready, 0) != hipSuccess) {
                 (void)hipGetLastError();
                 return SHMR_EC_DEVICE_ERROR;
             }
@@ -786,7 +801,7 @@ int plan_on_device(Plan& plan, int dev, hipStream_t stream, bool compact, const 
     } else if (pd->state != PlanDev::kDone) {
         // captured-only upload, or capturing now before the eager upload is
         // known complete: (re)upload on this stream -- identical bytes
-        const int rc = upload_plan(*pd, stream, cap);
+        const int rc = upload_plan(*pd, dev, stream, cap);
         if (rc) return rc;
     }
     *out = pd->dev;
@@ -1140,8 +1155,10 @@ UploadRing* UploadRing::for_device(int dev, int* rc, Kind kind) {
         ring->dev_id_ = dev;
         // on failure nothing is kept: the next call retries from scratch
         auto give_up = [&](int code) -> UploadRing* {
-            for (int i = 0; i < kSlots; ++i)
+            for (int i = 0; i < kSlots; ++i) {
                 if (ring->ev_[i]) (void)hipEventDestroy(ring->ev_[i]);
+                if (ring->mev_[i]) (void)hipEventDestroy(ring->mev_[i]);
+            }
             if (ring->dev_) (void)hipFree(ring->dev_);
             if (ring->host_) (void)hipHostFree(ring->host_);
             (void)hipGetLastError();
@@ -1155,7 +1172,8 @@ UploadRing* UploadRing::for_device(int dev, int* rc, Kind kind) {
             hipMalloc(reinterpret_cast<void**>(&ring->dev_), kSlots * kSlotBytes) != hipSuccess)
             return give_up(SHMR_EC_OUT_OF_MEMORY);
         for (int i = 0; i < kSlots; ++i)
-            if (hipEventCreateWithFlags(&ring->ev_[i], hipEventDisableTiming) != hipSuccess)
+            if (hipEventCreateWithFlags(&ring->ev_[i], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&ring->mev_[i], hipEventDisableTiming) != hipSuccess)
                 return give_up(SHMR_EC_DEVICE_ERROR);
         void* hd = nullptr;
         ring->host_unified_ = hipHostGetDevicePointer(&hd, ring->host_, 0) == hipSuccess && hd == ring->host_;
@@ -1178,11 +1196,11 @@ int UploadRing::acquire(uint8_t** host, uint8_t** dev, int* slot) {
             const bool armed = armed_[i];
             lock.unlock();
             if (armed) {
-                hipError_t q = hipEventQuery(ev_[i]);
+                hipError_t q = hipEventQuery(mev_[i]);
                 if (q == hipErrorNotReady) {   // the slot's last reader is still queued
                     (void)hipGetLastError();
                     count_device(dev_id_, kDevBlockingCalls);
-                    q = hipEventSynchronize(ev_[i]);
+                    q = hipEventSynchronize(mev_[i]);
                 }
                 if (q != hipSuccess) {
                     (void)hipGetLastError();
@@ -1207,7 +1225,7 @@ int UploadRing::upload(int slot, size_t bytes, hipStream_t stream) {
 }
 
 int UploadRing::release_after(int slot, hipStream_t stream) {
-    const bool ok = hipEventRecord(ev_[slot], stream) == hipSuccess;
+    const bool ok = record_mirrored(dev_id_, stream, ev_[slot], mev_[slot]) == SHMR_EC_OK;
     std::lock_guard<std::mutex> lock(mu_);
     armed_[slot] = ok;
     inuse_[slot] = false;
@@ -1269,7 +1287,7 @@ int PtrTableCache::lookup(const void* tab, size_t bytes, hipStream_t stream, con
         Entry& e = e_[i];
         if (e.valid && e.stream == stream && e.bytes == bytes && e.hash == h && std::memcmp(e.host, tab, bytes) == 0) {
             // (a stream handle reused after its stream was destroyed: wait on the device)
-            if (!event_done(e.up) && hipStreamWaitEvent(stream, e.up, 0) != hipSuccess) {
+            if (!event_done(e.mup) && hipStreamWaitEvent(stream, e.mup, 0) != hipSuccess) {
                 (void)hipGetLastError();
                 return SHMR_EC_DEVICE_ERROR;
             }
@@ -1292,8 +1310,8 @@ int PtrTableCache::lookup(const void* tab, size_t bytes, hipStream_t stream, con
             Entry& e = e_[i];
             // (readers on the same stream included: a destroyed stream's handle
             // may come back for a new stream while its kernels still run)
-            if (e.busy || !event_done(e.up)) continue;
-            if (e.used_armed && !event_done(e.used)) continue;
+            if (e.busy || !event_done(e.mup)) continue;
+            if (e.used_armed && !event_done(e.mused)) continue;
             if (victim < 0 || e.tick < e_[victim].tick) victim = i;
         }
     }
@@ -1305,7 +1323,9 @@ int PtrTableCache::lookup(const void* tab, size_t bytes, hipStream_t stream, con
         if (arena_alloc(dev_id_, UploadRing::kSlotBytes, false, &h, &d) != SHMR_EC_OK) return SHMR_EC_OK;
         RelaxedCapture relaxed;
         if (hipEventCreateWithFlags(&e.up, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&e.used, hipEventDisableTiming) != hipSuccess) {
+            hipEventCreateWithFlags(&e.used, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e.mup, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e.mused, hipEventDisableTiming) != hipSuccess) {
             (void)hipGetLastError();
             return SHMR_EC_OK;   // the arena block is abandoned (permanent memory)
         }
@@ -1314,11 +1334,11 @@ int PtrTableCache::lookup(const void* tab, size_t bytes, hipStream_t stream, con
     }
     e.valid = false;
     std::memcpy(e.host, tab, bytes);
-    if (hipMemcpyAsync(e.dev, e.host, bytes, hipMemcpyHostToDevice, stream) != hipSuccess ||
-        hipEventRecord(e.up, stream) != hipSuccess) {
+    if (hipMemcpyAsync(e.dev, e.host, bytes, hipMemcpyHostToDevice, stream) != hipSuccess) {
         (void)hipGetLastError();
         return SHMR_EC_DEVICE_ERROR;
     }
+    if (record_mirrored(dev_id_, stream, e.up, e.mup) != SHMR_EC_OK) return SHMR_EC_DEVICE_ERROR;
     e.bytes = bytes;
     e.hash = h;
     e.stream = stream;
@@ -1335,8 +1355,7 @@ int PtrTableCache::release_after(int entry, hipStream_t stream) {
     std::lock_guard<std::mutex> lock(mu_);
     Entry& e = e_[entry];
     --e.busy;
-    if (hipEventRecord(e.used, stream) != hipSuccess) {
-        (void)hipGetLastError();
+    if (record_mirrored(dev_id_, stream, e.used, e.mused) != SHMR_EC_OK) {
         e.valid = false;
         return SHMR_EC_DEVICE_ERROR;
     }

@@ -277,13 +277,23 @@ private:
     bool host_unified_ = false;
     uint8_t* host_ = nullptr;
     uint8_t* dev_ = nullptr;
-    hipEvent_t ev_[kSlots] = {};
+    hipEvent_t ev_[kSlots] = {};    // recorded on the caller's stream
+    hipEvent_t mev_[kSlots] = {};   // its mirror (record_mirrored): the one acquire() waits on
     bool armed_[kSlots] = {};
     bool inuse_[kSlots] = {};
     int next_ = 0;
     std::mutex mu_;
     std::condition_variable cv_;
 };
+
+// Events the library later queries, or makes another stream wait on, from any
+// thread are never used as recorded on a caller's stream: that stream may have
+// begun a graph capture since, and a query of (or a wait on) an event whose
+// stream is capturing fails with hipErrorCapturedEvent and invalidates that
+// capture (measured: profiles/r04/s8).  `on_caller` is recorded on `stream`;
+// the device's private stream waits for it and records `mirror`, which every
+// later query and cross-stream wait uses (complete no earlier than on_caller).
+int record_mirrored(int dev, hipStream_t stream, hipEvent_t on_caller, hipEvent_t mirror);
 
 // ---- per-device cache of shard-pointer tables (the *_ptrs_dev calls) -------
 // A table passed again with the same bytes on the same stream (a device Block
@@ -310,7 +320,8 @@ private:
         size_t bytes = 0;
         uint64_t hash = 0, tick = 0;
         hipStream_t stream = nullptr;
-        hipEvent_t up = nullptr, used = nullptr;
+        hipEvent_t up = nullptr, used = nullptr;     // recorded on the caller's stream
+        hipEvent_t mup = nullptr, mused = nullptr;   // their mirrors (record_mirrored): queried / waited on
         bool valid = false, used_armed = false;
         int busy = 0;
     };

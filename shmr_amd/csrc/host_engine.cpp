@@ -294,6 +294,7 @@ int run_mapped(const HostJob& job, const std::vector<uint64_t>& dptrs, bool alig
     const unsigned t = c.k() + c.p();
     std::vector<int> results(size_t(ndev), SHMR_EC_OK);
     auto worker = [&](int di) {
+        RelaxedCapture relaxed;   // devices 1.. run on threads of their own (default mode)
         int& result = results[size_t(di)];
         const int dev = devices[di];
         DeviceScope scope(dev);
@@ -532,6 +533,7 @@ int run_host_job(const HostJob& job, const int* devices, int ndev) {
     std::vector<int> results(size_t(ndev), SHMR_EC_OK);
 
     auto worker = [&](int di) {
+        RelaxedCapture relaxed;   // devices 1.. run on threads of their own (default mode)
         int& result = results[size_t(di)];
         const int dev = devices[di];
         DeviceScope scope(dev);

@@ -335,3 +335,85 @@ def test_library_allocations_while_another_thread_captures(gpu, mode):
     graph.replay()
     torch.cuda.synchronize()
     assert np.array_equal(parity.cpu().numpy(), _oracle_parity(k, p, data.cpu().numpy()))
+
+
+def test_events_recorded_before_a_capture_on_that_stream(gpu):
+    """The library's readiness events (a plan upload, an upload-ring slot, a
+    pointer-table cache entry) recorded by eager calls on stream S stay usable
+    by other threads after S begins a graph capture: every query or wait goes
+    to a mirror recorded on the device's private stream, never to the event on
+    S -- HIP fails a query of an event whose stream is capturing
+    (hipErrorCapturedEvent) and invalidates the capture (soak finding,
+    profiles/r04/s8)."""
+    import ctypes
+    import threading
+    import torch
+    from shmr_amd.reed_solomon import _ptr, _u8p
+    shmr_amd.device_init(0)
+    k, p, S, B = 11, 5, 4096, 40          # a codec no other test uses: fresh plans
+    t = k + p
+    rs = shmr_amd.ReedSolomon(k, p)
+    L = rs._L
+    rng = np.random.default_rng(77)
+    host = np.zeros((B, t, S), np.uint8)
+    host[:, :k] = rng.integers(0, 256, (B, k, S), dtype=np.uint8)
+    host[:, k:] = _oracle_parity(k, p, host[:, :k])
+    present = np.ones((B, t), np.uint8)
+    for b in range(B):                     # 40 runs of 2-row rebuilds: the upload-ring table launch
+        present[b, [[0, 1], [2, 3]][b % 2]] = 0
+    s_cap, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    # every buffer exists before the capture: the other thread makes no torch call
+    cw0, cw2 = torch.from_numpy(host).to(gpu), torch.from_numpy(host).to(gpu)
+    data = torch.from_numpy(np.ascontiguousarray(host[:, :k])).to(gpu)
+    par0, par_cap, par_other = (torch.zeros((B, p, S), dtype=torch.uint8, device=gpu) for _ in range(3))
+    pbuf = torch.zeros((9, t, S), dtype=torch.uint8, device=gpu)
+    pbuf[:, :k] = torch.from_numpy(host[:9, :k]).to(gpu)
+    tabs = [np.array([pbuf[j, i].data_ptr() for i in range(t)], dtype=np.uint64) for j in range(9)]
+    torch.cuda.synchronize()
+    # eager calls on s_cap: plan uploads, a ring slot and 8 table-cache entries recorded there
+    with torch.cuda.stream(s_cap):
+        rs.encode_batch_dev(data, par0)
+        rs.reconstruct_batch_dev(cw0, present)
+        for j in range(8):
+            assert L.shmr_ec_encode_ptrs_dev(rs._h, tabs[j].ctypes.data_as(ctypes.POINTER(_u8p)), 1, S, 0,
+                                             ctypes.c_void_p(s_cap.cuda_stream)) == 0
+    in_capture, done = threading.Event(), threading.Event()
+    rcs = []
+
+    def other():                            # C-ABI calls only, on s2, while s_cap captures
+        try:
+            assert in_capture.wait(60)
+            sp = ctypes.c_void_p(s2.cuda_stream)
+            rcs.append(L.shmr_ec_encode_batch_dev(rs._h, ctypes.c_void_p(data.data_ptr()), S, k * S,
+                                                  ctypes.c_void_p(par_other.data_ptr()), S, p * S, B, S, 0, sp))
+            for _ in range(33):             # around the 32-slot ring: reuses the slot s_cap armed
+                rcs.append(L.shmr_ec_reconstruct_batch_dev(rs._h, ctypes.c_void_p(cw2.data_ptr()), S, t * S,
+                                                           _ptr(present), B, S, 0, 0, sp))
+            # a ninth table: the cache's victim search looks at the 8 entries s_cap filled
+            rcs.append(L.shmr_ec_encode_ptrs_dev(rs._h, tabs[8].ctypes.data_as(ctypes.POINTER(_u8p)), 1, S, 0, sp))
+        except BaseException as e:   # reported by the capturing thread
+            rcs.append(repr(e))
+        finally:
+            done.set()
+
+    th = threading.Thread(target=other)
+    th.start()
+    graph = torch.cuda.CUDAGraph()
+    try:
+        with torch.cuda.graph(graph, stream=s_cap):
+            rs.encode_batch_dev(data, par_cap)
+            in_capture.set()
+            assert done.wait(120), "the other thread did not finish"
+    finally:
+        in_capture.set()
+        th.join(120)
+    assert rcs == [0] * 35, [shmr_amd.Error(r).name if isinstance(r, int) and r else r for r in rcs]
+    graph.replay()
+    torch.cuda.synchronize()
+    want = host[:, k:]
+    for name, par in (("eager", par0), ("captured", par_cap), ("other thread", par_other)):
+        assert np.array_equal(par.cpu().numpy(), want), name
+    assert np.array_equal(cw0.cpu().numpy(), host) and np.array_equal(cw2.cpu().numpy(), host)
+    got = pbuf.cpu().numpy()
+    for j in range(9):
+        assert np.array_equal(got[j, k:], want[j]), j

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Runs tests/test_gpu_capture.py's allocations-while-capturing case against a
+"""Runs one of tests/test_gpu_capture.py's cross-thread capture cases against a
 given product library (A/B of a fix: the same test on the library before and
 after it), printing one JSON line per capture mode.
 
@@ -20,6 +20,7 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib", default=os.path.join(ROOT, "shmr_amd", "_lib", "libshmr_ec.so"))
+    ap.add_argument("--test", default="test_library_allocations_while_another_thread_captures")
     a = ap.parse_args()
     import torch
     from shmr_amd import _native
@@ -28,13 +29,15 @@ def main():
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     gpu = torch.device("cuda", 0)
-    for mode in ("global", "thread_local"):
+    fn = getattr(mod, a.test)
+    modes = ("global", "thread_local") if fn.__code__.co_argcount == 2 else (None,)
+    for mode in modes:
         try:
-            mod.test_library_allocations_while_another_thread_captures(gpu, mode)
+            fn(gpu, mode) if mode else fn(gpu)
             out = "pass"
         except BaseException as e:   # noqa: BLE001 -- reported, next mode
             out = repr(e)[:600]
-        print(json.dumps({"lib": a.lib, "mode": mode, "result": out}), flush=True)
+        print(json.dumps({"lib": a.lib, "test": a.test, "mode": mode, "result": out}), flush=True)
 
 
 if __name__ == "__main__":

@@ -138,6 +138,49 @@ def main():
                                   "caller_mode": ["global", "thread_local", "relaxed"][call_mode],
                                   "call": name, "call_rc": out.get("rc", "hung"), "end_capture_rc": end}),
                       flush=True)
+    # Events recorded on a stream BEFORE that stream began capturing, used from another thread
+    # while it captures: the event itself, and a mirror (a second stream waited on the event
+    # before the capture, then recorded its own event).
+    priv = stream()
+    cap_stream = stream()                      # a fresh one (the first has seen invalidated captures)
+    for cap_mode in (GLOBAL, THREAD_LOCAL):
+        for name in ("query_event", "wait_event", "query_mirror", "wait_mirror"):
+            e, m = vp(), vp()
+            ck(H.hipEventCreateWithFlags(ctypes.byref(e), ctypes.c_uint(2)), "event")
+            ck(H.hipEventCreateWithFlags(ctypes.byref(m), ctypes.c_uint(2)), "event")
+            ck(H.hipMemsetAsync(dev, ctypes.c_int(1), ctypes.c_size_t(4096), cap_stream), "memset")
+            ck(H.hipEventRecord(e, cap_stream), "record")
+            ck(H.hipStreamWaitEvent(priv, e, ctypes.c_uint(0)), "wait")
+            ck(H.hipEventRecord(m, priv), "record m")
+            ck(H.hipStreamSynchronize(cap_stream), "sync")
+            ev = m if name.endswith("mirror") else e
+            out = {}
+
+            def other():
+                m2 = ctypes.c_int(RELAXED)
+                H.hipThreadExchangeStreamCaptureMode(ctypes.byref(m2))
+                if name.startswith("query"):
+                    out["rc"] = H.hipEventQuery(ev)
+                else:
+                    out["rc"] = H.hipStreamWaitEvent(own, ev, ctypes.c_uint(0))
+                    out["rc2"] = H.hipStreamSynchronize(own)
+                H.hipGetLastError()
+
+            ck(H.hipStreamBeginCapture(cap_stream, ctypes.c_int(cap_mode)), "begin")
+            ck(H.hipMemsetAsync(dev, ctypes.c_int(0), ctypes.c_size_t(4096), cap_stream), "memset")
+            th = threading.Thread(target=other)
+            th.start()
+            th.join(60)
+            g = vp()
+            end = H.hipStreamEndCapture(cap_stream, ctypes.byref(g))
+            H.hipGetLastError()
+            if end == 0 and g.value:
+                H.hipGraphDestroy(g)
+            print(json.dumps({"capture_mode": ["global", "thread_local"][cap_mode], "caller_mode": "relaxed",
+                              "call": name + " (recorded before the capture)", "call_rc": out.get("rc", "hung"),
+                              "call_rc2": out.get("rc2"), "end_capture_rc": end}), flush=True)
+            H.hipEventDestroy(e)
+            H.hipEventDestroy(m)
     H.hipDeviceSynchronize()
 
 

@@ -95,15 +95,15 @@ class _Nothing:
         return False
 
 
-def worker(tid, deadline, errors, counts):
+def worker(tid, deadline, errors, counts, ops=tuple(range(7)), shapes=tuple(range(len(SHAPES)))):
     rng = np.random.default_rng([tid, 2024])
     stream = torch.cuda.Stream()
     slab = shmr_amd.PinnedBuffer(4 * 24 * 524288)
     kept = {}   # (shape, set) -> per-shard device buffers reused across calls (pointer-table cache hits)
     while time.time() < deadline and not errors:
-        k, p, L = SHAPES[int(rng.integers(0, len(SHAPES)))]
+        k, p, L = SHAPES[shapes[int(rng.integers(0, len(shapes)))]]
         rs = shmr_amd.ReedSolomon(k, p)
-        op = int(rng.integers(0, 7))
+        op = ops[int(rng.integers(0, len(ops)))]
         gate = GATE.exclusive() if op == 6 else GATE.shared() if op in (3, 4) else _Nothing()
         try:
             with gate:
@@ -277,10 +277,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=120)
     ap.add_argument("--threads", type=int, default=12)
+    ap.add_argument("--ops", default="0,1,2,3,4,5,6", help="subset of the operations (comma list)")
+    ap.add_argument("--shapes", default=",".join(str(i) for i in range(len(SHAPES))),
+                    help="subset of SHAPES (indices)")
     a = ap.parse_args()
+    ops = tuple(int(x) for x in a.ops.split(","))
+    shapes = tuple(int(x) for x in a.shapes.split(","))
     deadline = time.time() + a.seconds
     errors, counts = [], [0] * a.threads
-    th = [threading.Thread(target=worker, args=(t, deadline, errors, counts)) for t in range(a.threads)]
+    th = [threading.Thread(target=worker, args=(t, deadline, errors, counts, ops, shapes)) for t in range(a.threads)]
     for t in th:
         t.start()
     last = time.time()
