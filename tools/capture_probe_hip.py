@@ -142,9 +142,9 @@ def main():
     # while it captures: the event itself, and a mirror (a second stream waited on the event
     # before the capture, then recorded its own event).
     priv = stream()
-    cap_stream = stream()                      # a fresh one (the first has seen invalidated captures)
     for cap_mode in (GLOBAL, THREAD_LOCAL):
         for name in ("query_event", "wait_event", "query_mirror", "wait_mirror"):
+            cap_stream = stream()   # a fresh one per case: a stream whose capture was invalidated stays failed
             e, m = vp(), vp()
             ck(H.hipEventCreateWithFlags(ctypes.byref(e), ctypes.c_uint(2)), "event")
             ck(H.hipEventCreateWithFlags(ctypes.byref(m), ctypes.c_uint(2)), "event")
