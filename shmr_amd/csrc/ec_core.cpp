@@ -5,6 +5,7 @@
 #include <chrono>
 #include <cstring>
 #include <string>
+#include <unordered_set>
 
 namespace shmr {
 namespace core {
@@ -562,7 +563,27 @@ int capture_state(hipStream_t stream, bool* capturing) {
     return SHMR_EC_OK;
 }
 
+namespace {
+std::mutex g_own_mu;
+std::unordered_set<hipStream_t>* g_own_streams = new std::unordered_set<hipStream_t>;   // leaked
+}  // namespace
+
+void register_own_stream(hipStream_t s) {
+    std::lock_guard<std::mutex> lock(g_own_mu);
+    g_own_streams->insert(s);
+}
+
+bool own_stream(hipStream_t s) {
+    std::lock_guard<std::mutex> lock(g_own_mu);
+    return g_own_streams->count(s) != 0;
+}
+
 int record_mirrored(int dev, hipStream_t stream, hipEvent_t on_caller, hipEvent_t mirror) {
+    if (own_stream(stream)) {
+        if (hipEventRecord(mirror, stream) == hipSuccess) return SHMR_EC_OK;
+        (void)hipGetLastError();
+        return SHMR_EC_DEVICE_ERROR;
+    }
     DeviceState* ds = state_of(dev);
     if (!ds) {
         const int rc = device_init(dev, nullptr);
@@ -601,6 +622,7 @@ int device_init(int dev, hipStream_t caller) {
         delete ds;
         return SHMR_EC_DEVICE_ERROR;
     }
+    register_own_stream(ds->priv);
     int rc = add_chunk(*ds, kArenaChunk);
     if (rc) {
         (void)hipStreamDestroy(ds->priv);
@@ -1391,6 +1413,7 @@ Staging* StagingPool::acquire(int dev, size_t bytes, int* rc) {
             *rc = SHMR_EC_DEVICE_ERROR;
             return nullptr;
         }
+        register_own_stream(s->stream);
         count_device(dev, kDevStagingStreams);
     }
     if (s->cap < bytes) {

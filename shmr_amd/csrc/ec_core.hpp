@@ -293,7 +293,13 @@ private:
 // capture (measured: profiles/r04/s8).  `on_caller` is recorded on `stream`;
 // the device's private stream waits for it and records `mirror`, which every
 // later query and cross-stream wait uses (complete no earlier than on_caller).
+// A library-owned stream (staging, host pipelines, the private stream: never
+// captured) records `mirror` itself -- no private-stream wait, which would put
+// a barrier on a shared hardware queue for every per-block host call.
 int record_mirrored(int dev, hipStream_t stream, hipEvent_t on_caller, hipEvent_t mirror);
+// Streams the library creates (registered once, never destroyed).
+void register_own_stream(hipStream_t s);
+bool own_stream(hipStream_t s);
 
 // ---- per-device cache of shard-pointer tables (the *_ptrs_dev calls) -------
 // A table passed again with the same bytes on the same stream (a device Block

@@ -140,6 +140,7 @@ struct DevicePipe {
                     (void)hipGetLastError();
                     return SHMR_EC_DEVICE_ERROR;
                 }
+                register_own_stream(s.stream);
                 count_device(dev, kDevStagingStreams);
             }
             if (s.dcap < dbytes) {
