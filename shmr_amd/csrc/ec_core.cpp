@@ -1308,8 +1308,11 @@ int PtrTableCache::lookup(const void* tab, size_t bytes, hipStream_t stream, con
     for (int i = 0; i < kEntries; ++i) {
         Entry& e = e_[i];
         if (e.valid && e.stream == stream && e.bytes == bytes && e.hash == h && std::memcmp(e.host, tab, bytes) == 0) {
-            // (a stream handle reused after its stream was destroyed: wait on the device)
-            if (!event_done(e.mup) && hipStreamWaitEvent(stream, e.mup, 0) != hipSuccess) {
+            // (a stream handle reused after its stream was destroyed: wait on the device).
+            // The upload's own event, not its mirror: it was recorded on this
+            // stream, which is not capturing (the cache serves no captured call),
+            // and the mirror may queue behind other streams' events.
+            if (!event_done(e.up) && hipStreamWaitEvent(stream, e.up, 0) != hipSuccess) {
                 (void)hipGetLastError();
                 return SHMR_EC_DEVICE_ERROR;
             }
@@ -1332,8 +1335,10 @@ int PtrTableCache::lookup(const void* tab, size_t bytes, hipStream_t stream, con
             Entry& e = e_[i];
             // (readers on the same stream included: a destroyed stream's handle
             // may come back for a new stream while its kernels still run)
-            if (e.busy || !event_done(e.mup)) continue;
-            if (e.used_armed && !event_done(e.mused)) continue;
+            // (an entry of this stream -- not capturing -- may use its own events)
+            const bool mine = e.stream == stream;
+            if (e.busy || !event_done(mine ? e.up : e.mup)) continue;
+            if (e.used_armed && !event_done(mine ? e.used : e.mused)) continue;
             if (victim < 0 || e.tick < e_[victim].tick) victim = i;
         }
     }
