@@ -21,7 +21,10 @@
  * failure, never aborts (an internal allocation failure returns
  * SHMR_EC_OUT_OF_MEMORY), never frees caller memory.  Thread-safe: contexts
  * may be shared across threads or created per call (the reference creates a
- * ReedSolomon per block from rayon workers, src/vfs/mod.rs:93-96).
+ * ReedSolomon per block from rayon workers, src/vfs/mod.rs:93-96).  Every
+ * entry point runs under HIP's relaxed stream-capture mode (the calling
+ * thread's mode is restored on return), so calls from other threads neither
+ * fail nor break a graph capture in progress on some thread.
  */
 #ifndef SHMR_EC_H
 #define SHMR_EC_H
