@@ -288,9 +288,9 @@ private:
 
 // Events the library later queries, or makes another stream wait on, from any
 // thread are never used as recorded on a caller's stream: that stream may have
-// begun a graph capture since, and a query of (or a wait on) an event whose
-// stream is capturing fails with hipErrorCapturedEvent and invalidates that
-// capture (measured: profiles/r04/s8).  `on_caller` is recorded on `stream`;
+// begun a graph capture since: a query of an event whose stream is capturing
+// fails with hipErrorCapturedEvent and invalidates that capture, a wait on it
+// fails with hipErrorStreamCaptureIsolation (measured: profiles/r04/s8).  `on_caller` is recorded on `stream`;
 // the device's private stream waits for it and records `mirror`, which every
 // later query and cross-stream wait uses (complete no earlier than on_caller).
 // A library-owned stream (staging, host pipelines, the private stream: never
