@@ -768,11 +768,12 @@ int upload_plan(PlanDev& pd, int dev, hipStream_t stream, bool capturing) {
         return SHMR_EC_DEVICE_ERROR;
     }
     if (capturing) return SHMR_EC_OK;   // a graph node: same bytes on every replay
-    if (!pd.ready) {
+    for (hipEvent_t* e : {&pd.ready, &pd.mready}) {
+        if (*e) continue;
         RelaxedCapture relaxed;
-        if (hipEventCreateWithFlags(&pd.ready, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&pd.mready, hipEventDisableTiming) != hipSuccess) {
+        if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
             (void)hipGetLastError();
+            *e = nullptr;
             return SHMR_EC_DEVICE_ERROR;
         }
     }
