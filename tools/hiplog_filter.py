@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Filters HIP's API log (AMD_LOG_LEVEL=3, AMD_LOG_MASK=1) on stdin down to its
 failed calls: for every distinct (call, status) the count and the first few
-occurrences with the same thread's preceding lines.  Used by tools/gpu/r04l.sh
+occurrences with the same thread's preceding lines.  Used by tools/gpu/archive/r04l.sh
 to find which runtime call a soak failure comes from.
 
     prog 2> >(python tools/hiplog_filter.py > errors.txt)
