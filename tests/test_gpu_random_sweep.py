@@ -159,3 +159,129 @@ def test_random_host_blocks(gpu, case):
     for b in range(B):
         for i in range(t):
             assert np.array_equal(blocks[b][i], full[b][i]), (b, i)
+
+
+def _scatter(rng, n, L, aligned):
+    """Offsets of n regions of L bytes in shuffled order inside one buffer, with
+    random gaps (16-byte aligned starts or any byte); returns (offsets, size)."""
+    order = rng.permutation(n)
+    offs = np.zeros(n, np.int64)
+    pos = int(rng.integers(0, 16))
+    for j in order:
+        pos += int(rng.integers(0, 3)) * 16 + (0 if aligned else int(rng.integers(0, 16)))
+        if aligned:
+            pos = (pos + 15) // 16 * 16
+        offs[j] = pos
+        pos += L
+    return offs, pos + 64
+
+
+@pytest.mark.parametrize("case", range(24 * SCALE))
+def test_random_ptrs(gpu, case):
+    """Pointer tables (*_ptrs_dev, the crate's shard-per-Vec shape): every shard
+    anywhere in a shared buffer, in shuffled memory order, aligned or not; encode,
+    then rebuild random erasures into separate buffers (absent parity NULL under
+    data_only).  Rows are permuted into plan order on the host (r04): a wrong
+    permutation writes the wrong shard."""
+    import torch
+    rng = np.random.default_rng([0x9715, case])
+    k, p, L, B, _, _ = _shape(rng)
+    t = k + p
+    aligned = bool(rng.integers(0, 2))
+    offs, size = _scatter(rng, B * t, L, aligned)
+    host = np.full(size, SENTINEL, np.uint8)
+    full = []
+    for b in range(B):
+        sh = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)] + [np.zeros(L, np.uint8) for _ in range(p)]
+        c_oracle.encode(k, p, sh)
+        full.append(sh)
+        for i in range(k):
+            host[offs[b * t + i]:offs[b * t + i] + L] = sh[i]
+    d = torch.from_numpy(host).to(gpu)
+    base = d.data_ptr()
+    tab = np.array([base + int(o) for o in offs], dtype=np.uint64)
+    rs = shmr_amd.ReedSolomon(k, p)
+    rc = lib().shmr_ec_encode_ptrs_dev(rs._h, tab.ctypes.data_as(ctypes.POINTER(_u8p)), B, L, 0, _stream())
+    assert rc == 0, shmr_amd.Error(rc).name
+    torch.cuda.synchronize()
+    got = d.cpu().numpy()
+    expect = host.copy()
+    for b in range(B):
+        for i in range(k, t):
+            expect[offs[b * t + i]:offs[b * t + i] + L] = full[b][i]
+    assert np.array_equal(got, expect), ("encode", k, p, L, B, aligned)
+    # rebuild: absent shards point into a separate poisoned buffer
+    data_only = bool(rng.integers(0, 2))
+    present = np.ones((B, t), np.uint8)
+    for b in range(B):
+        if rng.integers(0, 4):
+            present[b, rng.choice(t, size=int(rng.integers(1, p + 1)), replace=False)] = 0
+    ooffs, osize = _scatter(rng, B * t, L, aligned)
+    out = torch.full((osize,), 0xEE, dtype=torch.uint8, device=gpu)
+    tab2 = tab.copy()
+    for b in range(B):
+        for i in range(t):
+            if not present[b, i]:
+                tab2[b * t + i] = 0 if (data_only and i >= k) else out.data_ptr() + int(ooffs[b * t + i])
+    rc = lib().shmr_ec_reconstruct_ptrs_dev(rs._h, tab2.ctypes.data_as(ctypes.POINTER(_u8p)),
+                                            present.ctypes.data_as(_u8p), B, L, int(data_only), 0, _stream())
+    assert rc == 0, shmr_amd.Error(rc).name
+    torch.cuda.synchronize()
+    assert np.array_equal(d.cpu().numpy(), expect), ("rebuild touched a present shard", k, p, L, B)
+    got = out.cpu().numpy()
+    want = np.full(osize, 0xEE, np.uint8)
+    for b in range(B):
+        for i in range(t):
+            if not present[b, i] and not (data_only and i >= k):
+                want[ooffs[b * t + i]:ooffs[b * t + i] + L] = full[b][i]
+    assert np.array_equal(got, want), ("rebuild", k, p, L, B, aligned, data_only)
+
+
+@pytest.mark.parametrize("case", range(24 * SCALE))
+def test_random_reconstruct_out(gpu, case):
+    """Compact rebuilds (shmr_ec_reconstruct_batch_dev_out, the crate's
+    fresh-buffer-per-None semantics): absent slots poisoned and never read,
+    rebuilt shards in ascending index into a separate output, nothing else
+    written."""
+    import torch
+    rng = np.random.default_rng([0xC0DE, case])
+    k, p, L, B, spitch, off = _shape(rng)
+    t = k + p
+    bpitch = t * spitch
+    data_only = bool(rng.integers(0, 2))
+    buf = np.full(off + B * bpitch + 64, SENTINEL, dtype=np.uint8)
+    present = np.ones((B, t), np.uint8)
+    full = []
+    for b in range(B):
+        sh = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)] + [np.zeros(L, np.uint8) for _ in range(p)]
+        c_oracle.encode(k, p, sh)
+        full.append(sh)
+        for i in range(t):
+            buf[off + b * bpitch + i * spitch: off + b * bpitch + i * spitch + L] = sh[i]
+        if rng.integers(0, 4):
+            present[b, rng.choice(t, size=int(rng.integers(1, p + 1)), replace=False)] = 0
+    for b in range(B):
+        for i in range(t):
+            if not present[b, i]:
+                buf[off + b * bpitch + i * spitch: off + b * bpitch + i * spitch + L] = 0xEE
+    nout = max(1, int(max(((present[b] == 0) & ((np.arange(t) < k) | (not data_only))).sum() for b in range(B))))
+    opitch = spitch + 16 * int(rng.integers(0, 2))
+    obpitch = nout * opitch
+    d = torch.from_numpy(buf).to(gpu)
+    out = torch.full((off + B * obpitch + 64,), SENTINEL, dtype=torch.uint8, device=gpu)
+    rs = shmr_amd.ReedSolomon(k, p)
+    rc = lib().shmr_ec_reconstruct_batch_dev_out(rs._h, ctypes.c_void_p(d.data_ptr() + off), spitch, bpitch,
+                                                 present.ctypes.data_as(_u8p), B, L, int(data_only),
+                                                 ctypes.c_void_p(out.data_ptr() + off), opitch, obpitch, 0, _stream())
+    assert rc == 0, shmr_amd.Error(rc).name
+    torch.cuda.synchronize()
+    assert np.array_equal(d.cpu().numpy(), buf), "the compact rebuild wrote its input"
+    want = np.full(off + B * obpitch + 64, SENTINEL, np.uint8)
+    for b in range(B):
+        j = 0
+        for i in range(t):
+            if not present[b, i] and (i < k or not data_only):
+                o = off + b * obpitch + j * opitch
+                want[o:o + L] = full[b][i]
+                j += 1
+    assert np.array_equal(out.cpu().numpy(), want), (k, p, L, B, spitch, off, data_only)
