@@ -285,3 +285,69 @@ def test_random_reconstruct_out(gpu, case):
                 want[o:o + L] = full[b][i]
                 j += 1
     assert np.array_equal(out.cpu().numpy(), want), (k, p, L, B, spitch, off, data_only)
+
+
+def _start(rs, fn, shards, present=None, data_only=False):
+    """shmr_ec_encode_start / shmr_ec_reconstruct_start through ctypes: (rc, op)."""
+    from shmr_amd.reed_solomon import _ptr
+    n = len(shards)
+    L = len(shards[0])
+    ptrs = (_u8p * n)(*[_ptr(s) for s in shards])
+    lens = (ctypes.c_size_t * n)(*[(L if present is None or present[i] else 0) for i in range(n)])
+    op = ctypes.c_void_p()
+    if fn == "encode":
+        rc = rs._L.shmr_ec_encode_start(rs._h, ptrs, lens, n, ctypes.byref(op))
+    else:
+        pr = np.ascontiguousarray(present, dtype=np.uint8)
+        rc = rs._L.shmr_ec_reconstruct_start(rs._h, ptrs, lens, _ptr(pr), n, int(data_only), ctypes.byref(op))
+    return rc, op
+
+
+@pytest.mark.parametrize("case", range(8 * SCALE))
+def test_random_started_calls(gpu, case):
+    """Started per-block calls (shmr_ec_*_start, the Block Cache's overlap of
+    file I/O with the GPU work): up to six ops of random shapes in flight at
+    once, mapped (zero-copy, pending until waited) or pageable, encodes and
+    rebuilds with data_only, waited in random order -- every byte equal to the
+    oracle's."""
+    rng = np.random.default_rng([0x57A7, case])
+    keep, pending = [], []
+    for _ in range(int(rng.integers(1, 7))):
+        k, p, L, _, _, _ = _shape(rng)
+        t = k + p
+        rs = shmr_amd.ReedSolomon(k, p)
+        if rng.integers(0, 2):
+            buf = shmr_amd.PinnedBuffer(t * L + 16)
+            base = int(rng.integers(0, 16))
+            arr = buf.array[base:base + t * L].reshape(t, L)
+            sh = [arr[i] for i in range(t)]
+            keep.append(buf)
+        else:
+            sh = [np.zeros(L, np.uint8) for _ in range(t)]
+        for i in range(k):
+            sh[i][:] = rng.integers(0, 256, L, dtype=np.uint8)
+        full = [s.copy() for s in sh[:k]] + [np.zeros(L, np.uint8) for _ in range(p)]
+        c_oracle.encode(k, p, full)
+        if rng.integers(0, 2):
+            for i in range(k, t):
+                sh[i][:] = SENTINEL
+            rc, op = _start(rs, "encode", sh)
+            want = full
+        else:
+            for i in range(k, t):
+                sh[i][:] = full[i]
+            present = np.ones(t, np.uint8)
+            present[rng.choice(t, size=int(rng.integers(1, p + 1)), replace=False)] = 0
+            data_only = bool(rng.integers(0, 2))
+            for i in np.flatnonzero(present == 0):
+                sh[i][:] = 0xEE
+            rc, op = _start(rs, "reconstruct", sh, present, data_only)
+            want = [(np.full(L, 0xEE, np.uint8) if (not present[i] and data_only and i >= k) else full[i])
+                    for i in range(t)]
+        assert rc == 0 and op.value, shmr_amd.Error(rc).name if rc else "no op"
+        pending.append((op, rs, sh, want, (k, p, L)))
+    for j in rng.permutation(len(pending)):
+        op, rs, sh, want, shape = pending[j]
+        assert rs._L.shmr_ec_op_wait(op) == 0
+        for i in range(len(sh)):
+            assert np.array_equal(sh[i], want[i]), (shape, i)
