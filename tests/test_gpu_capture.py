@@ -417,3 +417,35 @@ def test_events_recorded_before_a_capture_on_that_stream(gpu):
     got = pbuf.cpu().numpy()
     for j in range(9):
         assert np.array_equal(got[j, k:], want[j]), j
+
+
+def test_host_buffer_calls_inside_own_capture(gpu):
+    """A host-buffer call (synchronous, on the library's own streams) made by
+    the thread that is capturing a graph in the default global mode: it runs
+    eagerly and exactly, and the capture -- which it does not touch -- stays
+    valid and replays its own work."""
+    import torch
+    k, p, S = 6, 3, 70001
+    rs = shmr_amd.ReedSolomon(k, p)
+    shmr_amd.device_init(0)
+    rng = np.random.default_rng(41)
+    shards = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)] + [np.zeros(S, np.uint8) for _ in range(p)]
+    x = torch.zeros(1024, device=gpu)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=torch.cuda.Stream()):
+        x.add_(1)
+        rs.encode(shards)                                  # eager, not part of the graph
+        blocks = np.zeros((2, k + p, 4096), np.uint8)
+        blocks[:, :k] = rng.integers(0, 256, (2, k, 4096), dtype=np.uint8)
+        rs.encode_blocks_host(blocks)
+    want = [np.zeros(S, np.uint8) for _ in range(p)]
+    c_oracle.encode(k, p, [s.copy() for s in shards[:k]] + want)
+    for r in range(p):
+        assert np.array_equal(shards[k + r], want[r]), r
+    par = _oracle_parity(k, p, blocks[:, :k])
+    assert np.array_equal(blocks[:, k:], par)
+    graph.replay()
+    graph.replay()
+    torch.cuda.synchronize()
+    assert float(x[0].item()) == 2.0
