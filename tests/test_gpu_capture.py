@@ -449,3 +449,51 @@ def test_host_buffer_calls_inside_own_capture(gpu):
     graph.replay()
     torch.cuda.synchronize()
     assert float(x[0].item()) == 2.0
+
+
+def test_null_stream_call_while_another_thread_captures_a_blocking_stream(gpu):
+    """A device call on the legacy null stream while another thread captures a
+    BLOCKING stream in global mode: work on the null stream would join that
+    capture, so the library refuses the call (INVALID_ARGUMENT, nothing
+    enqueued) and the other capture stays valid (HIP runtime driven through
+    ctypes: torch's streams are non-blocking)."""
+    import ctypes
+    import threading
+    import torch
+    H = ctypes.CDLL("libamdhip64.so.7")   # the runtime torch (and the library) already loaded
+    vp = ctypes.c_void_p
+    k, p, S, B = 4, 2, 8192, 2
+    rs = shmr_amd.ReedSolomon(k, p)
+    shmr_amd.device_init(0)
+    data = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=gpu)
+    parity = torch.zeros((B, p, S), dtype=torch.uint8, device=gpu)
+    scratch = torch.zeros(4096, dtype=torch.uint8, device=gpu)
+    torch.cuda.synchronize()
+    blocking = vp()
+    assert H.hipStreamCreate(ctypes.byref(blocking)) == 0
+    in_capture, done = threading.Event(), threading.Event()
+    out = {}
+
+    def other():
+        assert in_capture.wait(60)
+        out["rc"] = rs._L.shmr_ec_encode_batch_dev(rs._h, vp(data.data_ptr()), S, k * S, vp(parity.data_ptr()),
+                                                  S, p * S, B, S, 0, vp(0))
+        done.set()
+
+    th = threading.Thread(target=other)
+    th.start()
+    assert H.hipStreamBeginCapture(blocking, ctypes.c_int(0)) == 0          # global mode
+    assert H.hipMemsetAsync(vp(scratch.data_ptr()), ctypes.c_int(7), ctypes.c_size_t(4096), blocking) == 0
+    in_capture.set()
+    assert done.wait(60)
+    th.join(60)
+    g = vp()
+    end = H.hipStreamEndCapture(blocking, ctypes.byref(g))
+    H.hipGetLastError()
+    if end == 0 and g.value:
+        H.hipGraphDestroy(g)
+    H.hipStreamDestroy(blocking)
+    assert end == 0, f"the other thread's capture was broken ({end})"
+    assert shmr_amd.Error(out["rc"]).name == "InvalidArgument", out
+    torch.cuda.synchronize()
+    assert not parity.any().item(), "a refused call enqueued work"
