@@ -497,3 +497,39 @@ def test_null_stream_call_while_another_thread_captures_a_blocking_stream(gpu):
     assert shmr_amd.Error(out["rc"]).name == "InvalidArgument", out
     torch.cuda.synchronize()
     assert not parity.any().item(), "a refused call enqueued work"
+
+
+def test_entry_points_restore_the_thread_capture_mode(gpu):
+    """Every entry point runs under the relaxed capture mode and gives the
+    calling thread its own mode back (global, thread-local or relaxed), on
+    success and on a refused call alike."""
+    import ctypes
+    import torch
+    H = ctypes.CDLL("libamdhip64.so.7")
+    k, p, S = 5, 2, 4096
+    rs = shmr_amd.ReedSolomon(k, p)
+    data = torch.randint(0, 256, (2, k, S), dtype=torch.uint8, device=gpu)
+    parity = torch.zeros((2, p, S), dtype=torch.uint8, device=gpu)
+    shards = [np.zeros(S, np.uint8) for _ in range(k + p)]
+
+    def mode_now():
+        m = ctypes.c_int(2)
+        assert H.hipThreadExchangeStreamCaptureMode(ctypes.byref(m)) == 0
+        back = ctypes.c_int(m.value)
+        assert H.hipThreadExchangeStreamCaptureMode(ctypes.byref(back)) == 0
+        return m.value
+
+    try:
+        for mode in (0, 1, 2):   # global, thread-local, relaxed
+            m = ctypes.c_int(mode)
+            assert H.hipThreadExchangeStreamCaptureMode(ctypes.byref(m)) == 0
+            rs.encode_batch_dev(data, parity)
+            rs.encode(shards)
+            with pytest.raises(shmr_amd.Error):
+                rs.reconstruct([None] * (k + p))          # refused: too few shards
+            assert mode_now() == mode
+    finally:
+        m = ctypes.c_int(0)
+        H.hipThreadExchangeStreamCaptureMode(ctypes.byref(m))
+    torch.cuda.synchronize()
+    assert np.array_equal(parity.cpu().numpy(), _oracle_parity(k, p, data.cpu().numpy()))
