@@ -94,6 +94,11 @@ def parse():
                          "shard its own GPU allocation named by a pointer table (shmr_ec_*_ptrs_dev) -- the "
                          "crate's shape, where each shard is a Vec<u8> of its own (reference block.rs:408-427) and "
                          "each rebuilt shard a fresh buffer (block.rs:556-565); not with codec104")
+    ap.add_argument("--ptrs-alloc", default="slab", choices=["slab", "torch"],
+                    help="--layout ptrs: where the shard buffers come from -- slab: shmr_ec_device_alloc_shards "
+                         "(every shard of the batch in one slab at the slot pitch, rebuilt shards in a second "
+                         "slab; the table forms a slot grid and runs through the strided kernels, knob ptrs_grid); "
+                         "torch: one torch allocation per shard (table kernels)")
     ap.add_argument("--process-model", default="process", choices=["process", "single"],
                     help="process: one process per GPU (torchrun, or self-spawned for --gpus N); single: one "
                          "process drives all N GPUs with one host thread + stream each (the reference daemon's "
@@ -203,7 +208,9 @@ class Shape:
         rows = p if self.erasures is None else self.erasures
         mode = 0 if self.erasures is None else 2 if self.compact else 1
         if args.layout == "ptrs":
-            mode = 3 if self.erasures is None else 4
+            # slab buffers form a slot grid: the strided kernels run (encode, compact rebuild)
+            mode = (0 if self.erasures is None else 2) if args.ptrs_alloc == "slab" else \
+                (3 if self.erasures is None else 4)
         self.tuning = shmr_amd.describe_variant(mode, k, rows)
         if self.codec:
             self.tuning = f"encode: {shmr_amd.describe_variant(False, k, p)}; reconstruct: {self.tuning}"
@@ -278,14 +285,18 @@ class Workload:
         torch.cuda.synchronize(dev)
 
     def _init_ptrs(self, g):
-        """--layout ptrs: every shard a separate torch allocation (the crate's
-        Vec<u8> per shard); the pointer table is marshalled once, as a Rust
-        shim would keep its Vec of pointers, and each step is one C call."""
+        """--layout ptrs: every shard a buffer of its own named by a pointer
+        table (the crate's Vec<u8> per shard); the table is marshalled once, as
+        a Rust shim would keep its Vec of pointers, and each step is one C call.
+        --ptrs-alloc slab: the buffers come from shmr_ec_device_alloc_shards
+        (INTEGRATION.md's Block Cache), torch: one torch allocation each."""
         sh, dev, rs = self.shape, self.dev, self.rs
         k, p, S, B = sh.k, sh.p, sh.S, sh.B
         t = k + p
         if sh.codec:
             raise SystemExit("--layout ptrs: encode and decode configs only (not codec104)")
+        if self.args.ptrs_alloc == "slab":
+            return self._init_slab(g)
         with torch.cuda.device(dev), torch.cuda.stream(self.stream):
             blocks = [[torch.randint(0, 256, (S,), dtype=torch.uint8, device=dev, generator=g) for _ in range(k)]
                       + [torch.zeros(S, dtype=torch.uint8, device=dev) for _ in range(p)] for _ in range(B)]
@@ -317,6 +328,51 @@ class Workload:
             self.keep, _, _, self.ptab = rs._dev_table(table, lambda b, i: True)
             self.shards = _Stacked(blocks, 0, t)
             self.rebuilt = _Stacked(self.outs, 0, sh.erasures)
+
+    def _init_slab(self, g):
+        sh, dev, rs = self.shape, self.dev, self.rs
+        k, p, S, B = sh.k, sh.p, sh.S, sh.B
+        t = k + p
+        self.stream_ptr = ctypes.c_void_p(self.stream.cuda_stream)
+        with torch.cuda.device(dev), torch.cuda.stream(self.stream):
+            if sh.erasures is None:
+                # the encode's inputs and outputs in slabs of their own (measured: data and
+                # parity interleaved in one slab run 1.7-3.6 points slower, profiles/r05/s1)
+                self.dslab = shmr_amd.ShardSlab(B, k, S, device=dev.index)
+                self.pslab = shmr_amd.ShardSlab(B, p, S, device=dev.index)
+                self.data, self.parity = self.dslab.tensor(), self.pslab.tensor()
+                self.data.zero_()
+                self.parity.zero_()
+                self.data[:, :, :S] = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=dev, generator=g)
+                addrs = np.concatenate([self.dslab.ptrs.reshape(B, k), self.pslab.ptrs.reshape(B, p)], axis=1)
+            else:
+                self.slab = shmr_amd.ShardSlab(B, t, S, device=dev.index)
+                view = self.slab.tensor()
+                view.zero_()
+                view[:, :k, :S] = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=dev, generator=g)
+                addrs = self.slab.ptrs.reshape(B, t).copy()
+                tab = np.ascontiguousarray(addrs.reshape(-1))
+                _native_check(rs._L.shmr_ec_encode_ptrs_dev(rs._h, tab.ctypes.data_as(ctypes.POINTER(
+                    ctypes.POINTER(ctypes.c_uint8))), B, S, dev.index, self.stream_ptr))
+                present = np.ones((B, t), dtype=np.uint8)
+                gb = np.array(placement.weak_batch(B, self.rank, self.world))   # global block ids of this device
+                if sh.erasures == 1:
+                    present[np.arange(B), gb % k] = 0
+                else:
+                    present[np.arange(B), gb % 10] = 0
+                    present[np.arange(B), (gb + 3) % 10] = 0
+                self.present = present
+                # a fresh buffer per None shard (the crate's vec![0; len]), from a second slab
+                e = sh.erasures
+                self.outs = shmr_amd.ShardSlab(B, e, S, device=dev.index)
+                for b in range(B):
+                    for j, i in enumerate(np.flatnonzero(present[b] == 0)):
+                        addrs[b, i] = self.outs.ptrs[b * e + j]
+                self.shards = view
+                self.rebuilt = self.outs.tensor()
+                self.rebuilt.zero_()
+            self.ptab_arr = np.ascontiguousarray(addrs.reshape(-1))
+            self.ptab = self.ptab_arr.ctypes.data_as(ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)))
 
     def vram(self, shape):
         """Batch tensor: torch's allocator, or with --contig physically
@@ -432,6 +488,11 @@ class _Stacked:
         return st[(slice(None),) + rest] if rest else st
 
 
+def _slot(S):
+    pitch = (S + 4095) // 4096 * 4096
+    return pitch + 4096 if pitch % 65536 == 0 else pitch
+
+
 def _native_check(rc):
     if rc != 0:
         raise RuntimeError(f"shmr_ec call failed: {_native.lib().shmr_ec_status_name(rc).decode()}")
@@ -483,6 +544,8 @@ def report(args, shape, world, ranks, elapsed, step_ms, ramp_steps, process_mode
                              "(one process, one host thread + stream per GPU: the daemon's shape)")),
             "tuning": shape.tuning,
             "memory": ("physically contiguous VRAM (shmr_ec_device_alloc)" if args.contig
+                       else "shmr_ec_device_alloc_shards slabs (hipMalloc)"
+                       if args.layout == "ptrs" and args.ptrs_alloc == "slab"
                        else "torch caching allocator (hipMalloc)"),
             "shard_pitch_bytes": None if args.layout == "ptrs" else shape.pitch,
             "rebuild_out": (None if shape.erasures is None else
@@ -490,8 +553,14 @@ def report(args, shape, world, ranks, elapsed, step_ms, ramp_steps, process_mode
                             if args.layout == "ptrs" else
                             "compact [blocks][erasures][pitch] output (crate semantics: a fresh buffer per None "
                             "shard)" if shape.compact else "in place, in the erased shards' own slots"),
-            "shard_layout": ("every shard a separate torch allocation, named by a pointer table (shmr_ec_*_ptrs_dev: "
-                             "the crate's Vec<u8> per shard)" if args.layout == "ptrs" else
+            "shard_layout": (("every shard a buffer of its own from shmr_ec_device_alloc_shards "
+                              f"({_slot(shape.S)} B slots; encode: data and parity shards in two slabs, rebuild: "
+                              "every shard in one slab and the rebuilt shards in a second), named by a pointer table "
+                              "(shmr_ec_*_ptrs_dev: the crate's Vec<u8> per shard); the table forms a slot grid, "
+                              "which runs through the strided kernels"
+                              if args.ptrs_alloc == "slab" else
+                              "every shard a separate torch allocation, named by a pointer table (shmr_ec_*_ptrs_dev: "
+                              "the crate's Vec<u8> per shard)") if args.layout == "ptrs" else
                              "contiguous shards (the reference's block buffer)" if shape.pitch == shape.S else
                              f"shard slots of {shape.pitch} B for {shape.S} B shards"
                              + (" (one 4 KiB page past the 4 KiB-aligned size for a power-of-two stride, "
@@ -598,15 +667,20 @@ def run(args):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    grids0 = shmr_amd.device_stats(dev.index)["ptr_table_grids"]
     t0 = time.perf_counter()
     step_ms = w.timed(args.steps)
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
+    grid_calls = shmr_amd.device_stats(dev.index)["ptr_table_grids"] - grids0
     if world > 1:
         dist.barrier()
     elapsed = max(wall, sum(step_ms) / 1e3)
     elapsed = placement.max_over_ranks(elapsed, device=dev if args.backend == "nccl" else None)
     out = report(args, shape, world, ranks, elapsed, step_ms, ramp_steps, "process")
+    if args.layout == "ptrs":
+        # pointer-table calls of the timed steps that ran as a slot grid (strided kernels)
+        out["config"]["ptr_table_grid_calls_timed"] = grid_calls
     if shape.codec:
         out["roofline"]["round_trip_bit_exact"] = w.round_trip()
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -663,7 +737,7 @@ def traffic_key(args) -> str:
     decode rebuilt in place (the compact output is the default)."""
     key = args.config
     if args.layout == "ptrs":
-        return key + "+ptrs"
+        return key + ("+ptrs" if args.ptrs_alloc == "slab" else "+ptrs_torch")
     if args.pitch_align == 1:
         key += "+packed"
     elif args.pitch_pad == 0:

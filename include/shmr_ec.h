@@ -279,6 +279,24 @@ int shmr_ec_host_unregister(void* p);
 int shmr_ec_device_alloc(int device, size_t bytes, int contiguous, void** out);
 int shmr_ec_device_free(int device, void* p);
 
+/* Shard buffers for the *_ptrs_dev calls with the slot placement of the
+ * device-resident batches: nblocks x shards_per_block buffers of shard_len
+ * bytes carved from one device slab (256-byte aligned base), each at the slot
+ * pitch P = shard_len rounded up to 4 KiB, plus one 4 KiB page when that is a
+ * multiple of 64 KiB:
+ *     out_ptrs[b * shards_per_block + i] = slab + (b * shards_per_block + i) * P.
+ * The crate keeps every shard in a Vec<u8> of its own (reference
+ * src/vfs/block.rs:408-419, :556-565); a device Block Cache that takes its
+ * shard buffers from here -- all total shards of its blocks in one call, and
+ * the buffers for rebuilt shards (one per absent shard) in another -- hands
+ * the *_ptrs_dev calls tables that form a slot grid, which run through the
+ * strided kernels (knob "ptrs_grid").  The bytes are not initialised.  Free
+ * with shmr_ec_device_free_shards(device, out_ptrs[0]); any other pointer
+ * returns INVALID_ARGUMENT. */
+int shmr_ec_device_alloc_shards(int device, size_t nblocks, size_t shards_per_block, size_t shard_len,
+                                uint8_t** out_ptrs);
+int shmr_ec_device_free_shards(int device, uint8_t* first);
+
 /* ---- configuration -------------------------------------------------------- */
 
 /* Device used by the host-buffer entry points (default 0; negative ->
@@ -299,6 +317,13 @@ int shmr_ec_set_device(shmr_ec_t* rs, int device);
  * (default 8192; 0 disables).  "mirror_zc" (0/1, default 1): pageable host
  * batches are gathered into a pinned mirror that the kernel codes in place
  * across PCIe (zero-copy) instead of DMA-ing it to device staging.
+ * "ptrs_grid" (0/1, default 1): a *_ptrs_dev table whose shards form a slot
+ * grid -- entry (b, i) at base + b * block_pitch + i * shard_pitch for the
+ * inputs, and for the outputs (encode: parity rows; reconstruct: the absent
+ * shards in place, or rebuilt shard j of block b at out + b * out_block_pitch +
+ * j * out_shard_pitch) -- runs through the strided kernels of the *_batch_dev
+ * calls with no table (same bytes; SHMR_EC_DEV_PTR_TABLE_GRIDS counts them);
+ * 0 always takes the table kernels.
  * "ptrs_direct" (default 16): zero-copy launches of at most this many 4 KiB
  * tiles read their shard-pointer table from pinned host memory in place
  * instead of uploading it first (0: always upload).  "sync_spin_us"
@@ -388,7 +413,9 @@ enum {
                                              (no upload) */
     SHMR_EC_DEV_CAPTURE_TABLES = 8,       /* capture-reserve blocks taken by captured calls */
     SHMR_EC_DEV_CAPTURE_RELEASED = 9,     /* ... and returned when their graph was destroyed */
-    SHMR_EC_DEV_COUNTERS = 10
+    SHMR_EC_DEV_PTR_TABLE_GRIDS = 10,     /* *_ptrs_dev calls whose table named a slot grid and ran
+                                             through the strided kernels (no table) */
+    SHMR_EC_DEV_COUNTERS = 11
 };
 int shmr_ec_device_stats(int device, uint64_t* out, size_t n);
 

@@ -69,6 +69,8 @@ SIGNATURES = [
      [ctypes.c_void_p, _u8pp, _u8p, _sz, _sz, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     ("shmr_ec_device_alloc", ctypes.c_int, [ctypes.c_int, _sz, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     ("shmr_ec_device_free", ctypes.c_int, [ctypes.c_int, ctypes.c_void_p]),
+    ("shmr_ec_device_alloc_shards", ctypes.c_int, [ctypes.c_int, _sz, _sz, _sz, _u8pp]),
+    ("shmr_ec_device_free_shards", ctypes.c_int, [ctypes.c_int, _u8p]),
     ("shmr_ec_host_alloc", ctypes.c_int, [_sz, ctypes.POINTER(ctypes.c_void_p)]),
     ("shmr_ec_host_free", None, [ctypes.c_void_p]),
     ("shmr_ec_host_register", ctypes.c_int, [ctypes.c_void_p, _sz]),

@@ -12,6 +12,8 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -37,6 +39,112 @@ int guarded(F&& f) noexcept {
         return SHMR_EC_DEVICE_ERROR;
     }
 }
+// ---- slot grids in shard-pointer tables -----------------------------------------
+// A *_ptrs_dev table whose shards sit on a grid -- entry (b, j) at base +
+// b * block_pitch + j * shard_pitch, as the buffers of a Block-Cache slab do
+// (shmr_ec_device_alloc_shards, or any [blocks][shards][pitch] array) -- names
+// exactly the addresses the strided kernels of the *_batch_dev calls compute
+// from (base, pitches): those run instead, with no table to upload or chase
+// (the table kernels' first loads wait on a scalar load of the block's table
+// row).  The fit is checked against every entry, so the
+// kernels touch the same bytes either way.
+struct GridEntry {
+    uint64_t b, j;
+    int64_t addr;
+};
+struct Grid {
+    int64_t base = 0, bpitch = 0, spitch = 0;
+};
+// Entries in ascending b, then ascending j within a block.  Pitches no entry
+// pair determines are 0 (the kernels never multiply them by a nonzero index).
+bool fit_grid(const std::vector<GridEntry>& e, Grid* g) {
+    *g = Grid{};
+    if (e.empty()) return true;
+    int64_t sp = 0, bp = 0;
+    for (size_t i = 1; i < e.size(); ++i) {
+        if (e[i].b != e[i - 1].b) continue;
+        const int64_t dj = int64_t(e[i].j - e[i - 1].j), da = e[i].addr - e[i - 1].addr;
+        if (dj <= 0 || da <= 0 || da % dj) return false;
+        sp = da / dj;
+        break;
+    }
+    for (size_t i = 1; i < e.size(); ++i) {
+        if (e[i].b == e[0].b) continue;
+        const int64_t db = int64_t(e[i].b - e[0].b);
+        const int64_t da = e[i].addr - e[0].addr - (int64_t(e[i].j) - int64_t(e[0].j)) * sp;
+        if (db <= 0 || da <= 0 || da % db) return false;
+        bp = da / db;
+        break;
+    }
+    const int64_t base = e[0].addr - int64_t(e[0].b) * bp - int64_t(e[0].j) * sp;
+    for (const GridEntry& x : e)
+        if (x.addr != base + int64_t(x.b) * bp + int64_t(x.j) * sp) return false;
+    g->base = base;
+    g->bpitch = bp;
+    g->spitch = sp;
+    return true;
+}
+uint8_t* grid_ptr(const Grid& g) { return reinterpret_cast<uint8_t*>(uintptr_t(g.base)); }
+
+// The strided equivalent of a pointer-table call, if its table is a grid:
+// *handled = true and the status of the strided call; else nothing enqueued.
+int ptrs_as_grid(Codec& c, uint8_t* const* tab, const uint8_t* present, size_t nblocks, size_t len, bool data_only,
+                 int device, hipStream_t stream, core::OpClass op, bool* handled) {
+    *handled = false;
+    const unsigned k = c.k(), t = k + c.p();
+    auto addr = [&](size_t b, unsigned i) { return int64_t(uintptr_t(tab[b * t + i])); };
+    std::vector<GridEntry> in, out;
+    in.reserve(nblocks * k);
+    out.reserve(nblocks * (t - k));
+    Grid gi, go;
+    if (op == core::kEncode) {
+        for (size_t b = 0; b < nblocks; ++b)
+            for (unsigned i = 0; i < t; ++i) (i < k ? in : out).push_back({b, i < k ? i : i - k, addr(b, i)});
+        if (!fit_grid(in, &gi) || !fit_grid(out, &go)) return SHMR_EC_OK;
+        *handled = true;
+        core::count_device(device, core::kDevPtrTableGrids);
+        const core::Layout L{grid_ptr(gi), grid_ptr(go), uint64_t(gi.bpitch), uint64_t(gi.spitch),
+                             uint64_t(go.bpitch), uint64_t(go.spitch), k};
+        return core::encode_on_device(c, device, L, nblocks, len, stream);
+    }
+    // reconstruct: every shard the call touches on one grid -> in place
+    std::vector<GridEntry> all;
+    all.reserve(nblocks * t);
+    for (size_t b = 0; b < nblocks; ++b) {
+        const uint8_t* pr = present + b * t;
+        unsigned np = 0;
+        for (unsigned i = 0; i < t; ++i) np += pr[i] ? 1 : 0;
+        unsigned j = 0;
+        for (unsigned i = 0; i < t; ++i) {
+            if (pr[i]) {
+                in.push_back({b, i, addr(b, i)});
+                all.push_back({b, i, addr(b, i)});
+            } else if (np != t && (i < k || !data_only)) {   // written
+                out.push_back({b, j++, addr(b, i)});
+                all.push_back({b, i, addr(b, i)});
+            }
+        }
+    }
+    Grid ga;
+    if (fit_grid(all, &ga)) {
+        *handled = true;
+        core::count_device(device, core::kDevPtrTableGrids);
+        return core::reconstruct_on_device(c, device, grid_ptr(ga), uint64_t(ga.spitch), uint64_t(ga.bpitch), present,
+                                           nblocks, len, data_only, stream);
+    }
+    // present shards on one grid, rebuilt shards on another -> compact output
+    if (!fit_grid(in, &gi) || !fit_grid(out, &go)) return SHMR_EC_OK;
+    *handled = true;
+    core::count_device(device, core::kDevPtrTableGrids);
+    core::Layout L{grid_ptr(gi), grid_ptr(go), uint64_t(gi.bpitch), uint64_t(gi.spitch),
+                   uint64_t(go.bpitch), uint64_t(go.spitch), 0};
+    L.compact = true;
+    return core::reconstruct_on_device(c, device, L, present, nblocks, len, data_only, stream);
+}
+
+// Slabs handed out by shmr_ec_device_alloc_shards (base -> device).
+std::mutex g_slab_mu;
+std::map<uintptr_t, int> g_slabs;
 }  // namespace
 
 extern "C" {
@@ -271,6 +379,47 @@ int shmr_ec_device_free(int device, void* p) {
         if (hipFree(p) == hipSuccess) return SHMR_EC_OK;
         (void)hipGetLastError();
         return SHMR_EC_DEVICE_ERROR;
+    });
+}
+
+// ---- shard buffers in slot placement (pointer-table calls) ----------------------
+int shmr_ec_device_alloc_shards(int device, size_t nblocks, size_t shards_per_block, size_t shard_len,
+                                uint8_t** out_ptrs) {
+    return guarded([&]() -> int {
+        if (!out_ptrs || nblocks == 0 || shards_per_block == 0 || shard_len == 0) return SHMR_EC_INVALID_ARGUMENT;
+        const uint64_t n = uint64_t(nblocks) * shards_per_block;
+        if (n / nblocks != shards_per_block) return SHMR_EC_INVALID_ARGUMENT;
+        // page-aligned slots, one page more for a
+        // power-of-two stride (the bench layout's placement)
+        uint64_t pitch = core::round_up(shard_len, 4096);
+        if (pitch % 65536 == 0) pitch += 4096;
+        if (pitch < shard_len || n > UINT64_MAX / pitch) return SHMR_EC_INVALID_ARGUMENT;
+        void* slab = nullptr;
+        const int rc = shmr_ec_device_alloc(device, size_t(n * pitch), 0, &slab);
+        if (rc) return rc;
+        try {
+            std::lock_guard<std::mutex> lk(g_slab_mu);
+            g_slabs[uintptr_t(slab)] = device;
+        } catch (...) {
+            (void)shmr_ec_device_free(device, slab);
+            throw;
+        }
+        uint8_t* base = static_cast<uint8_t*>(slab);
+        for (uint64_t j = 0; j < n; ++j) out_ptrs[j] = base + j * pitch;
+        return SHMR_EC_OK;
+    });
+}
+
+int shmr_ec_device_free_shards(int device, uint8_t* first) {
+    return guarded([&]() -> int {
+        if (!first) return SHMR_EC_OK;
+        {
+            std::lock_guard<std::mutex> lk(g_slab_mu);
+            auto it = g_slabs.find(uintptr_t(first));
+            if (it == g_slabs.end() || it->second != device) return SHMR_EC_INVALID_ARGUMENT;
+            g_slabs.erase(it);
+        }
+        return shmr_ec_device_free(device, first);
     });
 }
 
@@ -621,6 +770,11 @@ static int ptrs_dev(shmr_ec_t* rs, uint8_t* const* d_shards, const uint8_t* pres
         core::DeviceScope scope(device);
         if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
         const hipStream_t stream = static_cast<hipStream_t>(stream_);
+        if (core::ptrs_grid()) {
+            bool handled = false;
+            rc = ptrs_as_grid(c, d_shards, present, nblocks, shard_len, data_only != 0, device, stream, op, &handled);
+            if (handled || rc) return rc;
+        }
         rc = core::device_init(device, stream);
         if (rc) return rc;
         // The kernels read each block's row in plan order (input t at [t],

@@ -53,6 +53,9 @@ std::atomic<int> g_alias_devices{0};   // tools build: alias device IDs (see ec_
 // Reconstructs over device shard-pointer tables take segment launches (plans in
 // the kernel arguments) when they fit; 0 = always the uploaded block/plan table
 std::atomic<int> g_ptrs_segs{1};
+// Pointer tables that name a slot grid (ptrs_dev_grid) take the strided kernels
+// of the *_batch_dev calls; 0 = always the table kernels
+std::atomic<int> g_ptrs_grid{1};
 // Misaligned device-resident shards: kAuto = the vector kernels (modes 0 / 1)
 // where the device passed probe_unaligned_vector, else the realigning kernel
 // (mode 3); 0 = always mode 3 (what a device that fails the probe runs: exact
@@ -122,6 +125,10 @@ int set_tuning(const char* key, int value) {
     }
     if (k == "ptrs_segs") {
         g_ptrs_segs = value == kAuto ? 1 : (value != 0);
+        return SHMR_EC_OK;
+    }
+    if (k == "ptrs_grid") {
+        g_ptrs_grid = value == kAuto ? 1 : (value != 0);
         return SHMR_EC_OK;
     }
     if (k == "ptrs_direct") {
@@ -235,6 +242,7 @@ int get_tuning(const char* key) {
     if (k == "bounce_kib") return g_bounce_kib;
     if (k == "mirror_zc") return g_mirror_zc;
     if (k == "ptrs_segs") return g_ptrs_segs;
+    if (k == "ptrs_grid") return g_ptrs_grid;
     if (k == "ptrs_direct") return g_ptrs_direct;
     if (k == "sync_spin_us") return g_sync_spin;
     if (k == "alias_devices") return g_alias_devices;
@@ -363,6 +371,8 @@ uint64_t bounce_limit() { return uint64_t(g_bounce_kib.load()) << 10; }
 bool mirror_zero_copy() { return g_mirror_zc.load() != 0; }
 
 uint64_t ptrs_direct_max() { return uint64_t(g_ptrs_direct.load()); }
+
+bool ptrs_grid() { return g_ptrs_grid.load() != 0; }
 
 hipError_t sync_stream(hipStream_t stream) {
     const int spin = g_sync_spin.load();

@@ -64,6 +64,11 @@ bool mirror_zero_copy();
 // across PCIe instead of uploading it first (knob "ptrs_direct"; 0 = always
 // upload).
 uint64_t ptrs_direct_max();
+// Device pointer tables whose shards form a slot grid (entry (b, j) at base +
+// b * block_pitch + j * shard_pitch: a Block-Cache slab, shmr_ec_device_alloc_shards)
+// run through the strided kernels of the *_batch_dev calls (knob "ptrs_grid",
+// default 1; 0 = always the table kernels).
+bool ptrs_grid();
 // Waits for `stream`: polls it for up to the "sync_spin_us" knob before a
 // blocking hipStreamSynchronize (short single-block calls finish within the
 // spin and skip the blocking wake-up).
@@ -93,6 +98,7 @@ enum DevCounter {
     kDevPtrTableHits,
     kDevCaptureTables,
     kDevCaptureReleased,
+    kDevPtrTableGrids,
     kDevCounters
 };
 void count_device(int dev, DevCounter c, uint64_t n = 1);

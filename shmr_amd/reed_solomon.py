@@ -21,7 +21,7 @@ from . import _native
 from ._native import _u8p, lib
 
 __all__ = ["Error", "ReedSolomon", "calculate_shard_size", "device_count", "set_tuning", "get_tuning", "describe_variant",
-           "PinnedBuffer", "host_register", "host_unregister", "path_stats", "device_init", "kernel_inventory", "capture_reserve"]
+           "PinnedBuffer", "ShardSlab", "host_register", "host_unregister", "path_stats", "device_init", "kernel_inventory", "capture_reserve"]
 
 
 class Error(Exception):
@@ -524,6 +524,58 @@ class DeviceBuffer:
             self._p = None
 
 
+class ShardSlab:
+    """Shard buffers from shmr_ec_device_alloc_shards: ``nblocks`` x
+    ``shards_per_block`` buffers of ``shard_len`` bytes at the slot pitch of the
+    device-resident batches (4 KiB-aligned slots, one page more for a
+    power-of-two stride), carved from one device slab -- a device Block Cache
+    for the crate's buffer-per-shard shape (reference src/vfs/block.rs:408-419).
+    ``ptrs`` is the uint64 address table [nblocks * shards_per_block];
+    ``shard(b, i)`` a 1-D uint8 tensor view of one shard; ``tensor()`` the
+    whole slab as [nblocks, shards_per_block, pitch]."""
+
+    def __init__(self, nblocks: int, shards_per_block: int, shard_len: int, device: int = 0):
+        self._L = lib()
+        n = nblocks * shards_per_block
+        arr = (_u8p * max(n, 1))()
+        _check(self._L.shmr_ec_device_alloc_shards(int(device), int(nblocks), int(shards_per_block), int(shard_len),
+                                                    arr))
+        self.ptrs = np.array([ctypes.cast(arr[j], ctypes.c_void_p).value for j in range(n)], dtype=np.uint64)
+        self._first = arr[0]
+        self.nblocks, self.shards_per_block, self.shard_len, self.device = nblocks, shards_per_block, shard_len, device
+        self.pitch = int(self.ptrs[1] - self.ptrs[0]) if n > 1 else (shard_len + 4095) // 4096 * 4096
+        self._views = []
+
+    def tensor(self):
+        import torch
+        view = _RawView(self, int(self.ptrs[0]), (self.nblocks, self.shards_per_block, self.pitch))
+        return torch.as_tensor(view, device=torch.device("cuda", self.device))
+
+    def shard(self, b: int, i: int):
+        import torch
+        view = _RawView(self, int(self.ptrs[b * self.shards_per_block + i]), (self.shard_len,))
+        return torch.as_tensor(view, device=torch.device("cuda", self.device))
+
+    def table(self):
+        """ctypes pointer table over ``ptrs`` (valid while the slab lives)."""
+        return self.ptrs.ctypes.data_as(ctypes.POINTER(_u8p))
+
+    def __del__(self):
+        f = getattr(self, "_first", None)
+        if f:
+            self._L.shmr_ec_device_free_shards(self.device, f)
+            self._first = None
+
+
+class _RawView:
+    """``__cuda_array_interface__`` over part of a ShardSlab (keeps it alive)."""
+
+    def __init__(self, owner, addr, shape):
+        self.owner = owner
+        self.__cuda_array_interface__ = {"shape": shape, "typestr": "|u1", "data": (addr, False), "version": 2,
+                                         "strides": None}
+
+
 def host_register(arr: np.ndarray) -> None:
     """Page-lock and map an existing C-contiguous host array for zero-copy
     use by the host-buffer entry points (shmr_ec_host_register)."""
@@ -548,7 +600,8 @@ def path_stats():
 
 
 DEVICE_COUNTERS = ("blocks_encoded", "blocks_reconstructed", "launches", "plan_images", "upload_rings",
-                   "staging_streams", "blocking_calls", "ptr_table_hits", "capture_tables", "capture_released")
+                   "staging_streams", "blocking_calls", "ptr_table_hits", "capture_tables", "capture_released",
+                   "ptr_table_grids")
 
 
 def device_init(device: int = 0) -> None:

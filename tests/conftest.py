@@ -28,3 +28,16 @@ def pytest_collection_modifyitems(config, items):
                 if "gpu" in getattr(it, "fixturenames", ()) and it.get_closest_marker("gpu") is None]
     if unmarked:
         raise pytest.UsageError("tests use the gpu fixture without @pytest.mark.gpu: " + ", ".join(unmarked))
+
+
+@pytest.fixture
+def table_kernels():
+    """Pointer-table calls take the table kernels even when their shards form a
+    slot grid (knob ptrs_grid=0): for tests of the table path itself (table
+    cache, upload chunks, the table kernels of the sweep)."""
+    import shmr_amd
+    shmr_amd.set_tuning(ptrs_grid=0)
+    try:
+        yield
+    finally:
+        shmr_amd.set_tuning(ptrs_grid=-2)

@@ -35,7 +35,8 @@ def run_bench(*args):
                                                 ("decode83", 16, ("--rebuild-out", "inplace")),
                                                 ("codec104", 4, ("--rebuild-out", "inplace")),
                                                 ("encode83", 16, ("--layout", "ptrs")),
-                                                ("decode104", 4, ("--layout", "ptrs"))])
+                                                ("decode104", 4, ("--layout", "ptrs")),
+                                                ("decode83", 16, ("--layout", "ptrs", "--ptrs-alloc", "torch"))])
 def test_bench_line_contract(gpu, config, blocks, extra):
     d = run_bench("--config", config, "--blocks", str(blocks), *extra)
     assert KEYS <= set(d)
@@ -46,6 +47,9 @@ def test_bench_line_contract(gpu, config, blocks, extra):
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
     assert 0 < r["frac"] < 1 and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
     assert "traffic" in r               # null here: the PMC table is keyed by the bench batch size
+    if "--layout" in extra:               # slab buffers: every timed call ran as a slot grid
+        slab = "torch" not in extra
+        assert d["config"]["ptr_table_grid_calls_timed"] == (3 if slab else 0)
     c = d["cpu_baseline"]
     assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0 and c["sample"]
     if config == "encode83":

@@ -186,7 +186,7 @@ def _wait_released(dev, want, timeout=10.0):
     return shmr_amd.device_stats(dev)["capture_released"]
 
 
-def test_capture_reserve_reused_across_graphs_and_large_capture(gpu):
+def test_capture_reserve_reused_across_graphs_and_large_capture(gpu, table_kernels):
     """Captured calls take their tables from the capture reserve and give them
     back when the graph is destroyed: 120 capture / replay / destroy cycles of a
     48 KiB pointer table run in the 4 MiB reserve (without the release they
@@ -337,7 +337,7 @@ def test_library_allocations_while_another_thread_captures(gpu, mode):
     assert np.array_equal(parity.cpu().numpy(), _oracle_parity(k, p, data.cpu().numpy()))
 
 
-def test_events_recorded_before_a_capture_on_that_stream(gpu):
+def test_events_recorded_before_a_capture_on_that_stream(gpu, table_kernels):
     """The library's readiness events (a plan upload, an upload-ring slot, a
     pointer-table cache entry) recorded by eager calls on stream S stay usable
     by other threads after S begins a graph capture: every query or wait goes

@@ -186,7 +186,13 @@ def _run_case(gpu, s, seed):
 
 @pytest.fixture(scope="module")
 def before():
-    return shmr_amd.kernel_inventory()
+    # the sweep's device shard views sit on a slot grid: keep them on the
+    # table kernels (knob ptrs_grid) so every pointer-table kernel is launched
+    shmr_amd.set_tuning(ptrs_grid=0)
+    try:
+        yield shmr_amd.kernel_inventory()
+    finally:
+        shmr_amd.set_tuning(ptrs_grid=-2)
 
 
 @pytest.mark.parametrize("decode", [False, True])

@@ -258,7 +258,7 @@ def test_ptrs_validation(gpu):
                                               64, 0, 0, None) == -100      # the same without data_only
 
 
-def test_ptrs_table_cache(gpu):
+def test_ptrs_table_cache(gpu, table_kernels):
     """A table passed again on the same stream is reused from the device's
     table cache (no upload; counter ptr_table_hits), and stays exact when the
     shards' bytes change between calls; a changed table, or the same table on
@@ -316,7 +316,7 @@ def test_ptrs_table_cache(gpu):
             check(s)
 
 
-def test_ptrs_many_shards_and_chunks(gpu):
+def test_ptrs_many_shards_and_chunks(gpu, table_kernels):
     """RS(200,55) (255 shards, the crate's maximum total) over 130 blocks: the
     pointer table spans two upload chunks (128 blocks per 256 KiB slot); encode,
     then a reconstruct with random erasures (up to 55 per block, mixed patterns),

@@ -1,19 +1,29 @@
 #!/usr/bin/env python3
-"""Pointer tables against padded slots, interleaved rounds in one process
-(product library).  Splits the gap between the crate's shard-per-buffer shape
-(`*_ptrs_dev`) and the Block-Cache slot layout (`*_batch_dev`, bench.py's
-default) into the kernel's own cost and the allocations' placement:
+"""The crate's shard-per-buffer shape on device (*_ptrs_dev) against the
+Block-Cache slot layout (*_batch_dev, bench.py's default), interleaved rounds
+in one process (product library).  Splits the gap into the table kernels'
+own cost and the buffers' placement, and measures the placements a Rust shim
+can get:
 
-  slots        bench.py's layout: data / parity (or compact rebuild output) in
-               page-padded slots (shard pitch roundup(S, 4 KiB), + 4 KiB when
-               that is a multiple of 64 KiB)
-  ptrs_slots   *_ptrs_dev over a pointer table naming exactly those slots: the
-               same addresses and bytes -- any difference is the table
-  ptrs_torch   *_ptrs_dev over one torch allocation per shard (bench.py
-               --layout ptrs): the caching allocator packs them back to back
-  ptrs_page    *_ptrs_dev over per-shard allocations spaced by S + 4 KiB, as
-               glibc's mmap-served Vec<u8> allocations of these sizes are
-               (reference src/vfs/block.rs:408-419)
+  slots          bench.py's layout: data / parity (or compact rebuild output) in
+                 page-padded slots (shard pitch roundup(S, 4 KiB), + 4 KiB when
+                 that is a multiple of 64 KiB), torch tensors, *_batch_dev
+  slab           shmr_ec_device_alloc_shards: all total shards of the batch in one
+                 slab (+ a second slab for rebuilt shards, one per absent shard);
+                 the table is a slot grid -> the strided kernels (knob ptrs_grid)
+  slab_sep       encode: data and parity in slabs of their own (grid)
+  slab_inplace   rebuild: absent shards rebuilt in their own slots of the slab (grid)
+  slab_tab       the slab's table with ptrs_grid=0: the table kernels over the
+                 same addresses -- any difference to `slab` is the table
+  slab_sep_tab   encode: the separate slabs with ptrs_grid=0
+  smajor         shard-major slab: shard i of block b at base + (i * B + b) * P (one
+                 grid whose data and parity shards fill separate regions; rebuilt
+                 shards in a second shard-major slab); _tab / _inplace as above
+  hipmalloc      one shmr_ec_device_alloc (hipMalloc) per shard
+  ptrs_torch     one torch allocation per shard (back to back in the caching allocator)
+  ptrs_page      per-shard allocations spaced by S + 4 KiB, 16 B past a page, as
+                 glibc's mmap-served Vec<u8> allocations of these sizes are
+                 (reference src/vfs/block.rs:408-419)
 
     python tools/ptrs_ab.py --config encode83 --rounds 11
 """
@@ -24,6 +34,7 @@ import ctypes
 import json
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -48,6 +59,7 @@ def main():
     ap.add_argument("--config", default="encode83", choices=sorted(CFG))
     ap.add_argument("--rounds", type=int, default=11)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--legs", default="", help="comma-separated subset of the legs (default: all)")
     a = ap.parse_args()
     k, p, block, er, B = CFG[a.config]
     t = k + p
@@ -66,58 +78,141 @@ def main():
         for j in range(er):
             present[rows, (rows + 3 * j) % min(t, 10)] = 0
     pr = _ptr(present)
-    runs, keep = {}, []
+    runs, keep, tables = {}, [], {}
 
-    def table(addr):   # addr(b, i) -> device address; a ctypes table [B * t]
-        arr = np.array([addr(b, i) for b in range(B) for i in range(t)], dtype=np.uint64)
+    def table(addrs):   # [B * t] uint64 addresses -> ctypes table
+        arr = np.ascontiguousarray(np.asarray(addrs, dtype=np.uint64).reshape(-1))
         keep.append(arr)
         return arr.ctypes.data_as(ctypes.POINTER(_u8p))
 
-    def ptrs_run(tab):
-        if er == 0:
-            return lambda: rs._L.shmr_ec_encode_ptrs_dev(rs._h, tab, B, S, 0, sp)
-        return lambda: rs._L.shmr_ec_reconstruct_ptrs_dev(rs._h, tab, pr, B, S, 0, 0, sp)
+    def ptrs_run(tab, grid=True):
+        def f():
+            if not grid:
+                shmr_amd.set_tuning(ptrs_grid=0)
+            try:
+                if er == 0:
+                    return rs._L.shmr_ec_encode_ptrs_dev(rs._h, tab, B, S, 0, sp)
+                return rs._L.shmr_ec_reconstruct_ptrs_dev(rs._h, tab, pr, B, S, 0, 0, sp)
+            finally:
+                if not grid:
+                    shmr_amd.set_tuning(ptrs_grid=-2)
+        return f
 
-    # slots: data [B, k, P], parity [B, p, P]; decode: all shards [B, t, P] + compact out [B, er, P]
+    def rebuilt_into(addrs, out_addr):
+        """addrs [B, t]: absent entries replaced by out_addr(b, j) (j-th absent shard)"""
+        addrs = np.array(addrs, dtype=np.uint64).reshape(B, t)
+        for b in range(B):
+            for j, i in enumerate(np.flatnonzero(present[b] == 0)):
+                addrs[b, i] = out_addr(b, j)
+        return addrs
+
+    # -- slots (bench layout) --------------------------------------------------
     if er == 0:
         data = torch.randint(0, 256, (B, k, P), dtype=torch.uint8, device=dev, generator=g)
         par = torch.empty((B, p, P), dtype=torch.uint8, device=dev)
         runs["slots"] = lambda: rs.encode_batch_dev(data, par, shard_len=S)
-        d0, p0 = data.data_ptr(), par.data_ptr()
-        runs["ptrs_slots"] = ptrs_run(table(lambda b, i: d0 + (b * k + i) * P if i < k else p0 + (b * p + i - k) * P))
     else:
         sh = torch.zeros((B, t, P), dtype=torch.uint8, device=dev)
         sh[:, :k, :S] = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=dev, generator=g)
         rs.encode_batch_dev(sh[:, :k], sh[:, k:], shard_len=S)
         out = torch.zeros((B, er, P), dtype=torch.uint8, device=dev)
         runs["slots"] = lambda: rs.reconstruct_batch_dev_out(sh, present, out, shard_len=S)
-        s0, o0 = sh.data_ptr(), out.data_ptr()
-        slot_of = {}
-        for b in range(B):
-            for j, i in enumerate(np.flatnonzero(present[b] == 0)):
-                slot_of[(b, int(i))] = o0 + (b * er + j) * P
-        runs["ptrs_slots"] = ptrs_run(table(lambda b, i: slot_of.get((b, i), s0 + (b * t + i) * P)))
-    # one torch allocation per shard (back to back in the caching allocator)
-    bufs = [[torch.randint(0, 256, (S,), dtype=torch.uint8, device=dev, generator=g) for _ in range(t)]
-            for _ in range(B)]
+
+    # -- allocator slabs --------------------------------------------------------
+    slab = shmr_amd.ShardSlab(B, t, S)
+    sv = slab.tensor()
+    sv[:, :k, :S] = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=dev, generator=g)
+    enc_tab = table(slab.ptrs)
+    assert rs._L.shmr_ec_encode_ptrs_dev(rs._h, enc_tab, B, S, 0, sp) == 0     # codewords for the rebuilds
+    if er == 0:
+        runs["slab"] = ptrs_run(enc_tab)
+        runs["slab_tab"] = ptrs_run(enc_tab, grid=False)
+        ds, ps = shmr_amd.ShardSlab(B, k, S), shmr_amd.ShardSlab(B, p, S)
+        ds.tensor()[:, :, :S] = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=dev, generator=g)
+        sep = np.concatenate([ds.ptrs.reshape(B, k), ps.ptrs.reshape(B, p)], axis=1)
+        sep_tab = table(sep)
+        runs["slab_sep"] = ptrs_run(sep_tab)
+        runs["slab_sep_tab"] = ptrs_run(sep_tab, grid=False)
+        keep.extend([ds, ps])
+    else:
+        outs = shmr_amd.ShardSlab(B, er, S)
+        dec_tab = table(rebuilt_into(slab.ptrs, lambda b, j: outs.ptrs[b * er + j]))
+        runs["slab"] = ptrs_run(dec_tab)
+        runs["slab_tab"] = ptrs_run(dec_tab, grid=False)
+        runs["slab_inplace"] = ptrs_run(enc_tab)
+        keep.append(outs)
+    keep.append(slab)
+    # shard-major slab: shard i of block b at base + (i * B + b) * P -- one grid
+    # (spitch B * P, bpitch P) whose data and parity shards fill separate regions
+    smaj = shmr_amd.DeviceBuffer(B * t * P, device=0, contiguous=False)
+    m0 = int(smaj._p.value)
+    mv = smaj.tensor((t, B, P))
+    mv[:k, :, :S] = torch.randint(0, 256, (k, B, S), dtype=torch.uint8, device=dev, generator=g)
+    sm = np.array([[m0 + (i * B + b) * P for i in range(t)] for b in range(B)], dtype=np.uint64)
+    sm_tab = table(sm)
+    assert rs._L.shmr_ec_encode_ptrs_dev(rs._h, sm_tab, B, S, 0, sp) == 0
+    keep.append(smaj)
+    if er:
+        souts = shmr_amd.DeviceBuffer(B * er * P, device=0, contiguous=False)
+        keep.append(souts)
+        o0 = int(souts._p.value)
+        sm_dec = table(rebuilt_into(sm, lambda b, j: o0 + (j * B + b) * P))
+        runs["smajor"] = ptrs_run(sm_dec)
+        runs["smajor_tab"] = ptrs_run(sm_dec, grid=False)
+        runs["smajor_inplace"] = ptrs_run(sm_tab)
+    else:
+        runs["smajor"] = ptrs_run(sm_tab)
+        runs["smajor_tab"] = ptrs_run(sm_tab, grid=False)
+
+    # -- one hipMalloc per shard (shmr_ec_device_alloc) ------------------------------
+    bufs = [[shmr_amd.DeviceBuffer(S, device=0, contiguous=False) for _ in range(t)] for _ in range(B)]
+    for blk in bufs:
+        for i in range(k):
+            blk[i].tensor().copy_(torch.randint(0, 256, (S,), dtype=torch.uint8, device=dev, generator=g))
     keep.append(bufs)
-    runs["ptrs_torch"] = ptrs_run(table(lambda b, i: bufs[b][i].data_ptr()))
-    # per-shard allocations spaced S + 4 KiB (glibc's mmap-served Vec<u8>: header page + data)
+    hm = np.array([[int(b_._p.value) for b_ in blk] for blk in bufs], dtype=np.uint64)
+    hm_tab = table(hm)
+    assert rs._L.shmr_ec_encode_ptrs_dev(rs._h, hm_tab, B, S, 0, sp) == 0
+    if er:
+        obufs = [[shmr_amd.DeviceBuffer(S, device=0, contiguous=False) for _ in range(er)] for _ in range(B)]
+        keep.append(obufs)
+        hm_tab = table(rebuilt_into(hm, lambda b, j: int(obufs[b][j]._p.value)))
+    runs["hipmalloc"] = ptrs_run(hm_tab)
+
+    # -- one torch allocation per shard ----------------------------------------------
+    tb = [[torch.randint(0, 256, (S,), dtype=torch.uint8, device=dev, generator=g) for _ in range(t)]
+          for _ in range(B)]
+    keep.append(tb)
+    tt = np.array([[s.data_ptr() for s in blk] for blk in tb], dtype=np.uint64)
+    t_tab = table(tt)
+    assert rs._L.shmr_ec_encode_ptrs_dev(rs._h, t_tab, B, S, 0, sp) == 0
+    if er:
+        tout = [[torch.zeros(S, dtype=torch.uint8, device=dev) for _ in range(er)] for _ in range(B)]
+        keep.append(tout)
+        t_tab = table(rebuilt_into(tt, lambda b, j: tout[b][j].data_ptr()))
+    runs["ptrs_torch"] = ptrs_run(t_tab)
+
+    # -- glibc-like placement ---------------------------------------------------------
     span = (S + 4096 + 4095) // 4096 * 4096
-    arena = torch.randint(0, 256, (B * t * span,), dtype=torch.uint8, device=dev, generator=g)
+    arena = torch.randint(0, 256, ((B * t + (B * er if er else 0)) * span,), dtype=torch.uint8, device=dev,
+                          generator=g)
+    keep.append(arena)
     a0 = arena.data_ptr()
-    runs["ptrs_page"] = ptrs_run(table(lambda b, i: a0 + (b * t + i) * span + 16))
-    # rebuild inputs of the pointer layouts must be codewords as well (a zero or random
-    # parity input changes the rate): encode them first
-    for name in ("ptrs_torch", "ptrs_page"):
-        if er:
-            tab = keep[-1] if name == "ptrs_page" else keep[-2]
-            assert rs._L.shmr_ec_encode_ptrs_dev(rs._h, tab.ctypes.data_as(ctypes.POINTER(_u8p)), B, S, 0, sp) == 0
+    pg = np.array([[a0 + (b * t + i) * span + 16 for i in range(t)] for b in range(B)], dtype=np.uint64)
+    pg_tab = table(pg)
+    assert rs._L.shmr_ec_encode_ptrs_dev(rs._h, pg_tab, B, S, 0, sp) == 0
+    if er:
+        pg_tab = table(rebuilt_into(pg, lambda b, j: a0 + (B * t + b * er + j) * span + 16))
+    runs["ptrs_page"] = ptrs_run(pg_tab)
+
+    if a.legs:
+        want = set(a.legs.split(","))
+        runs = {n: f for n, f in runs.items() if n in want}
     algo = B * (k + (er or p)) * S
     for f in runs.values():
         assert f() in (None, 0)
     torch.cuda.synchronize()
-    import time
+    grids0 = shmr_amd.device_stats(0)["ptr_table_grids"]
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 0.5:   # clock ramp
         for f in runs.values():
@@ -134,10 +229,13 @@ def main():
             e1.record(st)
             torch.cuda.synchronize()
             times[n].append(e0.elapsed_time(e1) / a.iters)
+    grid_calls = shmr_amd.device_stats(0)["ptr_table_grids"] - grids0
     for n, ts in times.items():
         med = float(np.median(ts))
         print(json.dumps({"config": a.config, "layout": n, "median_ms": round(med, 4), "min_ms": round(min(ts), 4),
-                          "frac": round(algo / (med / 1e3) / 8e12, 4)}))
+                          "frac": round(algo / (med / 1e3) / 8e12, 4),
+                          "build_id": shmr_amd.reed_solomon.lib().shmr_ec_build_id().decode()}))
+    print(json.dumps({"config": a.config, "grid_calls": grid_calls}))
 
 
 if __name__ == "__main__":
