@@ -105,6 +105,11 @@ def parse():
                          "shape, src/lib.rs:36-59)")
     ap.add_argument("--single-stream", default="own", choices=["own", "current"],
                     help=argparse.SUPPRESS)   # single model: a stream per device, or torch's current stream (A/B)
+    ap.add_argument("--dump-dir", default="",
+                    help="after the timed region, every rank writes the data and parity shards of its first "
+                         "--dump-blocks blocks (encode configs) with their global block ids to "
+                         "DIR/rank<r>.npz, for a test-side check against the CPU oracle")
+    ap.add_argument("--dump-blocks", type=int, default=2)
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher rehearsal without a GPU: ranks join the process group, exchange their "
                          "identities and rank 0 prints one JSON line (tests/test_bench_launch.py)")
@@ -683,6 +688,8 @@ def run(args):
         out["config"]["ptr_table_grid_calls_timed"] = grid_calls
     if shape.codec:
         out["roofline"]["round_trip_bit_exact"] = w.round_trip()
+    if args.dump_dir and shape.erasures is None:
+        dump_blocks(args, shape, w, rank, world)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_leg(args, shape, w)
     if rank == 0:
@@ -728,6 +735,17 @@ def run_single(args):
     if n == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_leg(args, shape, works[0])
     print(json.dumps(out), flush=True)
+
+
+def dump_blocks(args, shape, w, rank, world):
+    """--dump-dir: this rank's first blocks as coded (test-side oracle check of
+    every rank's share, tests/test_gpu_dist.py)."""
+    n = min(args.dump_blocks, shape.B)
+    S = shape.S
+    os.makedirs(args.dump_dir, exist_ok=True)
+    np.savez(os.path.join(args.dump_dir, f"rank{rank}.npz"),
+             data=w.data[:n, :, :S].cpu().numpy(), parity=w.parity[:n, :, :S].cpu().numpy(),
+             blocks=np.array(placement.weak_batch(shape.B, rank, world)[:n]), device=w.dev.index)
 
 
 def traffic_key(args) -> str:

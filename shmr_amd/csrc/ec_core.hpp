@@ -137,8 +137,14 @@ inline CaptureModeTls& capture_mode_tls() {
     static thread_local CaptureModeTls t;
     return t;
 }
+// (-DSHMR_EC_NO_RELAXED_CAPTURE compiles the guard out: the measurement build of
+// tools/guard_ab.cpp; never the product.)
 class RelaxedCapture {
 public:
+#ifdef SHMR_EC_NO_RELAXED_CAPTURE
+    RelaxedCapture() {}
+    ~RelaxedCapture() {}
+#else
     RelaxedCapture() {
         ok_ = hipThreadExchangeStreamCaptureMode(&prev_) == hipSuccess;
         if (!ok_) {
@@ -153,6 +159,7 @@ public:
         --capture_mode_tls().depth;
         (void)hipThreadExchangeStreamCaptureMode(&prev_);
     }
+#endif
     RelaxedCapture(const RelaxedCapture&) = delete;
     RelaxedCapture& operator=(const RelaxedCapture&) = delete;
 

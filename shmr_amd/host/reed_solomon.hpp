@@ -37,7 +37,13 @@ public:
         op_ = nullptr;
         return EcStatus{o ? shmr_ec_op_wait(o) : SHMR_EC_OK};
     }
-    shmr_ec_op_t** out() { return &op_; }
+    // For a *_start call: an op still pending from an earlier start is waited
+    // for first (its kernels may still use that call's buffers; handing out
+    // &op_ would make the C call overwrite it with NULL and lose it).
+    shmr_ec_op_t** out() {
+        if (op_) (void)wait();
+        return &op_;
+    }
 
 private:
     shmr_ec_op_t* op_ = nullptr;

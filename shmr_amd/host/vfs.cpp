@@ -664,6 +664,22 @@ Status VirtualBlock::sync_data(bool force, int device, PhaseTimes* times) const 
             });
             const double tw2 = times ? now_s() : 0;
             es = op.wait();
+            if (es.ok() && opt_.fault_encode_wait) es = EcStatus{SHMR_EC_DEVICE_ERROR};   // test hook
+            if (!es.ok()) {
+                // The data shard files already hold the new bytes while the parity
+                // files hold the old parity: the stripe is no codeword.  Make that
+                // detectable -- every parity file truncated to 0 bytes (a short
+                // shard: an erasure under VfsOptions::short_shard_is_erasure /
+                // missing_shard_is_erasure), never a silent rebuild from stale
+                // parity -- and leave the block dirty so the next flush re-encodes.
+                // (The reference unwraps the encode before any write, block.rs:427.)
+                for (size_t i = k; i < nw; ++i) {
+                    if (st_->ensure_fd(i, *cfg_)) continue;
+                    const int fd = st_->handles[i].second;
+                    if (::ftruncate(fd, 0) == 0 && opt_.fsync_shards) (void)::fsync(fd);
+                }
+                st_->should_flush.store(true);
+            }
             if (times) times->codec_s += now_s() - tc - (tw2 - tw), times->io_s += tw2 - tw;
             if (es.ok() && nw > k) {
                 const double tp = times ? now_s() : 0;

@@ -133,6 +133,10 @@ struct VfsOptions {
     // fsync every shard file after writing it (write_path, block.rs:633).
     // Benchmarks may turn it off to separate the device path from the disk.
     bool fsync_shards = true;
+    // Test hook: a per-block Erasure flush reports a device error at the
+    // encode's wait, after the data shard files went out (the failure path
+    // that truncates the parity files and keeps the block dirty).
+    bool fault_encode_wait = false;
 };
 
 // Where a VirtualFile flush / batched load spent its time (last call).

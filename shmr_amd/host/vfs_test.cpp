@@ -546,6 +546,56 @@ void test_erasure_block_missing_shards() {
     CHECK(st && st->kind == ShmrError::EcError && st->code == SHMR_EC_TOO_FEW_SHARDS_PRESENT);
 }
 
+// A per-block flush whose encode fails at the wait, after the data shard
+// files went out (mapped Block Cache: started encode): the parity files are
+// truncated (the stripe is detectably no codeword), the block stays dirty,
+// and the next flush -- forced or not -- re-encodes and rewrites the stripe.
+void test_erasure_flush_encode_failure() {
+    auto cfg = test_config();
+    auto in = read_input();
+    const uint64_t size = 1024 * 1024;
+    CHECK(in.size() >= 2 * size);
+    const size_t S = calculate_shard_size(size, 8);
+    VirtualBlock b;
+    CHECK_OK(VirtualBlock::create(19, 0, cfg, size, BlockTopology::erasure(1, 8, 3), &b));
+    VfsOptions o;
+    o.missing_shard_is_erasure = true;
+    o.short_shard_is_erasure = true;
+    o.pread_from_start = true;
+    o.pinned_buffers = true;
+    b.set_options(o);
+    size_t n = 0;
+    CHECK_OK(b.write(0, in.data(), size, &n));
+    CHECK_OK(b.sync_data(true));
+    for (size_t i = 0; i < 11; ++i) CHECK(fsize(shard_file(*cfg, b, i)) == S);
+    // new bytes; the flush's encode fails at the wait
+    CHECK_OK(b.write(0, in.data() + size, size, &n));
+    o.fault_encode_wait = true;
+    b.set_options(o);
+    Status st = b.sync_data(true);
+    CHECK(st && st->kind == ShmrError::EcError && st->code == SHMR_EC_DEVICE_ERROR);
+    for (size_t i = 0; i < 8; ++i) {   // the data shards went out
+        std::ifstream f(shard_file(*cfg, b, i), std::ios::binary);
+        std::vector<uint8_t> got(S);
+        f.read(reinterpret_cast<char*>(got.data()), std::streamsize(S));
+        CHECK(std::equal(got.begin(), got.end(), in.begin() + size + i * S));
+    }
+    for (size_t i = 8; i < 11; ++i) CHECK(fsize(shard_file(*cfg, b, i)) == 0);   // no stale parity
+    // the block is still dirty: an unforced flush re-encodes
+    o.fault_encode_wait = false;
+    b.set_options(o);
+    CHECK_OK(b.sync_data(false));
+    for (size_t i = 8; i < 11; ++i) CHECK(fsize(shard_file(*cfg, b, i)) == S);
+    CHECK_OK(b.drop_buffer());
+    CHECK_OK(b.drop_handles());
+    fs::remove(shard_file(*cfg, b, 2));
+    fs::remove(shard_file(*cfg, b, 6));
+    std::vector<uint8_t> rb(size);
+    CHECK_OK(b.read(0, rb.data(), rb.size(), &n));
+    CHECK(std::equal(rb.begin(), rb.end(), in.begin() + size));
+    print_shards(*cfg, 0, b);
+}
+
 // VirtualFile with Erasure blocks: one batched GPU encode per flush.
 void test_virtual_file_erasure_batch() {
     auto cfg = test_config();
@@ -1175,6 +1225,7 @@ int main(int argc, char** argv) {
         {"virtual_file_chunk_model", test_virtual_file_chunk_model},
         {"erasure_block_sync_load", test_erasure_block_sync_load},
         {"erasure_block_missing_shards", test_erasure_block_missing_shards},
+        {"erasure_flush_encode_failure", test_erasure_flush_encode_failure},
         {"virtual_file_erasure_batch", test_virtual_file_erasure_batch},
         {"replace_block_erasure", test_replace_block_erasure},
         {"virtual_file_batched_reconstruct", test_virtual_file_batched_reconstruct},

@@ -117,3 +117,24 @@ def test_cpu_threads_default_is_available_parallelism(monkeypatch):
     monkeypatch.setattr(bench, "cpu_quota", lambda: 16.0)
     assert bench.cpu_threads(0) == 16
     assert bench.cpu_threads(5) == 5
+
+
+def test_direct_launch_eight_ranks():
+    """The driver's N = 8 launch shape (bench.py started directly): eight
+    ranks, one line, ranks 0..7 with their own processes."""
+    r = _run([sys.executable, BENCH, "--gpus", "8", "--launch-check"], timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1 and lines[0]["ranks_seen"] == 8 and lines[0]["n_gpus"] == 8
+    assert [x["rank"] for x in lines[0]["ranks"]] == list(range(8))
+    assert len({x["pid"] for x in lines[0]["ranks"]}) == 8
+
+
+def test_torchrun_launch_eight_ranks():
+    r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+              "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), BENCH, "--gpus", "8", "--launch-check"],
+             timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1 and lines[0]["ranks_seen"] == 8
+    assert [x["local_rank"] for x in lines[0]["ranks"]] == list(range(8))

@@ -47,8 +47,8 @@ def _worker(rank, world, port, nblocks, out_q):
         dist.destroy_process_group()
 
 
-def test_round_robin_partition_world2():
-    world, nblocks = 2, 11
+@pytest.mark.parametrize("world,nblocks", [(2, 11), (8, 29)])
+def test_round_robin_partition(world, nblocks):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -62,8 +62,11 @@ def test_round_robin_partition_world2():
     results.sort()
     parts = [r[1] for r in results]
     assert placement.check_partition(parts, nblocks)
-    assert parts[0] == [0, 2, 4, 6, 8, 10] and parts[1] == [1, 3, 5, 7, 9]
-    assert all(r[3] == 2.0 for r in results)               # max over ranks
+    if world == 2:
+        assert parts[0] == [0, 2, 4, 6, 8, 10] and parts[1] == [1, 3, 5, 7, 9]
+    for r, part in enumerate(parts):
+        assert part == list(range(r, nblocks, world))
+    assert all(r[3] == float(world) for r in results)      # max over ranks (rank r reports 1 + r)
     # every rank's parity equals a single-process encode of the same block
     from oracle import c_oracle
     from oracle import rs_oracle as O

@@ -270,6 +270,55 @@ def test_capture_reserve_reused_across_graphs_and_large_capture(gpu, table_kerne
     gc.collect()
 
 
+def test_capture_block_not_reused_while_a_replay_is_queued(gpu, table_kernels):
+    """A captured call's table block goes back to the capture reserve when its
+    graph is destroyed.  Destroying the graph (and its executable) while a
+    replay is still queued -- behind a long kernel on the replay's stream --
+    must not let a new capture take that block: the new capture writes its own
+    table into it at once, and the queued replay's H2D node and kernel would
+    then read the other call's shard pointers.  The first replay
+    must hit only its own buffers."""
+    import ctypes
+    import gc
+    import torch
+    shmr_amd.device_init(0)
+    k, p, S, B = 4, 2, 4096 * 4, 64
+    t = k + p
+    rs = shmr_amd.ReedSolomon(k, p)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    buf1 = torch.randint(0, 256, (B * t * S,), dtype=torch.uint8, device=gpu)
+    buf2 = torch.randint(0, 256, (B * t * S,), dtype=torch.uint8, device=gpu)
+    _, tab1 = _ptr_table(buf1.data_ptr(), B, t, S)
+    _, tab2 = _ptr_table(buf2.data_ptr(), B, t, S)
+    g1 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g1, stream=s1):
+        assert rs._L.shmr_ec_encode_ptrs_dev(rs._h, tab1, B, S, 0, ctypes.c_void_p(s1.cuda_stream)) == 0
+    buf1.view(B, t, S)[:, k:] = 0
+    buf2.view(B, t, S)[:, k:] = 0
+    torch.cuda.synchronize()
+    st0 = shmr_amd.device_stats(0)
+    with torch.cuda.stream(s1):
+        torch.cuda._sleep(400_000_000)       # ~0.2 s: the replay below waits behind it
+        g1.replay()
+    del g1
+    gc.collect()
+    early = shmr_amd.device_stats(0)["capture_released"] - st0["capture_released"]
+    g2 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g2, stream=s2):
+        assert rs._L.shmr_ec_encode_ptrs_dev(rs._h, tab2, B, S, 0, ctypes.c_void_p(s2.cuda_stream)) == 0
+    torch.cuda.synchronize()
+    h1 = buf1.view(B, t, S).cpu().numpy()
+    print(f"capture blocks released before the queued replay ran: {early}")
+    assert not buf2.view(B, t, S)[:, k:].any().item(), "the queued replay wrote through the new capture's table"
+    assert np.array_equal(h1[:, k:], _oracle_parity(k, p, h1[:, :k])), "the queued replay lost its own table"
+    g2.replay()
+    torch.cuda.synchronize()
+    h2 = buf2.view(B, t, S).cpu().numpy()
+    assert np.array_equal(h2[:, k:], _oracle_parity(k, p, h2[:, :k]))
+    del g2
+    gc.collect()
+
+
 @pytest.mark.parametrize("mode", ["global", "thread_local"])
 def test_library_allocations_while_another_thread_captures(gpu, mode):
     """One thread holds a graph capture open while another makes calls that

@@ -34,7 +34,7 @@ def _env():
     return dict(os.environ, SHMR_BENCH_SHARE_GPU="1", MASTER_ADDR="127.0.0.1")
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_library_round_robin_ranks(gpu, world):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "tests", "gpu_dist_worker.py")]
@@ -70,3 +70,34 @@ def test_bench_self_launch_two_ranks(gpu, config):
     assert b["n_gpus"] == 2 and b["ranks_seen"] == 2 and b["launcher"] == "spawn"
     assert b["config"]["global_batch_blocks"] == 32 and b["value"] > 0 and b["cpu_baseline"] is None
     assert [d["rank"] for d in b["devices"]] == [0, 1]
+
+
+def test_bench_self_launch_eight_ranks(gpu, tmp_path):
+    """bench.py --gpus 8 as the driver's 8-GPU run starts it, on one GPU
+    (SHMR_BENCH_SHARE_GPU=1): eight ranks join, the line counts them and
+    reports the one physical GPU honestly (distinct_gpus 1), the global batch
+    is 8 x B blocks round-robin, and every rank's coded blocks equal the
+    oracle's (each rank dumps its first blocks after the timed region)."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--blocks", "4", "--steps", "3",
+           "--warmup", "1", "--ramp-seconds", "0.05", "--no-cpu", "--dump-dir", str(tmp_path), "--dump-blocks", "2"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=_env())
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    b = json.loads(lines[0])
+    assert b["n_gpus"] == 8 and b["ranks_seen"] == 8 and b["launcher"] == "spawn"
+    assert [d["rank"] for d in b["devices"]] == list(range(8))
+    assert b["distinct_gpus"] == 1                 # one physical GPU shared by the eight ranks
+    assert b["config"]["global_batch_blocks"] == 32 and b["scaling"] == "weak" and b["value"] > 0
+    seen = []
+    for r in range(8):
+        z = np.load(os.path.join(str(tmp_path), f"rank{r}.npz"))
+        data, parity, blocks = z["data"], z["parity"], z["blocks"]
+        assert list(blocks) == placement.weak_batch(4, r, 8)[:2]
+        assert all(placement.owner(int(g), 8) == r for g in blocks)
+        seen.extend(int(g) for g in blocks)
+        n, k, S = data.shape
+        want = np.zeros((n, parity.shape[1], S), np.uint8)
+        c_oracle.encode_batch(k, parity.shape[1], np.ascontiguousarray(data), want, n, S, 8)
+        assert np.array_equal(parity, want), f"rank {r}"
+    assert len(set(seen)) == 16

@@ -162,3 +162,65 @@ def test_device_batch_on_alias_id(aliases):
     with pytest.raises(shmr_amd.Error) as e:       # one past the last alias
         rs.encode_batch_dev(data, parity, shard_len=S, device=n + 3)
     assert e.value.code == INVALID
+
+
+def test_eight_device_ids_single_process(gpu):
+    """The daemon's single-process shape at N = 8, rehearsed with alias IDs
+    (tools build; alias_devices = 8 - n): per-device state created by eight
+    threads at once, then pageable and mapped host batches (encode and a
+    reconstruct of two erasures per block, a pattern per block) round-robin
+    over eight IDs.  Every ID shows its own counter set (blocks, plan images,
+    staging streams, upload rings) and every byte equals the oracle's."""
+    import threading
+    with _native.tools():
+        n = shmr_amd.device_count()
+        extra = max(0, 8 - n)
+        shmr_amd.set_tuning(alias_devices=max(extra, 1))
+        try:
+            ids = list(range(8))
+            errs = []
+
+            def init(d):
+                try:
+                    shmr_amd.device_init(d)
+                except Exception as e:   # reported below
+                    errs.append((d, repr(e)))
+            th = [threading.Thread(target=init, args=(d,)) for d in ids]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join(60)
+            assert not errs, errs
+            k, p, S, B = 8, 3, 65536 + 48, 24
+            rs = shmr_amd.ReedSolomon(k, p)
+            before = {d: shmr_amd.device_stats(d) for d in ids}
+            blk = _blocks(k, p, S, B, 11)
+            want = _expect(k, p, blk)
+            rs.encode_blocks_host(blk, devices=ids)                  # pageable: per-device pinned mirrors
+            assert np.array_equal(blk, want)
+            slab = shmr_amd.PinnedBuffer(B * (k + p) * S)             # mapped: zero-copy per device
+            arr = slab.array.reshape(B, k + p, S)
+            arr[:] = _blocks(k, p, S, B, 12)
+            want2 = _expect(k, p, arr.copy())
+            rs.encode_blocks_host(arr, devices=ids)
+            assert np.array_equal(arr, want2)
+            present = np.ones((B, k + p), np.uint8)
+            for b in range(B):
+                present[b, [b % (k + p), (b + 4) % (k + p)]] = 0
+            arr[present == 0] = 0
+            rs.reconstruct_blocks_host(arr, present, devices=ids)
+            assert np.array_equal(arr, want2)
+            work = want.copy()
+            work[present == 0] = 0xEE
+            rs.reconstruct_blocks_host(work, present, devices=ids)
+            assert np.array_equal(work, want)
+            after = {d: shmr_amd.device_stats(d) for d in ids}
+            for d in ids:
+                dd = _delta(before[d], after[d])
+                assert dd["blocks_encoded"] == 2 * B // 8, (d, dd)
+                assert dd["blocks_reconstructed"] == 2 * B // 8, (d, dd)
+                assert after[d]["plan_images"] >= 1 and after[d]["staging_streams"] >= 1, (d, after[d])
+                assert after[d]["upload_rings"] >= 1, (d, after[d])
+            del slab
+        finally:
+            shmr_amd.set_tuning(alias_devices=0)
