@@ -63,6 +63,23 @@ def test_mul_slice_kat(c, inp, want):
         assert c_oracle.apply(np.array([[c]], np.uint8), [x], len(x), variant=variant)[0].tolist() == want
 
 
+@pytest.mark.parametrize("c,inp,want", KAT["published"]["mul_slice_full"])
+def test_mul_slice_full_upstream_vector(c, inp, want):
+    """All 34 inputs of the upstream mul_slice(25) vector, each byte checked
+    on its own (so a failure names the input)."""
+    for x, y in zip(inp, want):
+        assert O.gal_mul(c, x) == y, (c, x)
+    got = np.zeros(len(inp), np.uint8)
+    O.mul_slice(c, np.array(inp, np.uint8), got)
+    assert list(got) == want
+
+
+def test_published_kats_name_their_source():
+    pub = KAT["published"]
+    for key in ("gal_mul", "gal_exp", "mul_slice", "mul_slice_full", "encode", "mat_mul", "mat_invert"):
+        assert key in pub and pub["sources"][key], key
+
+
 @pytest.mark.parametrize("a,b,want", KAT["published"]["mat_mul"])
 def test_mat_mul_kat(a, b, want):
     assert O.mat_mul(np.array(a, np.uint8), np.array(b, np.uint8)).tolist() == want
