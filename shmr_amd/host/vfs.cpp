@@ -4,6 +4,7 @@
 
 #include <fcntl.h>
 #include <sys/stat.h>
+#include <sys/statfs.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -427,6 +428,109 @@ int read_slot_counted(int fd, uint8_t* slot, size_t S, bool from_start, bool* od
     return read_slot(fd, slot, S, from_start, odd);
 }
 
+// ---- direct I/O (VfsOptions::direct_io) -------------------------------------
+// Shard files read into / written from the Block-Cache slots with O_DIRECT:
+// the bytes move between the disk and the (page-aligned, possibly mapped)
+// slot with no page-cache copy.  Only whole 4 KiB-aligned slots qualify (S a
+// multiple of 4096 -- RS(8,3) 4 MiB blocks; RS(10,4) 16 MiB's S = 1,677,722
+// does not); everything else, and every file system that refuses O_DIRECT
+// (tmpfs, overlay: EINVAL at open), takes the buffered path.  The on-disk
+// format is unchanged: raw S bytes per shard at offset 0 (block.rs:611-634).
+constexpr size_t kDirectAlign = 4096;
+struct DirectStats {
+    std::atomic<uint64_t> reads{0}, writes{0}, fallbacks{0}, refusals{0};
+    std::mutex mu;
+    int refused_errno = 0;
+    std::string refused_fs;
+    int io_errno = 0;   // first O_DIRECT read/write error (e.g. EFAULT: a buffer the kernel cannot pin)
+};
+DirectStats& g_direct() {
+    static DirectStats* d = new DirectStats;   // leaked: outlives static destructors
+    return *d;
+}
+void note_direct_io_error(int err) {
+    DirectStats& d = g_direct();
+    std::lock_guard<std::mutex> lock(d.mu);
+    if (!d.io_errno) d.io_errno = err;
+}
+bool direct_eligible(const void* p, size_t S) {
+    return S > 0 && S % kDirectAlign == 0 && (uintptr_t(p) % kDirectAlign) == 0;
+}
+std::string fs_name(const fs::path& file) {
+    struct statfs sf {};
+    if (::statfs(file.parent_path().c_str(), &sf) != 0) return "unknown";
+    switch (static_cast<unsigned long>(sf.f_type)) {
+        case 0x01021994UL: return "tmpfs";
+        case 0x794c7630UL: return "overlayfs";
+        case 0xEF53UL: return "ext4";
+        case 0x58465342UL: return "xfs";
+        case 0x9123683EUL: return "btrfs";
+        case 0x6969UL: return "nfs";
+        case 0x65735546UL: return "fuse";
+        default: {
+            char b[32];
+            std::snprintf(b, sizeof b, "0x%lx", static_cast<unsigned long>(sf.f_type));
+            return b;
+        }
+    }
+}
+// An O_DIRECT descriptor of `file`, or -1 (refusal recorded once per errno).
+int open_direct(const fs::path& file) {
+    const int fd = ::open(file.c_str(), O_RDWR | O_CREAT | O_DIRECT, 0644);
+    if (fd >= 0) return fd;
+    const int err = errno;
+    DirectStats& d = g_direct();
+    d.refusals.fetch_add(1, std::memory_order_relaxed);
+    std::lock_guard<std::mutex> lock(d.mu);
+    if (!d.refused_errno) {
+        d.refused_errno = err;
+        d.refused_fs = fs_name(file);
+    }
+    return -1;
+}
+// pwrite of a whole aligned slot at offset 0 (+ fdatasync): write_path's
+// twin.  Returns 0, or the errno of a failed write (the caller then writes
+// the shard buffered: O_DIRECT can refuse a buffer, e.g. EFAULT for memory
+// the kernel cannot pin, or EINVAL).
+int write_direct(int fd, const uint8_t* buf, size_t len, bool sync) {
+    size_t done = 0;
+    while (done < len) {
+        const ssize_t n = ::pwrite(fd, buf + done, len - done, off_t(done));
+        if (n < 0) {
+            if (errno == EINTR) continue;
+            return errno;
+        }
+        if (n == 0) return EIO;
+        done += size_t(n);
+    }
+    if (sync && ::fdatasync(fd) != 0) return errno;
+    g_direct().writes.fetch_add(1, std::memory_order_relaxed);
+    return 0;
+}
+// read_slot's twin for a file of exactly S bytes (from offset 0); returns -1
+// when the file has another length (the caller reads it buffered: the
+// reference's zero-pad / drain rules need the exact byte count).
+int read_slot_direct(int fd, uint8_t* slot, size_t S, bool* odd) {
+    struct stat st {};
+    if (::fstat(fd, &st) != 0) return errno;
+    if (uint64_t(st.st_size) != S) return -1;
+    size_t got = 0;
+    while (got < S) {
+        const ssize_t n = ::pread(fd, slot + got, S - got, off_t(got));
+        if (n < 0) {
+            if (errno == EINTR) continue;
+            return errno;
+        }
+        if (n == 0) break;
+        got += size_t(n);
+    }
+    if (got != S) return -1;
+    *odd = false;
+    g_shard_reads.fetch_add(1, std::memory_order_relaxed);
+    g_direct().reads.fetch_add(1, std::memory_order_relaxed);
+    return 0;
+}
+
 // VfsOptions::read_needed_shards: which shard files of an Erasure block a
 // load reads (plan[i]: kRead, kPresentUnread, or kAbsent).  The reference
 // reads all k+p (block.rs:531-556) and returns ec_data[..size] (block.rs:576).  The file sizes
@@ -481,11 +585,58 @@ struct VirtualBlock::State {
         handles[i].second = fd;
         return std::nullopt;
     }
+    // VfsOptions::direct_io: shard i's O_DIRECT descriptor, opened on first
+    // use (creating the file like ensure_fd); -1 when the file system refuses
+    // it (then never retried for this handle).  Caller holds handles_mu.
+    int direct_fd(size_t i, const ShmrFsConfig& cfg) {
+        if (dfds.size() < handles.size()) dfds.resize(handles.size(), -1);
+        if (dfds[i] >= 0 || dfds[i] == -2) return dfds[i] >= 0 ? dfds[i] : -1;
+        fs::path file;
+        if (handles[i].first.resolve(cfg, &file, nullptr)) return -1;
+        const int fd = open_direct(file);
+        dfds[i] = fd >= 0 ? fd : -2;
+        return fd;
+    }
     void close_handles() {
         for (auto& h : handles)
             if (h.second >= 0) ::close(h.second);
         handles.clear();
+        for (int fd : dfds)
+            if (fd >= 0) ::close(fd);
+        dfds.clear();
     }
+    // Writes shard i from `buf` (write_path; O_DIRECT under direct_io when the
+    // slot qualifies).
+    Status write_shard(size_t i, const ShmrFsConfig& cfg, const VfsOptions& o, const uint8_t* buf, size_t len) {
+        if (auto e = ensure_fd(i, cfg)) return e;
+        if (o.direct_io && direct_eligible(buf, len)) {
+            const int dfd = direct_fd(i, cfg);
+            if (dfd >= 0) {
+                const int err = write_direct(dfd, buf, len, o.fsync_shards);
+                if (err == 0) return std::nullopt;
+                note_direct_io_error(err);
+            }
+            g_direct().fallbacks.fetch_add(1, std::memory_order_relaxed);
+        }
+        return write_path(handles[i].second, buf, len, o.fsync_shards);
+    }
+    // Reads shard i into its slot (read_slot; O_DIRECT under direct_io for an
+    // intact file into a qualifying slot, read from offset 0).
+    int read_shard(size_t i, int fd, const ShmrFsConfig& cfg, const VfsOptions& o, uint8_t* slot, size_t S,
+                   bool* odd) {
+        if (o.direct_io && o.pread_from_start && direct_eligible(slot, S) && i < handles.size() &&
+            handles[i].second >= 0) {
+            const int dfd = direct_fd(i, cfg);
+            if (dfd >= 0) {
+                const int rc = read_slot_direct(dfd, slot, S, odd);
+                if (rc == 0) return 0;
+                if (rc > 0) note_direct_io_error(rc);   // read buffered below (-1: not exactly S bytes)
+            }
+            g_direct().fallbacks.fetch_add(1, std::memory_order_relaxed);
+        }
+        return read_slot_counted(fd, slot, S, o.pread_from_start, odd);
+    }
+    std::vector<int> dfds;   // O_DIRECT descriptors (direct_io), -1 unopened, -2 refused
     ~State() { close_handles(); }
 };
 
@@ -658,10 +809,7 @@ Status VirtualBlock::sync_data(bool force, int device, PhaseTimes* times) const 
         if (es.ok()) {
             const size_t k = topology.data, nw = std::min(n, nh);
             const double tw = times ? now_s() : 0;
-            parallel_for(std::min(k, nw), 16, [&](size_t i) {
-                res[i] = st_->ensure_fd(i, *cfg_);
-                if (!res[i]) res[i] = write_path(st_->handles[i].second, ptrs[i], S, opt_.fsync_shards);
-            });
+            parallel_for(std::min(k, nw), 16, [&](size_t i) { res[i] = st_->write_shard(i, *cfg_, opt_, ptrs[i], S); });
             const double tw2 = times ? now_s() : 0;
             es = op.wait();
             if (es.ok() && opt_.fault_encode_wait) es = EcStatus{SHMR_EC_DEVICE_ERROR};   // test hook
@@ -685,8 +833,7 @@ Status VirtualBlock::sync_data(bool force, int device, PhaseTimes* times) const 
                 const double tp = times ? now_s() : 0;
                 parallel_for(nw - k, 16, [&](size_t j) {
                     const size_t i = k + j;
-                    res[i] = st_->ensure_fd(i, *cfg_);
-                    if (!res[i]) res[i] = write_path(st_->handles[i].second, ptrs[i], S, opt_.fsync_shards);
+                    res[i] = st_->write_shard(i, *cfg_, opt_, ptrs[i], S);
                 });
                 if (times) times->io_s += now_s() - tp;
             }
@@ -770,7 +917,7 @@ Status VirtualBlock::load_block(bool* reconstructed, int device, PhaseTimes* tim
         if (!planned) std::fill(plan.begin(), plan.end(), uint8_t(kRead));
         auto read_one = [&](size_t i) {
             bool o = false;
-            if (fds[i] >= 0 && read_slot_counted(fds[i], ptrs[i], S, opt_.pread_from_start, &o) == 0) {   // Err -> None
+            if (fds[i] >= 0 && st_->read_shard(i, fds[i], *cfg_, opt_, ptrs[i], S, &o) == 0) {   // Err -> None
                 present[i] = !(o && opt_.short_shard_is_erasure);
                 odd[i] = o;
             }
@@ -1242,10 +1389,8 @@ Status VirtualFile::sync_data(bool force) {
         std::vector<Status> task_res(tasks.size());
         parallel_for(tasks.size(), 32, [&](size_t t) {
             auto& st = *blocks[tasks[t].blk].st_;
-            task_res[t] = st.ensure_fd(tasks[t].shard, *cfg_);
-            if (!task_res[t])
-                task_res[t] = write_path(st.handles[tasks[t].shard].second, st.buffer.data() + tasks[t].shard * g.S,
-                                         g.S, blocks[tasks[t].blk].opt_.fsync_shards);
+            task_res[t] = st.write_shard(tasks[t].shard, *cfg_, blocks[tasks[t].blk].opt_,
+                                         st.buffer.data() + tasks[t].shard * g.S, g.S);
         });
         for (size_t t = 0; t < tasks.size(); ++t)
             if (task_res[t] && !results[tasks[t].blk]) results[tasks[t].blk] = task_res[t];
@@ -1414,7 +1559,7 @@ Status VirtualFile::load_blocks(const std::vector<size_t>& block_indices,
             const Task& tk = tasks[t];
             const VfsOptions& o = blocks[tk.blk].opt_;
             bool od = false;
-            if (tk.fd >= 0 && read_slot_counted(tk.fd, tk.slot, tk.S, o.pread_from_start, &od) == 0) {
+            if (tk.fd >= 0 && blocks[tk.blk].st_->read_shard(tk.shard, tk.fd, *cfg_, o, tk.slot, tk.S, &od) == 0) {
                 present[t] = !(od && o.short_shard_is_erasure);
                 odd[t] = od;
             }
@@ -1571,5 +1716,19 @@ Status VirtualFile::rewrite_erasure(uint8_t data, uint8_t parity) {
 size_t block_cache_trim() { return BufferPool::get().trim(); }
 
 uint64_t shard_reads_total() { return g_shard_reads.load(); }
+
+DirectIoStats direct_io_stats() {
+    DirectStats& d = g_direct();
+    DirectIoStats out;
+    out.reads = d.reads.load();
+    out.writes = d.writes.load();
+    out.fallbacks = d.fallbacks.load();
+    out.refusals = d.refusals.load();
+    std::lock_guard<std::mutex> lock(d.mu);
+    out.refused_errno = d.refused_errno;
+    out.refused_fs = d.refused_fs;
+    out.io_errno = d.io_errno;
+    return out;
+}
 
 }  // namespace shmr

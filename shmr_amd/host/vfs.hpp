@@ -137,7 +137,27 @@ struct VfsOptions {
     // encode's wait, after the data shard files went out (the failure path
     // that truncates the parity files and keeps the block dirty).
     bool fault_encode_wait = false;
+    // Shard files read into and written from the Block-Cache slots with
+    // O_DIRECT (no page-cache copy; raw S bytes at offset 0, the same files).
+    // Applies to slots that are whole 4 KiB-aligned pages (S a multiple of
+    // 4096) and reads from offset 0 (pread_from_start); a file system that
+    // refuses O_DIRECT (tmpfs, overlay) and any other slot take the buffered
+    // path (direct_io_stats() counts both).  Reads of hot files then come
+    // from the disk instead of the page cache.
+    bool direct_io = false;
 };
+
+// What VfsOptions::direct_io did since the library was loaded: shard files
+// read / written with O_DIRECT, shard I/O that fell back to the buffered path
+// (refused, failed, or a file that is not exactly S bytes), refused opens, the
+// first refusal's errno and file system, and the first O_DIRECT I/O error.
+struct DirectIoStats {
+    uint64_t reads = 0, writes = 0, fallbacks = 0, refusals = 0;
+    int refused_errno = 0;
+    std::string refused_fs;
+    int io_errno = 0;   // first O_DIRECT read/write error (the shard then went buffered)
+};
+DirectIoStats direct_io_stats();
 
 // Where a VirtualFile flush / batched load spent its time (last call).
 // The codec and I/O phases of a batch are pipelined (batch b+1's codec call

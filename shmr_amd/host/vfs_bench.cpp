@@ -164,7 +164,11 @@ int main(int argc, char** argv) {
     std::vector<size_t> batch_mib = {VirtualFile::kAutoBatch, 0};
     for (int i = 6; i < argc; ++i) batch_mib.push_back(std::strtoull(argv[i], nullptr, 10));
     // read_needed_shards (8 of 11 shard reads per load) for the auto batch
-    for (int pinned = 1; pinned >= 0; --pinned)
+    // SHMR_VFS_DIRECT=1: shard files through O_DIRECT (VfsOptions::direct_io);
+    // SHMR_VFS_PINNED_ONLY=1: the mapped Block Cache modes only
+    const bool direct = std::getenv("SHMR_VFS_DIRECT") && std::atoi(std::getenv("SHMR_VFS_DIRECT")) != 0;
+    const bool pinned_only = std::getenv("SHMR_VFS_PINNED_ONLY") && std::atoi(std::getenv("SHMR_VFS_PINNED_ONLY")) != 0;
+    for (int pinned = 1; pinned >= (pinned_only ? 1 : 0); --pinned)
     for (size_t bm : batch_mib)
     for (int needed = 0; needed <= (bm == VirtualFile::kAutoBatch ? 1 : 0); ++needed) {
         VfsOptions o;
@@ -174,6 +178,8 @@ int main(int argc, char** argv) {
         o.short_shard_is_erasure = true;
         o.pinned_buffers = pinned != 0;
         o.fsync_shards = do_fsync;
+        o.direct_io = direct;
+        const DirectIoStats d0 = direct_io_stats();
         Result best;
         best.sync_s = best.read_s = best.write_s = best.per_block_sync_s = 1e30;
         uint64_t zc0 = 0, st0 = 0, zc1 = 0, st1 = 0;
@@ -203,6 +209,15 @@ int main(int argc, char** argv) {
         };
         const std::string batch_name =
             bm == VirtualFile::kAutoBatch ? "auto" : bm == 0 ? "one batch" : std::to_string(bm) + " MiB";
+        const DirectIoStats d1 = direct_io_stats();
+        char dio[384];
+        std::snprintf(dio, sizeof dio,
+                      "\"direct_io\": {\"requested\": %s, \"reads\": %llu, \"writes\": %llu, \"fallbacks\": %llu, "
+                      "\"refused_opens\": %llu, \"refused_errno\": %d, \"refused_fs\": \"%s\", \"io_errno\": %d}, ",
+                      direct ? "true" : "false", (unsigned long long)(d1.reads - d0.reads),
+                      (unsigned long long)(d1.writes - d0.writes), (unsigned long long)(d1.fallbacks - d0.fallbacks),
+                      (unsigned long long)(d1.refusals - d0.refusals), d1.refused_errno, d1.refused_fs.c_str(),
+                      d1.io_errno);
         std::printf(
             "{\"buffers\": \"%s\", \"codec_blocks_zero_copy\": %llu, \"codec_blocks_staged\": %llu, \"batch\": \"%s\", "
             "\"file_MiB\": %llu, \"block_MiB\": %llu, \"topology\": \"Erasure(1, 8, 3)\", "
@@ -212,7 +227,7 @@ int main(int argc, char** argv) {
             "\"read_reconstruct_GiBps\": %s, \"read_shard_io_GiBps\": %s, \"read_pipeline_GiBps\": %s, "
             "\"reconstructed_blocks\": %zu, \"sync_prepare_ms\": %.2f, \"read_prepare_ms\": %.2f, "
             "\"read_needed_shards\": %s, \"shard_reads_per_block\": %.2f, \"per_block_task_threads\": %s, "
-            "%s\"verified\": true}\n",
+            "%s%s\"verified\": true}\n",
             pinned ? "mapped Block Cache (shmr_ec_host_alloc)" : "pageable", (unsigned long long)(zc1 - zc0),
             (unsigned long long)(st1 - st0), batch_name.c_str(), (unsigned long long)file_mib,
             (unsigned long long)block_mib, int(do_fsync), reps, rate(best.write_s).c_str(), rate(best.sync_s).c_str(),
@@ -220,7 +235,7 @@ int main(int argc, char** argv) {
             rate(best.per_block_sync_s).c_str(), rate(best.read_s).c_str(), rate(best.load.codec_s).c_str(),
             rate(best.load.io_s).c_str(), rate(best.load.total_s).c_str(), best.load.blocks, best.sync.prepare_s * 1e3,
             best.load.prepare_s * 1e3, needed ? "true" : "false", best.shard_reads_per_block,
-            std::getenv("SHMR_VFS_TASKS") ? std::getenv("SHMR_VFS_TASKS") : "16", tasks_json(best).c_str());
+            std::getenv("SHMR_VFS_TASKS") ? std::getenv("SHMR_VFS_TASKS") : "16", tasks_json(best).c_str(), dio);
         std::fflush(stdout);
     }
     return 0;

@@ -596,6 +596,72 @@ void test_erasure_flush_encode_failure() {
     print_shards(*cfg, 0, b);
 }
 
+// VfsOptions::direct_io: shard files written and read with O_DIRECT into and
+// out of the Block-Cache slots (or, where the file system refuses O_DIRECT,
+// through the buffered path -- counted either way).  A file of Erasure(1, 8,
+// 3) 1 MiB blocks (S = 131,072: whole pages) through write -> sync -> lose
+// a shard per block -> read; then one Erasure(1, 10, 4) block, whose S =
+// 104,858 is not a whole page and must take the buffered path.
+void direct_io_roundtrip(bool pinned) {
+    auto cfg = test_config();
+    auto in = read_input();
+    const uint64_t bs = 1024 * 1024;
+    const size_t nblk = in.size() / bs;
+    CHECK(nblk * bs == in.size() && nblk > 1);
+    VfsOptions o;
+    o.missing_shard_is_erasure = true;
+    o.short_shard_is_erasure = true;
+    o.pread_from_start = true;
+    o.pinned_buffers = pinned;
+    o.direct_io = true;
+    VirtualFile vf = VirtualFile::new_with(pinned ? 21 : 22, 0);
+    vf.populate(cfg);
+    for (size_t i = 0; i < nblk; ++i) {
+        VirtualBlock b;
+        CHECK_OK(VirtualBlock::create(vf.ino, i + 1, cfg, bs, BlockTopology::erasure(1, 8, 3), &b));
+        vf.blocks.push_back(b);
+    }
+    vf.set_options(o);
+    const DirectIoStats d0 = direct_io_stats();
+    size_t n = 0;
+    CHECK_OK(vf.write(0, in.data(), in.size(), &n));
+    CHECK_OK(vf.sync_data(true));
+    for (size_t i = 0; i < nblk; ++i) print_shards(*cfg, i, vf.blocks[i]);
+    CHECK_OK(vf.drop_buffers());
+    CHECK_OK(vf.drop_handles());
+    for (size_t i = 0; i < nblk; ++i) fs::remove(shard_file(*cfg, vf.blocks[i], (i * 3) % 11));
+    std::vector<uint8_t> rb(in.size());
+    CHECK_OK(vf.read(0, rb.data(), rb.size(), &n));
+    CHECK(n == in.size() && rb == in);
+    const DirectIoStats d1 = direct_io_stats();
+    const uint64_t used = (d1.reads - d0.reads) + (d1.writes - d0.writes);
+    const uint64_t fell = d1.fallbacks - d0.fallbacks;
+    // shard writes and reads went direct, or fell back (a refusal names its file system)
+    CHECK(used + fell > 0);
+    if (d1.refusals > d0.refusals) CHECK(!d1.refused_fs.empty() && d1.refused_errno != 0);
+    std::printf("DIRECT reads=%llu writes=%llu fallbacks=%llu refusals=%llu fs=%s errno=%d io_errno=%d\n",
+                (unsigned long long)(d1.reads - d0.reads), (unsigned long long)(d1.writes - d0.writes),
+                (unsigned long long)fell, (unsigned long long)(d1.refusals - d0.refusals),
+                d1.refused_fs.empty() ? "-" : d1.refused_fs.c_str(), d1.refused_errno, d1.io_errno);
+    // a block whose shards are not whole pages: buffered, same bytes
+    VirtualBlock odd;
+    CHECK_OK(VirtualBlock::create(vf.ino + 100, 0, cfg, bs, BlockTopology::erasure(1, 10, 4), &odd));
+    odd.set_options(o);
+    CHECK_OK(odd.write(0, in.data(), bs, &n));
+    const DirectIoStats d2 = direct_io_stats();
+    CHECK_OK(odd.sync_data(true));
+    CHECK_OK(odd.drop_buffer());
+    CHECK_OK(odd.drop_handles());
+    fs::remove(shard_file(*cfg, odd, 4));
+    std::vector<uint8_t> ob(bs);
+    CHECK_OK(odd.read(0, ob.data(), ob.size(), &n));
+    CHECK(std::equal(ob.begin(), ob.end(), in.begin()));
+    const DirectIoStats d3 = direct_io_stats();
+    CHECK(d3.reads == d2.reads && d3.writes == d2.writes && d3.fallbacks > d2.fallbacks);
+}
+void test_direct_io_mapped() { direct_io_roundtrip(true); }
+void test_direct_io_pageable() { direct_io_roundtrip(false); }
+
 // VirtualFile with Erasure blocks: one batched GPU encode per flush.
 void test_virtual_file_erasure_batch() {
     auto cfg = test_config();
@@ -1226,6 +1292,8 @@ int main(int argc, char** argv) {
         {"erasure_block_sync_load", test_erasure_block_sync_load},
         {"erasure_block_missing_shards", test_erasure_block_missing_shards},
         {"erasure_flush_encode_failure", test_erasure_flush_encode_failure},
+        {"direct_io_mapped", test_direct_io_mapped},
+        {"direct_io_pageable", test_direct_io_pageable},
         {"virtual_file_erasure_batch", test_virtual_file_erasure_batch},
         {"replace_block_erasure", test_replace_block_erasure},
         {"virtual_file_batched_reconstruct", test_virtual_file_batched_reconstruct},

@@ -136,6 +136,38 @@ def test_erasure_flush_encode_failure(tmp_path, gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("buffers", ["mapped", "pageable"])
+def test_direct_io_shard_files(tmp_path, gpu, buffers):
+    """VfsOptions::direct_io (SURVEY 8(f) row 3): shard files written and read
+    with O_DIRECT, or -- where the file system refuses it -- through the
+    buffered path, counted (the case prints which); the shard files are the
+    oracle's either way, and the read rebuilds a lost shard per block."""
+    nblk, k, p = 4, 8, 3
+    data = np.concatenate([O.seeded_block(O.BENCH_SEED, 700 + i, MiB) for i in range(nblk)])
+    args = [BIN, "direct_io_" + buffers, str(tmp_path)]
+    path = os.path.join(str(tmp_path), "input.bin")
+    with open(path, "wb") as f:
+        f.write(data.tobytes())
+    out = subprocess.run(args + [path], capture_output=True, text=True, timeout=300)
+    lines = out.stdout.strip().splitlines()
+    assert out.returncode == 0 and lines and lines[-1] == "PASS", out.stdout + out.stderr
+    direct = [l for l in lines if l.startswith("DIRECT ")]
+    assert len(direct) == 1
+    print(direct[0])
+    shards = {}
+    for line in lines:
+        if line.startswith("SHARDS "):
+            parts = line.split()
+            shards[int(parts[1])] = parts[2:]
+    for b in range(nblk):
+        want = O.sync_data_erasure(data[b * MiB:(b + 1) * MiB].tobytes(), MiB, k, p)
+        for i, fpath in enumerate(shards[b]):
+            if i == (b * 3) % 11:
+                continue                  # removed by the case (rebuilt into the read, rewritten by the flush)
+            assert np.array_equal(read(fpath), want[i]), f"block {b} shard {i}"
+
+
+@pytest.mark.gpu
 def test_virtual_file_erasure_batch(tmp_path, gpu):
     nblk, k, p = 6, 8, 3
     data = np.concatenate([O.seeded_block(O.BENCH_SEED, 200 + i, MiB) for i in range(nblk)])
