@@ -159,7 +159,18 @@ int shmr_ec_op_wait(shmr_ec_op_t* op);
  * capture that would need the initialisation returns INVALID_ARGUMENT with
  * nothing enqueued, and so does one whose stream state cannot be read (the
  * legacy null stream while another thread captures in global mode).
- * SHMR_EC_DEV_BLOCKING_CALLS counts the exceptions. */
+ * SHMR_EC_DEV_BLOCKING_CALLS counts the exceptions.
+ *
+ * Cross-stream coupling: the readiness of an upload (a plan image, an upload-
+ * ring slot, a table-cache entry) that a call enqueued on a caller stream is
+ * tracked by an event mirrored onto the device's one private stream, which
+ * waits for the caller stream's events in the order they were recorded.  A
+ * later call on ANOTHER stream that needs such an upload (or a busy ring
+ * slot) may therefore wait for work queued earlier on unrelated caller
+ * streams.  A stream held back by something outside the library (a host
+ * function, a stream wait on a value, a collective) can delay, and with a
+ * full ring block, another thread's call until it progresses.  Streams that
+ * only reuse plans and tables already uploaded are not affected. */
 
 /* One-time per-device initialisation (probe of the memory system's unaligned
  * access mode on a private stream, the plan arena and a 4 MiB capture reserve
