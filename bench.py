@@ -110,6 +110,9 @@ def parse():
                          "--dump-blocks blocks (encode configs) with their global block ids to "
                          "DIR/rank<r>.npz, for a test-side check against the CPU oracle")
     ap.add_argument("--dump-blocks", type=int, default=2)
+    ap.add_argument("--no-host-probe", action="store_true",
+                    help="skip the untimed host-path probe after the timed region (mapped Block-Cache blocks coded "
+                         "zero-copy on this rank's GPU; rank 0 also over every visible GPU from one process)")
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher rehearsal without a GPU: ranks join the process group, exchange their "
                          "identities and rank 0 prints one JSON line (tests/test_bench_launch.py)")
@@ -690,6 +693,16 @@ def run(args):
         out["roofline"]["round_trip_bit_exact"] = w.round_trip()
     if args.dump_dir and shape.erasures is None:
         dump_blocks(args, shape, w, rank, world)
+    # per-rank figures (the line's roofline is the slowest rank's) and the host-path probe
+    mine = {"rank": rank, "device": dev.index, "ms_per_step": round(float(np.mean(step_ms)), 4),
+            "frac": round(shape.algo_bytes_per_block * shape.B / (float(np.mean(step_ms)) / 1e3) / HBM_PEAK, 4)}
+    if not args.no_host_probe:
+        mine["host_probe"] = host_probe(dev.index, all_devices=rank == 0)
+    per_rank = [mine]
+    if world > 1:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
+    out["per_rank"] = per_rank
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_leg(args, shape, w)
     if rank == 0:
@@ -735,6 +748,41 @@ def run_single(args):
     if n == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_leg(args, shape, works[0])
     print(json.dumps(out), flush=True)
+
+
+def host_probe(local: int, all_devices: bool):
+    """Untimed, after the timed region: the host path (BASELINE config 5's
+    start and end in host memory) on this rank's GPU -- two RS(8,3) blocks in
+    mapped Block-Cache memory coded zero-copy (shmr_ec_encode_blocks_host),
+    their parity compared with a device-resident encode of the same bytes on
+    the same GPU.  Rank 0 also codes 2 blocks per visible GPU from this one
+    process, round-robin over all of them: on a multi-GPU node that is the
+    check that mapped host memory is addressed the same way from every device
+    (host_engine.cpp's zero-copy precondition)."""
+    k, p, S = 8, 3, 65536
+    ndev = torch.cuda.device_count()
+    devices = list(range(ndev)) if all_devices else [local]
+    nb = 2 * len(devices)
+    rs = shmr_amd.ReedSolomon(k, p)
+    buf = shmr_amd.PinnedBuffer(nb * (k + p) * S)
+    arr = buf.array.reshape(nb, k + p, S)
+    g = np.random.default_rng([SEED, local, nb])
+    arr[:, :k] = g.integers(0, 256, (nb, k, S), dtype=np.uint8)
+    arr[:, k:] = 0
+    z0, s0 = shmr_amd.path_stats()
+    before = {d: shmr_amd.device_stats(d)["blocks_encoded"] for d in devices}
+    rs.encode_blocks_host(arr, devices=devices)
+    z1, s1 = shmr_amd.path_stats()
+    per_dev = {d: shmr_amd.device_stats(d)["blocks_encoded"] - before[d] for d in devices}
+    with torch.cuda.device(local):
+        data = torch.from_numpy(np.ascontiguousarray(arr[:, :k])).to(f"cuda:{local}")
+        par = torch.zeros((nb, p, S), dtype=torch.uint8, device=f"cuda:{local}")
+        rs.encode_batch_dev(data, par)
+        torch.cuda.synchronize(local)
+        same = bool(np.array_equal(par.cpu().numpy(), arr[:, k:]))
+    del buf
+    return {"devices": devices, "blocks": nb, "zero_copy_blocks": z1 - z0, "staged_blocks": s1 - s0,
+            "blocks_per_device": [per_dev[d] for d in devices], "parity_equals_device_resident": same}
 
 
 def dump_blocks(args, shape, w, rank, world):

@@ -50,6 +50,11 @@ def test_bench_line_contract(gpu, config, blocks, extra):
     if "--layout" in extra:               # slab buffers: every timed call ran as a slot grid
         slab = "torch" not in extra
         assert d["config"]["ptr_table_grid_calls_timed"] == (3 if slab else 0)
+    pr = d["per_rank"]
+    assert len(pr) == 1 and pr[0]["rank"] == 0 and 0 < pr[0]["frac"] < 1
+    hp = pr[0]["host_probe"]
+    assert hp["parity_equals_device_resident"] is True and hp["zero_copy_blocks"] == hp["blocks"] > 0
+    assert sum(hp["blocks_per_device"]) == hp["blocks"]
     c = d["cpu_baseline"]
     assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0 and c["sample"]
     if config == "encode83":

@@ -89,6 +89,10 @@ def test_bench_self_launch_eight_ranks(gpu, tmp_path):
     assert [d["rank"] for d in b["devices"]] == list(range(8))
     assert b["distinct_gpus"] == 1                 # one physical GPU shared by the eight ranks
     assert b["config"]["global_batch_blocks"] == 32 and b["scaling"] == "weak" and b["value"] > 0
+    assert [r["rank"] for r in b["per_rank"]] == list(range(8))
+    for r in b["per_rank"]:      # every rank's host-path probe: zero-copy, same parity as device-resident
+        hp = r["host_probe"]
+        assert hp["parity_equals_device_resident"] is True and hp["zero_copy_blocks"] == hp["blocks"], r
     seen = []
     for r in range(8):
         z = np.load(os.path.join(str(tmp_path), f"rank{r}.npz"))
