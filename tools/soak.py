@@ -95,7 +95,7 @@ class _Nothing:
         return False
 
 
-def worker(tid, deadline, errors, counts, ops=tuple(range(7)), shapes=tuple(range(len(SHAPES)))):
+def worker(tid, deadline, errors, counts, ops=tuple(range(8)), shapes=tuple(range(len(SHAPES)))):
     rng = np.random.default_rng([tid, 2024])
     stream = torch.cuda.Stream()
     slab = shmr_amd.PinnedBuffer(4 * 24 * 524288)
@@ -104,7 +104,7 @@ def worker(tid, deadline, errors, counts, ops=tuple(range(7)), shapes=tuple(rang
         k, p, L = SHAPES[shapes[int(rng.integers(0, len(shapes)))]]
         rs = shmr_amd.ReedSolomon(k, p)
         op = ops[int(rng.integers(0, len(ops)))]
-        gate = GATE.exclusive() if op == 6 else GATE.shared() if op in (3, 4) else _Nothing()
+        gate = GATE.exclusive() if op == 6 else GATE.shared() if op in (3, 4, 7) else _Nothing()
         try:
             with gate:
                 if op == 0:        # per-block calls, pageable or mapped
@@ -232,6 +232,55 @@ def worker(tid, deadline, errors, counts, ops=tuple(range(7)), shapes=tuple(rang
                         if not all(np.array_equal(partial[b][i].cpu().numpy(), want[i]) for i in lost[b]):
                             errors.append((tid, "ptrs reconstruct", k, p, L, B))
                             break
+                elif op == 7:      # slab buffers (shmr_ec_device_alloc_shards): grid pointer tables, strided kernels
+                    import ctypes
+                    from shmr_amd.reed_solomon import _u8p
+                    key = ("slab", k, p, L)
+                    if key not in kept:
+                        B = int(rng.integers(1, 6))
+                        kept[key] = (shmr_amd.ShardSlab(B, k, L), shmr_amd.ShardSlab(B, p, L),
+                                     shmr_amd.ShardSlab(B, k + p, L), shmr_amd.ShardSlab(B, p, L))
+                    ds, ps, js, outs = kept[key]
+                    B = ds.nblocks
+                    host = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+                    sp = ctypes.c_void_p(stream.cuda_stream)
+                    tab = np.ascontiguousarray(np.concatenate([ds.ptrs.reshape(B, k), ps.ptrs.reshape(B, p)], axis=1))
+                    present = np.ones((B, k + p), np.uint8)
+                    for b in range(B):
+                        present[b, rng.choice(k + p, size=int(rng.integers(1, p + 1)), replace=False)] = 0
+                    fresh = js.ptrs.reshape(B, k + p).copy()   # rebuilt shard j of block b -> outs slot (b, j)
+                    for b in range(B):
+                        for j, i in enumerate(np.flatnonzero(present[b] == 0)):
+                            fresh[b, i] = outs.ptrs[b * p + j]
+                    fresh = np.ascontiguousarray(fresh)
+                    with torch.cuda.stream(stream):
+                        ds.tensor()[:, :, :L] = torch.from_numpy(host).cuda()
+                        assert rs._L.shmr_ec_encode_ptrs_dev(rs._h, tab.ctypes.data_as(ctypes.POINTER(_u8p)), B, L, 0,
+                                                             sp) == 0
+                        jv = js.tensor()
+                        jv[:, :k, :L] = ds.tensor()[:, :, :L]
+                        jv[:, k:, :L] = ps.tensor()[:, :, :L]
+                        full = jv[:, :, :L].clone()
+                        jv[:, :, :L][torch.from_numpy(present == 0).cuda()] = 0xEE
+                        assert rs._L.shmr_ec_reconstruct_ptrs_dev(rs._h, fresh.ctypes.data_as(ctypes.POINTER(_u8p)),
+                                                                  present.ctypes.data_as(_u8p), B, L, 0, 0, sp) == 0
+                        rebuilt = outs.tensor()[:, :, :L].clone()
+                        assert rs._L.shmr_ec_reconstruct_ptrs_dev(
+                            rs._h, js.ptrs.ctypes.data_as(ctypes.POINTER(_u8p)), present.ctypes.data_as(_u8p), B, L,
+                            0, 0, sp) == 0
+                    stream.synchronize()
+                    h, hr = full.cpu().numpy(), rebuilt.cpu().numpy()
+                    if not np.array_equal(js.tensor()[:, :, :L].cpu().numpy(), h):
+                        errors.append((tid, "slab rebuild in place", k, p, L, B))
+                    for b in range(B):
+                        want = oracle_encode(k, p, list(host[b]))
+                        if not all(np.array_equal(h[b, i], want[i]) for i in range(k, k + p)):
+                            errors.append((tid, "slab encode", k, p, L, B))
+                            break
+                        if not all(np.array_equal(hr[b, j], h[b, i])
+                                   for j, i in enumerate(np.flatnonzero(present[b] == 0))):
+                            errors.append((tid, "slab rebuild fresh", k, p, L, B))
+                            break
                 else:              # device-resident batch on this thread's stream: encode, in-place and compact rebuild
                     B = int(rng.integers(1, 9))
                     P = (L + 255) // 256 * 256
@@ -277,7 +326,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=120)
     ap.add_argument("--threads", type=int, default=12)
-    ap.add_argument("--ops", default="0,1,2,3,4,5,6", help="subset of the operations (comma list)")
+    ap.add_argument("--ops", default="0,1,2,3,4,5,6,7", help="subset of the operations (comma list)")
     ap.add_argument("--shapes", default=",".join(str(i) for i in range(len(SHAPES))),
                     help="subset of SHAPES (indices)")
     a = ap.parse_args()
@@ -299,7 +348,8 @@ def main():
                       "zero_copy_blocks": zc, "staged_blocks": st,
                       "ptr_table_hits": shmr_amd.device_stats(0)["ptr_table_hits"],
                       "capture_tables": shmr_amd.device_stats(0)["capture_tables"],
-                      "capture_released": shmr_amd.device_stats(0)["capture_released"]}), flush=True)
+                      "capture_released": shmr_amd.device_stats(0)["capture_released"],
+                      "ptr_table_grids": shmr_amd.device_stats(0)["ptr_table_grids"]}), flush=True)
     sys.exit(1 if errors else 0)
 
 
