@@ -76,10 +76,12 @@ bool fit_grid(const std::vector<GridEntry>& e, Grid* g) {
         bp = da / db;
         break;
     }
-    const int64_t base = e[0].addr - int64_t(e[0].b) * bp - int64_t(e[0].j) * sp;
+    // checked in the kernels' own arithmetic: 64-bit unsigned, wrapping
+    const uint64_t ubp = uint64_t(bp), usp = uint64_t(sp);
+    const uint64_t base = uint64_t(e[0].addr) - e[0].b * ubp - e[0].j * usp;
     for (const GridEntry& x : e)
-        if (x.addr != base + int64_t(x.b) * bp + int64_t(x.j) * sp) return false;
-    g->base = base;
+        if (uint64_t(x.addr) != base + x.b * ubp + x.j * usp) return false;
+    g->base = int64_t(base);
     g->bpitch = bp;
     g->spitch = sp;
     return true;
