@@ -588,8 +588,10 @@ struct VirtualBlock::State {
     // VfsOptions::direct_io: shard i's O_DIRECT descriptor, opened on first
     // use (creating the file like ensure_fd); -1 when the file system refuses
     // it (then never retried for this handle).  Caller holds handles_mu.
+    // (dfds is sized with the handles by open_handles, before the parallel
+    // shard I/O that calls this for distinct i.)
     int direct_fd(size_t i, const ShmrFsConfig& cfg) {
-        if (dfds.size() < handles.size()) dfds.resize(handles.size(), -1);
+        if (i >= dfds.size()) return -1;
         if (dfds[i] >= 0 || dfds[i] == -2) return dfds[i] >= 0 ? dfds[i] : -1;
         fs::path file;
         if (handles[i].first.resolve(cfg, &file, nullptr)) return -1;
@@ -609,8 +611,8 @@ struct VirtualBlock::State {
     // slot qualifies).
     Status write_shard(size_t i, const ShmrFsConfig& cfg, const VfsOptions& o, const uint8_t* buf, size_t len) {
         if (auto e = ensure_fd(i, cfg)) return e;
-        if (o.direct_io && direct_eligible(buf, len)) {
-            const int dfd = direct_fd(i, cfg);
+        if (o.direct_io) {
+            const int dfd = direct_eligible(buf, len) ? direct_fd(i, cfg) : -1;
             if (dfd >= 0) {
                 const int err = write_direct(dfd, buf, len, o.fsync_shards);
                 if (err == 0) return std::nullopt;
@@ -624,9 +626,8 @@ struct VirtualBlock::State {
     // intact file into a qualifying slot, read from offset 0).
     int read_shard(size_t i, int fd, const ShmrFsConfig& cfg, const VfsOptions& o, uint8_t* slot, size_t S,
                    bool* odd) {
-        if (o.direct_io && o.pread_from_start && direct_eligible(slot, S) && i < handles.size() &&
-            handles[i].second >= 0) {
-            const int dfd = direct_fd(i, cfg);
+        if (o.direct_io && o.pread_from_start && i < handles.size() && handles[i].second >= 0) {
+            const int dfd = direct_eligible(slot, S) ? direct_fd(i, cfg) : -1;
             if (dfd >= 0) {
                 const int rc = read_slot_direct(dfd, slot, S, odd);
                 if (rc == 0) return 0;
@@ -872,6 +873,7 @@ Status VirtualBlock::open_handles() const {
         }
         st_->handles.emplace_back(shard, fd);
     }
+    st_->dfds.assign(st_->handles.size(), -1);
     st_->shard_loaded.store(true);
     return std::nullopt;
 }

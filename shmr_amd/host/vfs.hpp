@@ -148,9 +148,10 @@ struct VfsOptions {
 };
 
 // What VfsOptions::direct_io did since the library was loaded: shard files
-// read / written with O_DIRECT, shard I/O that fell back to the buffered path
-// (refused, failed, or a file that is not exactly S bytes), refused opens, the
-// first refusal's errno and file system, and the first O_DIRECT I/O error.
+// read / written with O_DIRECT, shard I/O under direct_io that went buffered
+// (a slot that is not whole pages, a refused open, a failed O_DIRECT call, or
+// a file that is not exactly S bytes), refused opens, the first refusal's
+// errno and file system, and the first O_DIRECT I/O error.
 struct DirectIoStats {
     uint64_t reads = 0, writes = 0, fallbacks = 0, refusals = 0;
     int refused_errno = 0;
