@@ -351,3 +351,110 @@ def test_random_started_calls(gpu, case):
         assert rs._L.shmr_ec_op_wait(op) == 0
         for i in range(len(sh)):
             assert np.array_equal(sh[i], want[i]), (shape, i)
+
+
+@pytest.mark.parametrize("case", range(24 * SCALE))
+def test_random_grid_tables(gpu, case):
+    """Pointer tables that name a slot grid (knob ptrs_grid, r05): random grid
+    geometry -- data and parity in one joint grid or two, pitches aligned or
+    not, strides with gaps -- encoded, then rebuilt either in place (every
+    shard on one grid) or into a second grid of fresh buffers (rebuilt shard j
+    of block b), data_only random.  Every call must be recognised as a grid
+    (counter ptr_table_grids), write exactly the oracle's bytes and nothing
+    outside the shards."""
+    import torch
+    rng = np.random.default_rng([0x6D1D, case])
+    k, p, L, B, spitch, off = _shape(rng)
+    t = k + p
+    aligned = spitch % 16 == 0 and off % 16 == 0
+    joint = bool(rng.integers(0, 2))
+    gap = int(rng.integers(0, 3)) * (16 if aligned else 7)
+    if joint:                                          # [B][t] slots in one grid
+        bp = t * spitch + gap
+        addr = np.array([[off + b * bp + i * spitch for i in range(t)] for b in range(B)], np.int64)
+        size = off + B * bp + 64
+    else:                                              # data grid, then a parity grid after it
+        bpd, bpp = k * spitch + gap, p * spitch + gap
+        pbase = off + B * bpd + 32 * int(rng.integers(0, 3))
+        addr = np.array([[off + b * bpd + i * spitch for i in range(k)] +
+                         [pbase + b * bpp + r * spitch for r in range(p)] for b in range(B)], np.int64)
+        size = pbase + B * bpp + 64
+    host = np.full(size, SENTINEL, np.uint8)
+    full = []
+    for b in range(B):
+        sh = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)] + [np.zeros(L, np.uint8) for _ in range(p)]
+        c_oracle.encode(k, p, sh)
+        full.append(sh)
+        for i in range(k):
+            host[addr[b, i]:addr[b, i] + L] = sh[i]
+    d = torch.from_numpy(host).to(gpu)
+    base = d.data_ptr()
+    tab = np.ascontiguousarray((addr + base).astype(np.uint64).reshape(-1))
+    rs = shmr_amd.ReedSolomon(k, p)
+    g0 = shmr_amd.device_stats(0)["ptr_table_grids"]
+    rc = lib().shmr_ec_encode_ptrs_dev(rs._h, tab.ctypes.data_as(ctypes.POINTER(_u8p)), B, L, 0, _stream())
+    assert rc == 0, shmr_amd.Error(rc).name
+    torch.cuda.synchronize()
+    assert shmr_amd.device_stats(0)["ptr_table_grids"] == g0 + 1, ("encode not taken as a grid", joint, gap)
+    expect = host.copy()
+    for b in range(B):
+        for i in range(k, t):
+            expect[addr[b, i]:addr[b, i] + L] = full[b][i]
+    assert np.array_equal(d.cpu().numpy(), expect), ("grid encode", k, p, L, B, joint, gap, aligned)
+    # rebuild
+    data_only = bool(rng.integers(0, 2))
+    present = np.ones((B, t), np.uint8)
+    for b in range(B):
+        if rng.integers(0, 4):
+            present[b, rng.choice(t, size=int(rng.integers(1, p + 1)), replace=False)] = 0
+    written = (present == 0)
+    if data_only:
+        written[:, k:] = False
+    fresh = bool(rng.integers(0, 2)) and written.any()
+    work = expect.copy()
+    for b in range(B):
+        for i in range(t):
+            if not present[b, i]:
+                work[addr[b, i]:addr[b, i] + L] = 0x3C   # poison the absent shards' slots
+    d = torch.from_numpy(work).to(gpu)
+    tab2 = (addr + d.data_ptr()).astype(np.uint64)
+    if fresh:                                          # rebuilt shard j of block b in an output grid
+        nout = int(written.sum(axis=1).max())
+        ospitch = spitch + (16 if aligned else 3) * int(rng.integers(0, 2))
+        obp = nout * ospitch + gap
+        out = torch.full((B * obp + 64,), 0xEE, dtype=torch.uint8, device=gpu)
+        for b in range(B):
+            j = 0
+            for i in range(t):
+                if written[b, i]:
+                    tab2[b, i] = out.data_ptr() + b * obp + j * ospitch
+                    j += 1
+                elif not present[b, i]:
+                    tab2[b, i] = 0                     # absent parity under data_only: NULL
+    tab2 = np.ascontiguousarray(tab2.reshape(-1))
+    g1 = shmr_amd.device_stats(0)["ptr_table_grids"]
+    rc = lib().shmr_ec_reconstruct_ptrs_dev(rs._h, tab2.ctypes.data_as(ctypes.POINTER(_u8p)),
+                                            present.ctypes.data_as(_u8p), B, L, int(data_only), 0, _stream())
+    assert rc == 0, shmr_amd.Error(rc).name
+    torch.cuda.synchronize()
+    if joint:   # (two grids: the present shards span both, so the table kernels may run -- bytes equal)
+        assert shmr_amd.device_stats(0)["ptr_table_grids"] == g1 + 1, ("rebuild not taken as a grid", fresh)
+    got = d.cpu().numpy()
+    want = work.copy()
+    if not fresh:
+        for b in range(B):
+            for i in range(t):
+                if written[b, i]:
+                    want[addr[b, i]:addr[b, i] + L] = full[b][i]
+        assert np.array_equal(got, want), ("grid rebuild in place", k, p, L, B, joint, data_only)
+    else:
+        assert np.array_equal(got, want), ("grid rebuild touched the shard buffer", k, p, L, B)
+        o = out.cpu().numpy()
+        ow = np.full(B * obp + 64, 0xEE, np.uint8)
+        for b in range(B):
+            j = 0
+            for i in range(t):
+                if written[b, i]:
+                    ow[b * obp + j * ospitch:b * obp + j * ospitch + L] = full[b][i]
+                    j += 1
+        assert np.array_equal(o, ow), ("grid rebuild into fresh buffers", k, p, L, B, data_only)
