@@ -4,7 +4,12 @@
 // every shard.  Used to compare library builds (e.g. the host-sanitized one of
 // tools/asan_host.sh) without the StorageBlock layer on top.
 //
-//   g++ -O1 -g -std=c++17 -Iinclude tools/abi_check.cpp -Lshmr_amd/_lib -lshmr_ec -o tools/_bin/abi_check
+// Then the same blocks in device memory from shmr_ec_device_alloc_shards
+// through pointer tables on a slot grid (encode; rebuild into a second slab).
+//
+//   hipcc -O1 -g -std=c++17 -Iinclude tools/abi_check.cpp -Lshmr_amd/_lib -lshmr_ec -o tools/_bin/abi_check
+#include <hip/hip_runtime.h>
+
 #include <cstdio>
 #include <cstring>
 #include <random>
@@ -107,6 +112,42 @@ int main(int argc, char** argv) {
             std::printf("MISMATCH block %zu shard %zu (present %d)\n", q / t, q % t, int(present[q]));
             ++bad;
         }
+    {   // device-resident slab buffers, pointer tables on a slot grid
+        std::vector<uint8_t*> dp(B * t), outs(B * 2);
+        rc = shmr_ec_device_alloc_shards(0, B, t, S, dp.data());
+        if (!rc) rc = shmr_ec_device_alloc_shards(0, B, 2, S, outs.data());
+        if (rc) {
+            std::printf("device_alloc_shards: %s\n", shmr_ec_status_name(rc));
+            return 1;
+        }
+        for (size_t q = 0; q < B * t; ++q)
+            if (hipMemcpy(dp[q], want[q].data(), (q % t) < k ? S : 0, hipMemcpyHostToDevice) != hipSuccess) return 1;
+        uint64_t g0[SHMR_EC_DEV_COUNTERS] = {}, g1[SHMR_EC_DEV_COUNTERS] = {};
+        shmr_ec_device_stats(0, g0, SHMR_EC_DEV_COUNTERS);
+        rc = shmr_ec_encode_ptrs_dev(rs, dp.data(), B, S, 0, nullptr);
+        std::vector<uint8_t*> tab(dp);
+        for (size_t b = 0; b < B; ++b) {   // absent shards -> the b-th row of the output slab
+            unsigned j = 0;
+            for (unsigned i = 0; i < t; ++i)
+                if (!present[b * t + i]) tab[b * t + i] = outs[b * 2 + j++];
+        }
+        if (!rc) rc = shmr_ec_reconstruct_ptrs_dev(rs, tab.data(), present.data(), B, S, 0, 0, nullptr);
+        if (hipDeviceSynchronize() != hipSuccess) return 1;
+        shmr_ec_device_stats(0, g1, SHMR_EC_DEV_COUNTERS);
+        std::printf("slab grid calls: %s, grid calls %llu\n", shmr_ec_status_name(rc),
+                    (unsigned long long)(g1[SHMR_EC_DEV_PTR_TABLE_GRIDS] - g0[SHMR_EC_DEV_PTR_TABLE_GRIDS]));
+        if (rc || g1[SHMR_EC_DEV_PTR_TABLE_GRIDS] - g0[SHMR_EC_DEV_PTR_TABLE_GRIDS] != 2) ++bad;
+        std::vector<uint8_t> h(S);
+        for (size_t q = 0; q < B * t; ++q) {
+            if (hipMemcpy(h.data(), tab[q], S, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+            if (std::memcmp(h.data(), want[q].data(), S) != 0) {
+                std::printf("SLAB MISMATCH block %zu shard %zu (present %d)\n", q / t, q % t, int(present[q]));
+                ++bad;
+            }
+        }
+        if (shmr_ec_device_free_shards(0, dp[1]) != SHMR_EC_INVALID_ARGUMENT) ++bad;   // not a slab base
+        if (shmr_ec_device_free_shards(0, dp[0]) || shmr_ec_device_free_shards(0, outs[0])) ++bad;
+    }
     for (auto* q : bufs) shmr_ec_host_free(q);
     shmr_ec_free(rs);
     std::printf(bad ? "FAIL\n" : "PASS\n");

@@ -16,7 +16,8 @@ virtual_file_chunk_model erasure_f32_hazard virtual_file_record_roundtrip virtua
 GPU_CASES="erasure_block_sync_load:700001 erasure_block_missing_shards:1048576 virtual_file_erasure_batch:6291456
 replace_block_erasure:300000 virtual_file_batched_reconstruct:12582912 rewrite_erasure:2109497
 virtual_file_mapped_per_block_flush:10485760 erasure_f32_hazard_release:16777217
-rewrite_erasure_record_reload:2109497 read_needed_shards:4194304 virtual_block_erasure_fuzz virtual_file_erasure_fuzz"
+rewrite_erasure_record_reload:2109497 read_needed_shards:4194304 virtual_block_erasure_fuzz virtual_file_erasure_fuzz
+erasure_flush_encode_failure:2097152 direct_io_mapped:4194304 direct_io_pageable:4194304"
 case "${1:-}" in
 build)
     # libshmr_ec.so's host code (C ABI, launch core, host engine) instrumented
