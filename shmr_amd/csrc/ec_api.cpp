@@ -19,6 +19,7 @@
 
 #include "ec_core.hpp"
 #include "host_engine.hpp"
+#include "ptr_grid.hpp"
 
 using shmr::core::Codec;
 using shmr::core::Plan;
@@ -48,44 +49,9 @@ int guarded(F&& f) noexcept {
 // (the table kernels' first loads wait on a scalar load of the block's table
 // row).  The fit is checked against every entry, so the
 // kernels touch the same bytes either way.
-struct GridEntry {
-    uint64_t b, j;
-    int64_t addr;
-};
-struct Grid {
-    int64_t base = 0, bpitch = 0, spitch = 0;
-};
-// Entries in ascending b, then ascending j within a block.  Pitches no entry
-// pair determines are 0 (the kernels never multiply them by a nonzero index).
-bool fit_grid(const std::vector<GridEntry>& e, Grid* g) {
-    *g = Grid{};
-    if (e.empty()) return true;
-    int64_t sp = 0, bp = 0;
-    for (size_t i = 1; i < e.size(); ++i) {
-        if (e[i].b != e[i - 1].b) continue;
-        const int64_t dj = int64_t(e[i].j - e[i - 1].j), da = e[i].addr - e[i - 1].addr;
-        if (dj <= 0 || da <= 0 || da % dj) return false;
-        sp = da / dj;
-        break;
-    }
-    for (size_t i = 1; i < e.size(); ++i) {
-        if (e[i].b == e[0].b) continue;
-        const int64_t db = int64_t(e[i].b - e[0].b);
-        const int64_t da = e[i].addr - e[0].addr - (int64_t(e[i].j) - int64_t(e[0].j)) * sp;
-        if (db <= 0 || da <= 0 || da % db) return false;
-        bp = da / db;
-        break;
-    }
-    // checked in the kernels' own arithmetic: 64-bit unsigned, wrapping
-    const uint64_t ubp = uint64_t(bp), usp = uint64_t(sp);
-    const uint64_t base = uint64_t(e[0].addr) - e[0].b * ubp - e[0].j * usp;
-    for (const GridEntry& x : e)
-        if (uint64_t(x.addr) != base + x.b * ubp + x.j * usp) return false;
-    g->base = int64_t(base);
-    g->bpitch = bp;
-    g->spitch = sp;
-    return true;
-}
+using GridEntry = shmr::grid::Entry;
+using shmr::grid::Grid;
+using shmr::grid::fit_grid;
 uint8_t* grid_ptr(const Grid& g) { return reinterpret_cast<uint8_t*>(uintptr_t(g.base)); }
 
 // The strided equivalent of a pointer-table call, if its table is a grid:
@@ -94,7 +60,7 @@ int ptrs_as_grid(Codec& c, uint8_t* const* tab, const uint8_t* present, size_t n
                  int device, hipStream_t stream, core::OpClass op, bool* handled) {
     *handled = false;
     const unsigned k = c.k(), t = k + c.p();
-    auto addr = [&](size_t b, unsigned i) { return int64_t(uintptr_t(tab[b * t + i])); };
+    auto addr = [&](size_t b, unsigned i) { return uint64_t(uintptr_t(tab[b * t + i])); };
     std::vector<GridEntry> in, out;
     in.reserve(nblocks * k);
     out.reserve(nblocks * (t - k));

@@ -1,0 +1,121 @@
+"""Host logic of the pointer-table slot grids (shmr_amd/csrc/ptr_grid.hpp), on
+the CPU: tools/ptr_grid_check.cpp is compiled with g++ and fed tables.
+
+A *_ptrs_dev table is run through the strided kernels only when fit_grid finds
+(base, block pitch, shard pitch) that reproduce every entry in the kernels'
+unsigned 64-bit arithmetic.  Soundness -- a returned grid
+reproduces every entry, pitches non-negative -- is what keeps the bytes
+identical to the table kernels'; completeness -- every slab-shaped table,
+including sparse ones where no block holds two entries (a rebuild of one lost
+shard per block), is recognised -- is what keeps the speed.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def checker(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("grid") / "ptr_grid_check")
+    subprocess.run(["g++", "-O1", "-std=c++17", "-I", os.path.join(ROOT, "shmr_amd", "csrc"),
+                    os.path.join(ROOT, "tools", "ptr_grid_check.cpp"), "-o", exe], check=True)
+
+    def run(cases):
+        inp = "".join(f"{len(c)}\n" + "".join(f"{b} {j} {a}\n" for b, j, a in c) for c in cases)
+        out = subprocess.run([exe], input=inp, capture_output=True, text=True, check=True).stdout.split("\n")
+        res = []
+        for line in out[:len(cases)]:
+            f = line.split()
+            res.append(None if f[0] == "0" else tuple(int(x) for x in f[1:]))
+        return res
+    return run
+
+
+M64 = (1 << 64) - 1
+
+
+def _reproduces(case, g):
+    base, bp, sp = g
+    return all(a == (base + b * bp + j * sp) & M64 for b, j, a in case) and bp >= 0 and sp >= 0
+
+
+def _grid_case(rng, sparse):
+    B = int(rng.integers(1, 9))
+    n = int(rng.integers(1, 12))
+    sp = int(rng.choice([16, 4096, 528384, int(rng.integers(1, 1 << 21))]))
+    bp = n * sp + int(rng.integers(0, 3)) * int(rng.choice([1, 7, 4096]))
+    if rng.integers(0, 3) == 0:
+        bp = int(rng.integers(0, 4)) * sp          # degenerate strides (collinear / overlapping blocks)
+    base = int(rng.integers(1 << 40, 1 << 47))
+    case = []
+    for b in range(B):
+        js = range(n)
+        if sparse:
+            js = sorted(rng.choice(n, size=int(rng.integers(0, min(n, 2) + 1)), replace=False).tolist())
+        for j in js:
+            case.append((b, j, base + b * bp + j * sp))
+    return case
+
+
+def test_slab_shaped_tables_fit(checker):
+    rng = np.random.default_rng(31)
+    cases = [_grid_case(rng, sparse=bool(i % 2)) for i in range(4000)]
+    cases = [c for c in cases if c]
+    res = checker(cases)
+    for c, g in zip(cases, res):
+        assert g is not None, c[:6]
+        assert _reproduces(c, g)
+
+
+def test_one_entry_per_block_with_varying_shard(checker):
+    """The case a dense-pair-only fit missed (r05 sweep case 217): RS(1,1)
+    blocks rebuilding one lost shard each -- no block holds two entries, the
+    shard index differs between blocks."""
+    sp, bp, base = 4111, 8236, 5
+    case = [(0, 0, base), (1, 0, base + bp), (2, 1, base + 2 * bp + sp)]
+    g = checker([case])[0]
+    assert g == (base, bp, sp)
+
+
+def test_tables_off_a_grid_are_refused_or_reproduced(checker):
+    """Soundness: perturbed and shuffled tables either find no grid or a grid
+    that reproduces every entry (then the strided kernels touch exactly the
+    table's addresses)."""
+    rng = np.random.default_rng(32)
+    cases = []
+    for _ in range(3000):
+        c = _grid_case(rng, sparse=False)
+        if len(c) < 2:
+            continue
+        c = list(c)
+        kind = int(rng.integers(0, 3))
+        i = int(rng.integers(0, len(c)))
+        if kind == 0:                                   # one address off by a few bytes
+            b, j, a = c[i]
+            c[i] = (b, j, a + int(rng.integers(1, 64)))
+        elif kind == 1:                                 # two entries' addresses swapped
+            i2 = int(rng.integers(0, len(c)))
+            (b1, j1, a1), (b2, j2, a2) = c[i], c[i2]
+            c[i], c[i2] = (b1, j1, a2), (b2, j2, a1)
+        else:                                           # descending pitch (not a slab)
+            c = [(b, j, (1 << 47) - a % (1 << 46)) for b, j, a in c]
+        cases.append(c)
+    refused = 0
+    for c, g in zip(cases, checker(cases)):
+        if g is None:
+            refused += 1
+        else:
+            assert _reproduces(c, g), c[:6]
+    assert refused > len(cases) // 2
+
+
+def test_duplicate_position_and_wrapping(checker):
+    assert checker([[(0, 0, 4096), (0, 0, 8192)]]) == [None]
+    # addresses near the top of the 64-bit space: the grid is checked modulo 2^64
+    top = (1 << 64) - 3 * 4096
+    g = checker([[(0, 0, top), (0, 1, top + 4096), (1, 0, top + 8192 - 4096 + 4096)]])[0]
+    assert g is not None and _reproduces([(0, 0, top), (0, 1, top + 4096), (1, 0, top + 8192)], g)
