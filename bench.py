@@ -54,7 +54,9 @@ CONFIGS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100,
+                    help="timed steps (default 100: ~46 ms of RS(8,3) encode, so the bracketing barrier / "
+                         "synchronize costs < 0.5 %% of the timed region instead of ~2 %% at 20 steps)")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="encode83", choices=sorted(CONFIGS))
     ap.add_argument("--blocks", type=int, default=0, help="blocks per GPU (default: 1024 for 1 MiB, 512 for 4 MiB, 64 for 16 MiB blocks)")
@@ -445,16 +447,19 @@ class Workload:
         return n
 
     def timed(self, steps):
-        """K steps bracketed by HIP events on this device's stream; returns the
-        per-step times in ms (the stream is drained on return)."""
+        """K steps bracketed by two HIP events on this device's stream (nothing
+        else between the launches: an event after every step measured 0.9 %
+        slower, profiles/r05/s8/gap_probe.txt); returns the K per-step times in
+        ms -- each the average over the region (the stream is drained on
+        return)."""
         with torch.cuda.device(self.dev), torch.cuda.stream(self.stream):
-            evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
-            evs[0].record(self.stream)
-            for i in range(steps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(self.stream)
+            for _ in range(steps):
                 self.step()
-                evs[i + 1].record(self.stream)
+            e1.record(self.stream)
             self.stream.synchronize()
-        return [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)]
+        return [e0.elapsed_time(e1) / steps] * steps
 
     def round_trip(self):
         """codec configs: the timed steps ran over already-consistent blocks --
