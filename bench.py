@@ -121,6 +121,31 @@ def parse():
     return ap.parse_args()
 
 
+_REAL_STDOUT = None
+
+
+def quiet_stdout() -> None:
+    """The contract is ONE JSON line on stdout, but native libraries print
+    there too (Gloo: "[Gloo] Rank r is connected to n peer ranks ..." from
+    every rank, interleaved): from here on fd 1 goes to stderr, and the line
+    is written to the saved stdout (emit)."""
+    global _REAL_STDOUT
+    if _REAL_STDOUT is None:
+        sys.stdout.flush()
+        _REAL_STDOUT = os.dup(1)
+        os.dup2(2, 1)
+
+
+def emit(obj) -> None:
+    line = (json.dumps(obj) + "\n").encode()
+    if _REAL_STDOUT is None:
+        sys.stdout.write(line.decode())
+        sys.stdout.flush()
+        return
+    sys.stdout.flush()
+    os.write(_REAL_STDOUT, line)
+
+
 def free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -178,7 +203,7 @@ def launch_check(args) -> None:
         ranks = [None] * seen
         dist_.all_gather_object(ranks, me)
     if rank == 0:
-        print(json.dumps({"launch_check": True, "n_gpus": args.gpus, "ranks_seen": seen, "ranks": ranks}), flush=True)
+        emit({"launch_check": True, "n_gpus": args.gpus, "ranks_seen": seen, "ranks": ranks})
     if world > 1:
         dist_.destroy_process_group()
 
@@ -188,9 +213,11 @@ def main():
     if args.process_model == "single":
         if "WORLD_SIZE" in os.environ and os.environ["WORLD_SIZE"] != "1":
             raise SystemExit("--process-model single runs as one process (not under a launcher)")
+        quiet_stdout()
         return run_single(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch(args.gpus, sys.argv[1:]))
+    quiet_stdout()
     if args.launch_check:
         return launch_check(args)
     run(args)
@@ -711,7 +738,7 @@ def run(args):
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_leg(args, shape, w)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     if world > 1:
         dist.destroy_process_group()
 
@@ -752,7 +779,7 @@ def run_single(args):
         out["roofline"]["round_trip_bit_exact"] = all(w.round_trip() for w in works)
     if n == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_leg(args, shape, works[0])
-    print(json.dumps(out), flush=True)
+    emit(out)
 
 
 def host_probe(local: int, all_devices: bool):

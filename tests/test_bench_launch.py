@@ -121,9 +121,11 @@ def test_cpu_threads_default_is_available_parallelism(monkeypatch):
 
 def test_direct_launch_eight_ranks():
     """The driver's N = 8 launch shape (bench.py started directly): eight
-    ranks, one line, ranks 0..7 with their own processes."""
+    ranks, one line, ranks 0..7 with their own processes -- and nothing else
+    on stdout (Gloo's connection messages go to stderr)."""
     r = _run([sys.executable, BENCH, "--gpus", "8", "--launch-check"], timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
+    assert len(r.stdout.strip().splitlines()) == 1, r.stdout[:2000]
     lines = _json_lines(r.stdout)
     assert len(lines) == 1 and lines[0]["ranks_seen"] == 8 and lines[0]["n_gpus"] == 8
     assert [x["rank"] for x in lines[0]["ranks"]] == list(range(8))
@@ -135,6 +137,7 @@ def test_torchrun_launch_eight_ranks():
               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), BENCH, "--gpus", "8", "--launch-check"],
              timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
+    assert len(r.stdout.strip().splitlines()) == 1, r.stdout[:2000]
     lines = _json_lines(r.stdout)
     assert len(lines) == 1 and lines[0]["ranks_seen"] == 8
     assert [x["local_rank"] for x in lines[0]["ranks"]] == list(range(8))

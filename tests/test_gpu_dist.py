@@ -82,8 +82,8 @@ def test_bench_self_launch_eight_ranks(gpu, tmp_path):
            "--warmup", "1", "--ramp-seconds", "0.05", "--no-cpu", "--dump-dir", str(tmp_path), "--dump-blocks", "2"]
     out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=_env())
     assert out.returncode == 0, out.stderr[-3000:]
-    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, out.stdout[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), out.stdout[-2000:]    # nothing else on stdout
     b = json.loads(lines[0])
     assert b["n_gpus"] == 8 and b["ranks_seen"] == 8 and b["launcher"] == "spawn"
     assert [d["rank"] for d in b["devices"]] == list(range(8))
