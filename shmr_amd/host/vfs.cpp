@@ -1445,7 +1445,7 @@ Status VirtualFile::load_blocks(const std::vector<size_t>& block_indices,
         const size_t nd = std::max<size_t>(1, devices.size());
         std::atomic<size_t> rebuilt{0};
         std::mutex tmu;
-        parallel_for(todo.size(), per_block_tasks, [&](size_t q) {
+        parallel_for(todo.size(), per_block_read_tasks, [&](size_t q) {
             const size_t i = todo[q];
             const VirtualBlock& b = blocks[i];
             bool rec = false;

@@ -269,9 +269,13 @@ public:
     // memory bandwidth and pipelining measured slower.
     static constexpr size_t kAutoBatch = ~size_t(0);
     size_t pipeline_batch_bytes = kAutoBatch;
-    // Concurrent per-block tasks of the mapped-buffer flush / load (the
+    // Concurrent per-block tasks of the mapped-buffer flush and load (the
     // reference's rayon fan-out, mod.rs:93-96; the worker pool has 32 threads).
+    // Loads run 24: +13 %, +14 % and +10-13 % read with erasure on three boxes
+    // (-1 % on a fourth; profiles/r04/s2, s9, s10, profiles/r05/s11); flushes
+    // stay at 16 (24 was no faster, and slower with fsync on one box).
     size_t per_block_tasks = 16;
+    size_t per_block_read_tasks = 24;
 
     // read (mod.rs:137-180): the blocks the range touches are loaded in one
     // batched call (load_blocks) and copied out as the reference's chunk loop

@@ -50,7 +50,9 @@ Result run_once(const std::shared_ptr<const ShmrFsConfig>& cfg, uint64_t ino, co
     vf.populate(cfg);
     vf.block_size = block_bytes;
     vf.pipeline_batch_bytes = batch_bytes;
-    if (const char* e = std::getenv("SHMR_VFS_TASKS")) vf.per_block_tasks = std::strtoull(e, nullptr, 10);
+    if (const char* e = std::getenv("SHMR_VFS_TASKS"))   // both (an experiment's override)
+        vf.per_block_tasks = vf.per_block_read_tasks = std::strtoull(e, nullptr, 10);
+    if (const char* e = std::getenv("SHMR_VFS_READ_TASKS")) vf.per_block_read_tasks = std::strtoull(e, nullptr, 10);
     for (size_t i = 0; i < nblk; ++i) {
         VirtualBlock b;
         DIE_IF(VirtualBlock::create(ino, i + 1, cfg, block_bytes, BlockTopology::erasure(1, 8, 3), &b));
@@ -235,7 +237,8 @@ int main(int argc, char** argv) {
             rate(best.per_block_sync_s).c_str(), rate(best.read_s).c_str(), rate(best.load.codec_s).c_str(),
             rate(best.load.io_s).c_str(), rate(best.load.total_s).c_str(), best.load.blocks, best.sync.prepare_s * 1e3,
             best.load.prepare_s * 1e3, needed ? "true" : "false", best.shard_reads_per_block,
-            std::getenv("SHMR_VFS_TASKS") ? std::getenv("SHMR_VFS_TASKS") : "16", tasks_json(best).c_str(), dio);
+            std::getenv("SHMR_VFS_TASKS") ? std::getenv("SHMR_VFS_TASKS") : "\"16 (flush) / 24 (load)\"",
+            tasks_json(best).c_str(), dio);
         std::fflush(stdout);
     }
     return 0;
