@@ -208,6 +208,27 @@ def test_ptrs_dev_validation_precedes_device_use():
         rs.encode_ptrs_dev([[torch.zeros(64, dtype=torch.uint8) for _ in range(6)]])   # host tensors
 
 
+def test_alloc_shards_argument_checks():
+    """shmr_ec_device_alloc_shards / _free_shards: bad arguments are refused
+    before any device work; without a GPU a well-formed allocation reports
+    NoDevice; only a slab base the library handed out can be freed (a NULL
+    first pointer is a no-op)."""
+    import ctypes
+    import torch
+    L = _native.lib()
+    u8p = _native._u8p
+    arr = (u8p * 8)()
+    assert L.shmr_ec_device_alloc_shards(0, 0, 4, 64, arr) == -100
+    assert L.shmr_ec_device_alloc_shards(0, 2, 0, 64, arr) == -100
+    assert L.shmr_ec_device_alloc_shards(0, 2, 4, 0, arr) == -100
+    assert L.shmr_ec_device_alloc_shards(0, 2, 4, 64, None) == -100
+    assert L.shmr_ec_device_alloc_shards(0, 1 << 40, 1 << 30, 64, arr) == -100   # count overflows
+    if not torch.cuda.is_available():
+        assert L.shmr_ec_device_alloc_shards(0, 2, 4, 64, arr) == -101           # NoDevice
+    assert L.shmr_ec_device_free_shards(0, None) == 0
+    assert L.shmr_ec_device_free_shards(0, ctypes.cast(ctypes.c_void_p(0x7000), u8p)) == -100
+
+
 def test_compute_without_gpu_fails_loudly():
     """No CPU fallback: on a machine without a GPU the compute entry points
     report NoDevice instead of computing anything."""
