@@ -303,7 +303,8 @@ int shmr_ec_device_free(int device, void* p);
  * the *_ptrs_dev calls tables that form a slot grid, which run through the
  * strided kernels (knob "ptrs_grid").  The bytes are not initialised.  Free
  * with shmr_ec_device_free_shards(device, out_ptrs[0]); any other pointer
- * returns INVALID_ARGUMENT. */
+ * returns INVALID_ARGUMENT (shmr_ec_device_free(device, out_ptrs[0]) frees
+ * it too). */
 int shmr_ec_device_alloc_shards(int device, size_t nblocks, size_t shards_per_block, size_t shard_len,
                                 uint8_t** out_ptrs);
 int shmr_ec_device_free_shards(int device, uint8_t* first);

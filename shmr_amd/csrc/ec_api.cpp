@@ -341,6 +341,12 @@ int shmr_ec_device_free(int device, void* p) {
         if (!p) return SHMR_EC_OK;
         int rc = core::check_device(device);
         if (rc) return rc;
+        {   // a slab freed this way leaves no registry entry for a later
+            // allocation at the same address to inherit
+            std::lock_guard<std::mutex> lk(g_slab_mu);
+            auto it = g_slabs.find(uintptr_t(p));
+            if (it != g_slabs.end() && it->second == device) g_slabs.erase(it);
+        }
         core::DeviceScope scope(device);
         if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
         core::RelaxedCapture relaxed;
@@ -385,7 +391,7 @@ int shmr_ec_device_free_shards(int device, uint8_t* first) {
             std::lock_guard<std::mutex> lk(g_slab_mu);
             auto it = g_slabs.find(uintptr_t(first));
             if (it == g_slabs.end() || it->second != device) return SHMR_EC_INVALID_ARGUMENT;
-            g_slabs.erase(it);
+            g_slabs.erase(it);   // under the lock: one of two racing frees wins
         }
         return shmr_ec_device_free(device, first);
     });

@@ -72,6 +72,10 @@ def test_alloc_shards_placement_and_free(gpu):
     assert L.shmr_ec_device_free_shards(0, arr[0]) == 0
     assert L.shmr_ec_device_free_shards(0, arr[0]) == -100          # freed already
     assert L.shmr_ec_device_free_shards(0, None) == 0
+    # freed the plain way, a slab leaves no registry entry behind
+    assert L.shmr_ec_device_alloc_shards(0, 1, 4, 64, arr) == 0
+    assert L.shmr_ec_device_free(0, arr[0]) == 0
+    assert L.shmr_ec_device_free_shards(0, arr[0]) == -100
 
 
 @pytest.mark.parametrize("k,p,S,B", [(8, 3, 65536, 9), (10, 4, 3 * 8192 + 2458, 5), (4, 2, 4096 * 5, 33),
