@@ -143,7 +143,9 @@ def emit(obj) -> None:
         sys.stdout.flush()
         return
     sys.stdout.flush()
-    os.write(_REAL_STDOUT, line)
+    view = memoryview(line)
+    while view:                      # os.write may take only part of a long line
+        view = view[os.write(_REAL_STDOUT, view):]
 
 
 def free_port() -> int:
