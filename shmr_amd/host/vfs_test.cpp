@@ -414,14 +414,16 @@ struct ChunkModel {
 
 void test_virtual_file_chunk_model() {
     auto cfg = test_config();
-    for (int trial = 0; trial < 4; ++trial) {
-        const uint64_t bs = trial % 2 ? 64 * 1024 : 16 * 1024;
+    for (int trial = 0; trial < 6; ++trial) {
+        // trials 4-5: 4 MiB blocks and multi-MiB copies at odd offsets
+        const bool big = trial >= 4;
+        const uint64_t bs = big ? 4 << 20 : trial % 2 ? 64 * 1024 : 16 * 1024;
         VirtualFile vf = VirtualFile::new_with(40 + trial, 0);
         vf.populate(cfg);
         vf.block_size = bs;
         ChunkModel m(bs);
         std::mt19937_64 rng(777 + trial);
-        for (int op = 0; op < 300; ++op) {
+        for (int op = 0; op < (big ? 24 : 300); ++op) {
             const bool is_write = vf.blocks.empty() || rng() % 3 != 0;
             const uint64_t span = vf.blocks.size() * bs + 2 * bs;
             uint64_t pos = rng() % span;
