@@ -524,6 +524,13 @@ class DeviceBuffer:
             self._p = None
 
 
+def _slot_pitch(shard_len: int) -> int:
+    """The allocator's slot pitch: shard_len rounded up
+    to 4 KiB, one page more when that is a multiple of 64 KiB."""
+    p = (shard_len + 4095) // 4096 * 4096
+    return p + 4096 if p % 65536 == 0 else p
+
+
 class ShardSlab:
     """Shard buffers from shmr_ec_device_alloc_shards: ``nblocks`` x
     ``shards_per_block`` buffers of ``shard_len`` bytes at the slot pitch of the
@@ -543,7 +550,7 @@ class ShardSlab:
         self.ptrs = np.array([ctypes.cast(arr[j], ctypes.c_void_p).value for j in range(n)], dtype=np.uint64)
         self._first = arr[0]
         self.nblocks, self.shards_per_block, self.shard_len, self.device = nblocks, shards_per_block, shard_len, device
-        self.pitch = int(self.ptrs[1] - self.ptrs[0]) if n > 1 else (shard_len + 4095) // 4096 * 4096
+        self.pitch = int(self.ptrs[1] - self.ptrs[0]) if n > 1 else _slot_pitch(shard_len)
         self._views = []
 
     def tensor(self):

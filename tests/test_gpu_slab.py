@@ -61,6 +61,7 @@ def test_alloc_shards_placement_and_free(gpu):
         assert int(slab.ptrs[0]) % 256 == 0
         assert np.array_equal(np.diff(slab.ptrs.astype(np.int64)), np.full(32, pitch))
         del slab
+    assert shmr_amd.ShardSlab(1, 1, 65536).pitch == 69632          # one buffer: the same rule
     arr = (_u8p * 4)()
     assert L.shmr_ec_device_alloc_shards(0, 0, 4, 64, arr) == -100
     assert L.shmr_ec_device_alloc_shards(0, 1, 0, 64, arr) == -100
