@@ -1,0 +1,140 @@
+// Device-resident blocks coded one call per block -- the reference's per-block
+// shape (VirtualFile::sync_data fans blocks out over rayon, src/vfs/mod.rs:93-96;
+// each VirtualBlock::sync_data encodes its own block, block.rs:427) on a device
+// Block Cache -- against one batched call over the same blocks.
+//
+// RS(8,3) 4 MiB blocks (S = 512 KiB) in padded slots of one hipMalloc'd slab.
+// Modes: the batch call (HIP events); T host threads each on a stream of its
+// own, each calling shmr_ec_encode_batch_dev for one block at a time, either
+// waiting for every call (hipStreamSynchronize: a per-block flush that must
+// know its parity is done) or only at the end (stream-ordered).  Every mode's
+// parity is compared byte for byte with the batch call's.
+// Build: hipcc --offload-arch=gfx950 -O2 -std=c++17 -Iinclude -o tools/_abx/perblock_dev tools/perblock_dev.cpp \
+//          -Lshmr_amd/_lib -lshmr_ec -Wl,-rpath,'$ORIGIN/../../shmr_amd/_lib' -lpthread
+// Usage: perblock_dev [blocks=256] [reps=5]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <thread>
+#include <vector>
+
+#include "shmr_ec.h"
+
+namespace {
+
+constexpr uint32_t K = 8, P = 3, T = K + P;
+constexpr size_t S = size_t(512) << 10;
+constexpr size_t PITCH = S + 4096;   // the slot rule: 512 KiB is a multiple of 64 KiB -> one page more
+constexpr size_t BLOCK = T * PITCH;
+
+#define CHECK_HIP(x)                                                                  \
+    do {                                                                              \
+        if ((x) != hipSuccess) {                                                      \
+            std::fprintf(stderr, "%s failed at line %d\n", #x, __LINE__);            \
+            std::exit(1);                                                             \
+        }                                                                             \
+    } while (0)
+
+int encode_one(shmr_ec_t* rs, uint8_t* slab, size_t b, size_t n, hipStream_t s) {
+    uint8_t* blk = slab + b * BLOCK;
+    return shmr_ec_encode_batch_dev(rs, blk, PITCH, BLOCK, blk + K * PITCH, PITCH, BLOCK, n, S, 0, s);
+}
+
+std::vector<uint8_t> parity_of(const uint8_t* slab, size_t blocks) {
+    std::vector<uint8_t> out(blocks * P * S);
+    for (size_t b = 0; b < blocks; ++b)
+        CHECK_HIP(hipMemcpy2D(out.data() + b * P * S, S, slab + b * BLOCK + K * PITCH, PITCH, S, P,
+                              hipMemcpyDeviceToHost));
+    return out;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    const size_t blocks = argc > 1 ? std::strtoul(argv[1], nullptr, 10) : 256;
+    const int reps = argc > 2 ? std::atoi(argv[2]) : 5;
+    if (shmr_ec_device_init(0) != 0) {
+        std::fprintf(stderr, "no device\n");
+        return 1;
+    }
+    shmr_ec_t* rs = nullptr;
+    if (shmr_ec_new(K, P, &rs) != 0) return 1;
+    uint8_t* slab = nullptr;
+    CHECK_HIP(hipMalloc(&slab, blocks * BLOCK));
+    {   // random data shards, zero parity
+        std::vector<uint8_t> host(blocks * BLOCK, 0);
+        std::mt19937_64 rng(0x53484D52);
+        for (size_t b = 0; b < blocks; ++b)
+            for (uint32_t i = 0; i < K; ++i)
+                for (size_t c = 0; c < S; c += 8) {
+                    const uint64_t v = rng();
+                    std::memcpy(&host[b * BLOCK + i * PITCH + c], &v, 8);
+                }
+        CHECK_HIP(hipMemcpy(slab, host.data(), host.size(), hipMemcpyHostToDevice));
+    }
+    const double data_gib = double(blocks) * K * S / double(1u << 30);
+    hipStream_t s0;
+    CHECK_HIP(hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
+    hipEvent_t e0, e1;
+    CHECK_HIP(hipEventCreate(&e0));
+    CHECK_HIP(hipEventCreate(&e1));
+    // batch reference (also warms plans and clocks)
+    double best_batch = 1e30;
+    for (int r = 0; r < reps + 2; ++r) {
+        CHECK_HIP(hipEventRecord(e0, s0));
+        if (encode_one(rs, slab, 0, blocks, s0) != 0) return 1;
+        CHECK_HIP(hipEventRecord(e1, s0));
+        CHECK_HIP(hipEventSynchronize(e1));
+        float ms = 0;
+        CHECK_HIP(hipEventElapsedTime(&ms, e0, e1));
+        if (r >= 2) best_batch = std::min(best_batch, double(ms) / 1e3);
+    }
+    const std::vector<uint8_t> want = parity_of(slab, blocks);
+    std::printf("{\"mode\": \"batch\", \"blocks\": %zu, \"GiBps\": %.1f, \"us_per_block\": %.2f}\n", blocks,
+                data_gib / best_batch, best_batch / blocks * 1e6);
+    std::fflush(stdout);
+    for (int wait_each = 1; wait_each >= 0; --wait_each)
+        for (int threads : {1, 2, 4, 8, 16, 32}) {
+            std::vector<hipStream_t> ss(static_cast<size_t>(threads));
+            for (auto& s : ss) CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+            double best = 1e30;
+            bool ok = true;
+            for (int r = 0; r < reps + 1; ++r) {
+                CHECK_HIP(hipMemset2D(slab + K * PITCH, BLOCK, 0, P * PITCH, blocks));   // parity cleared
+                CHECK_HIP(hipDeviceSynchronize());
+                std::vector<int> rc(size_t(threads), 0);
+                const auto t0 = std::chrono::steady_clock::now();
+                std::vector<std::thread> ts;
+                for (int t = 0; t < threads; ++t)
+                    ts.emplace_back([&, t] {
+                        hipStream_t s = ss[size_t(t)];
+                        for (size_t b = size_t(t); b < blocks; b += size_t(threads)) {
+                            if (encode_one(rs, slab, b, 1, s) != 0) rc[size_t(t)] = 1;
+                            if (wait_each && hipStreamSynchronize(s) != hipSuccess) rc[size_t(t)] = 1;
+                        }
+                        if (hipStreamSynchronize(s) != hipSuccess) rc[size_t(t)] = 1;
+                    });
+                for (auto& th : ts) th.join();
+                const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+                for (int x : rc) ok = ok && x == 0;
+                if (r >= 1) best = std::min(best, sec);   // rep 0 warms the streams' state
+            }
+            const bool same = parity_of(slab, blocks) == want;
+            std::printf("{\"mode\": \"per_block\", \"wait_each_call\": %s, \"threads\": %d, \"blocks\": %zu, "
+                        "\"GiBps\": %.1f, \"us_per_block\": %.2f, \"of_batch\": %.3f, \"ok\": %s, "
+                        "\"parity_equals_batch\": %s}\n",
+                        wait_each ? "true" : "false", threads, blocks, data_gib / best, best / blocks * 1e6,
+                        best_batch / best, ok ? "true" : "false", same ? "true" : "false");
+            std::fflush(stdout);
+            for (auto& s : ss) CHECK_HIP(hipStreamDestroy(s));
+            if (!ok || !same) return 1;
+        }
+    CHECK_HIP(hipFree(slab));
+    shmr_ec_free(rs);
+    return 0;
+}
