@@ -12,6 +12,9 @@
 // Build: hipcc --offload-arch=gfx950 -O2 -std=c++17 -Iinclude -o tools/_abx/perblock_dev tools/perblock_dev.cpp \
 //          -Lshmr_amd/_lib -lshmr_ec -Wl,-rpath,'$ORIGIN/../../shmr_amd/_lib' -lpthread
 // Usage: perblock_dev [blocks=256] [reps=5]
+// Linked against libshmr_ec_tools.so instead (perblock_dev_tools), SHMR_PB_SWEEP=1
+// repeats the per-block modes for kernel variants (tuning knobs), interleaved,
+// so a kernel trace shows each variant's single-block kernel time.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -20,6 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -98,8 +102,42 @@ int main(int argc, char** argv) {
     std::printf("{\"mode\": \"batch\", \"blocks\": %zu, \"GiBps\": %.1f, \"us_per_block\": %.2f}\n", blocks,
                 data_gib / best_batch, best_batch / blocks * 1e6);
     std::fflush(stdout);
+    struct Mode {
+        int wait_each, threads;
+    };
+    std::vector<Mode> modes;
     for (int wait_each = 1; wait_each >= 0; --wait_each)
-        for (int threads : {1, 2, 4, 8, 16, 32}) {
+        for (int threads : {1, 2, 4, 8, 16, 32}) modes.push_back({wait_each, threads});
+    // variant sweep (tools build): knob sets, each over the latency / throughput modes
+    std::vector<std::vector<std::pair<const char*, int>>> variants = {{}};
+    if (std::getenv("SHMR_PB_SWEEP")) {
+        // (depths 3/5/9 and the LDS-DMA ring are compiled without the early prologue)
+        variants = {{{"encode.depth", 2}},
+                    {{"encode.depth", 2}, {"encode.early", 0}},
+                    {{"encode.depth", 3}, {"encode.early", 0}},
+                    {{"encode.depth", 5}, {"encode.early", 0}},
+                    {{"encode.depth", 9}, {"encode.early", 0}},
+                    {{"encode.depth", 9}, {"encode.early", 0}, {"encode.glds", 1}},
+                    {{"encode.threads", 128}, {"encode.depth", 2}, {"encode.early", 0}},
+                    {{"encode.depth", 2}}};
+        modes = {{1, 1}, {1, 16}, {0, 1}, {0, 16}};
+    }
+    for (const auto& knobs : variants) {
+    for (const char* key : {"encode.depth", "encode.early", "encode.threads", "encode.glds"})
+        (void)shmr_ec_set_tuning(key, std::strcmp(key, "encode.threads") == 0 ? 256 : -2);
+    std::string label;
+    for (const auto& kv : knobs) {
+        if (shmr_ec_set_tuning(kv.first, kv.second) != 0) {
+            std::fprintf(stderr, "knob %s=%d refused\n", kv.first, kv.second);
+            return 1;
+        }
+        label += std::string(label.empty() ? "" : " ") + kv.first + "=" + std::to_string(kv.second);
+    }
+    char variant[256] = {0};
+    (void)shmr_ec_describe_variant(0, K, P, variant, sizeof variant);
+    for (const Mode& md : modes) {
+        const int wait_each = md.wait_each, threads = md.threads;
+        {
             std::vector<hipStream_t> ss(static_cast<size_t>(threads));
             for (auto& s : ss) CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
             double best = 1e30;
@@ -125,15 +163,18 @@ int main(int argc, char** argv) {
                 if (r >= 1) best = std::min(best, sec);   // rep 0 warms the streams' state
             }
             const bool same = parity_of(slab, blocks) == want;
-            std::printf("{\"mode\": \"per_block\", \"wait_each_call\": %s, \"threads\": %d, \"blocks\": %zu, "
+            std::printf("{\"mode\": \"per_block\", \"knobs\": \"%s\", \"variant\": \"%s\", "
+                        "\"wait_each_call\": %s, \"threads\": %d, \"blocks\": %zu, "
                         "\"GiBps\": %.1f, \"us_per_block\": %.2f, \"of_batch\": %.3f, \"ok\": %s, "
                         "\"parity_equals_batch\": %s}\n",
-                        wait_each ? "true" : "false", threads, blocks, data_gib / best, best / blocks * 1e6,
-                        best_batch / best, ok ? "true" : "false", same ? "true" : "false");
+                        label.c_str(), variant, wait_each ? "true" : "false", threads, blocks, data_gib / best,
+                        best / blocks * 1e6, best_batch / best, ok ? "true" : "false", same ? "true" : "false");
             std::fflush(stdout);
             for (auto& s : ss) CHECK_HIP(hipStreamDestroy(s));
             if (!ok || !same) return 1;
         }
+    }
+    }
     CHECK_HIP(hipFree(slab));
     shmr_ec_free(rs);
     return 0;
