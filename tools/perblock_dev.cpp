@@ -57,6 +57,33 @@ std::vector<uint8_t> parity_of(const uint8_t* slab, size_t blocks) {
     return out;
 }
 
+__global__ void nop_kernel(uint8_t* p) {
+    if (p && threadIdx.x == 1024) p[0] = 0;   // never true: an empty 256-lane workgroup
+}
+
+// Host time per enqueue, one thread, one stream, nothing waited for: the
+// library's per-block call against a bare hipLaunchKernelGGL of an empty
+// kernel with the same grid (128 workgroups of 256 lanes).
+void enqueue_cost(shmr_ec_t* rs, uint8_t* slab, size_t blocks, hipStream_t s) {
+    constexpr int kCalls = 512;
+    for (int rep = 0; rep < 3; ++rep) {
+        CHECK_HIP(hipStreamSynchronize(s));
+        auto t0 = std::chrono::steady_clock::now();
+        for (int i = 0; i < kCalls; ++i)
+            if (encode_one(rs, slab, size_t(i) % blocks, 1, s) != 0) std::exit(1);
+        const double lib = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        CHECK_HIP(hipStreamSynchronize(s));
+        t0 = std::chrono::steady_clock::now();
+        for (int i = 0; i < kCalls; ++i) hipLaunchKernelGGL(nop_kernel, dim3(128), dim3(256), 0, s, slab);
+        const double raw = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        CHECK_HIP(hipGetLastError());
+        CHECK_HIP(hipStreamSynchronize(s));
+        std::printf("{\"mode\": \"enqueue_cost\", \"calls\": %d, \"library_us_per_call\": %.2f, "
+                    "\"bare_launch_us\": %.2f}\n", kCalls, lib / kCalls * 1e6, raw / kCalls * 1e6);
+        std::fflush(stdout);
+    }
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -99,6 +126,7 @@ int main(int argc, char** argv) {
         if (r >= 2) best_batch = std::min(best_batch, double(ms) / 1e3);
     }
     const std::vector<uint8_t> want = parity_of(slab, blocks);
+    enqueue_cost(rs, slab, blocks, s0);
     std::printf("{\"mode\": \"batch\", \"blocks\": %zu, \"GiBps\": %.1f, \"us_per_block\": %.2f}\n", blocks,
                 data_gib / best_batch, best_batch / blocks * 1e6);
     std::fflush(stdout);
