@@ -587,9 +587,10 @@ struct VirtualBlock::State {
     }
     // VfsOptions::direct_io: shard i's O_DIRECT descriptor, opened on first
     // use (creating the file like ensure_fd); -1 when the file system refuses
-    // it (then never retried for this handle).  Caller holds handles_mu.
-    // (dfds is sized with the handles by open_handles, before the parallel
-    // shard I/O that calls this for distinct i.)
+    // it (then never retried for this handle).  The block operation that
+    // calls this holds handles_mu; its parallel shard workers each touch only
+    // their own i (dfds is sized with the handles by open_handles, before
+    // that parallel shard I/O starts).
     int direct_fd(size_t i, const ShmrFsConfig& cfg) {
         if (i >= dfds.size()) return -1;
         if (dfds[i] >= 0 || dfds[i] == -2) return dfds[i] >= 0 ? dfds[i] : -1;
