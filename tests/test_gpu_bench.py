@@ -85,3 +85,23 @@ def test_bench_single_process_model(gpu, config):
     assert d["cpu_baseline"]["value"] > 0
     if config == "codec104":
         assert d["roofline"]["round_trip_bit_exact"] is True
+
+
+@pytest.mark.gpu
+def test_bench_single_process_model_eight_devices(gpu):
+    """--process-model single --gpus 8, rehearsed on one card
+    (SHMR_BENCH_SHARE_GPU=1: eight device slots, eight host threads and
+    streams on the same GPU): one line, eight per-device figures, global
+    batch 8 x B, the codec round trip exact on every device."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1", "--ramp-seconds", "0.05",
+           "--no-cpu", "--config", "codec104", "--blocks", "2", "--process-model", "single", "--gpus", "8"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=150,
+                         env=dict(os.environ, SHMR_BENCH_SHARE_GPU="1"))
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["process_model"] == "single" and d["n_gpus"] == 8 and d["distinct_gpus"] == 1
+    assert len(d["per_device"]) == 8 and all(0 < x["frac"] < 1 for x in d["per_device"])
+    assert d["config"]["global_batch_blocks"] == 16 and d["value"] > 0
+    assert d["roofline"]["round_trip_bit_exact"] is True and d["cpu_baseline"] is None
