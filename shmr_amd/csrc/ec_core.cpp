@@ -1357,8 +1357,8 @@ int PtrTableCache::lookup(const void* tab, size_t bytes, hipStream_t stream, con
     Entry& e = e_[victim];
     if (!e.host) {
         // (no arena memory or events for a new entry: the caller takes the upload ring)
-        uint8_t *h = nullptr, *d = nullptr;
-        if (arena_alloc(dev_id_, UploadRing::kSlotBytes, false, &h, &d) != SHMR_EC_OK) return SHMR_EC_OK;
+        uint8_t *hblk = nullptr, *dblk = nullptr;
+        if (arena_alloc(dev_id_, UploadRing::kSlotBytes, false, &hblk, &dblk) != SHMR_EC_OK) return SHMR_EC_OK;
         RelaxedCapture relaxed;
         if (hipEventCreateWithFlags(&e.up, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&e.used, hipEventDisableTiming) != hipSuccess ||
@@ -1367,8 +1367,8 @@ int PtrTableCache::lookup(const void* tab, size_t bytes, hipStream_t stream, con
             (void)hipGetLastError();
             return SHMR_EC_OK;   // the arena block is abandoned (permanent memory)
         }
-        e.host = h;
-        e.dev = d;
+        e.host = hblk;
+        e.dev = dblk;
     }
     e.valid = false;
     std::memcpy(e.host, tab, bytes);

@@ -1178,15 +1178,15 @@ Status VirtualFile::read(uint64_t pos, uint8_t* buf, size_t len, size_t* nread) 
                                                [&](size_t bi) -> uint64_t { return blocks[bi].buffered_len(); },
                                                &c, &done);
     {   // runs already copied during the load (same run, same bytes) are skipped
-        std::vector<ReadRun> rest;
+        std::vector<ReadRun> left;
         size_t e = 0;
         for (const ReadRun& r : runs) {
             while (e < early.size() && early[e].off < r.off) ++e;
             const bool same = e < early.size() && copied[e] && early[e].blk == r.blk &&
                               early[e].block_pos == r.block_pos && early[e].off == r.off && early[e].len == r.len;
-            if (!same) rest.push_back(r);
+            if (!same) left.push_back(r);
         }
-        runs.swap(rest);
+        runs.swap(left);
     }
     const uint64_t end_chunk = len / chunk_size + pos / chunk_size;
     std::vector<Status> res(runs.size());
