@@ -21,7 +21,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 @pytest.fixture(scope="module")
 def checker(tmp_path_factory):
     exe = str(tmp_path_factory.mktemp("grid") / "ptr_grid_check")
-    subprocess.run(["g++", "-O1", "-std=c++17", "-I", os.path.join(ROOT, "shmr_amd", "csrc"),
+    # under ASan + UBSan (any report aborts the checker and fails the test): the
+    # solver's __int128 products and its wrapping uint64 reproduction
+    subprocess.run(["g++", "-O1", "-std=c++17", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                    "-I", os.path.join(ROOT, "shmr_amd", "csrc"),
                     os.path.join(ROOT, "tools", "ptr_grid_check.cpp"), "-o", exe], check=True)
 
     def run(cases):
@@ -119,3 +122,27 @@ def test_duplicate_position_and_wrapping(checker):
     top = (1 << 64) - 3 * 4096
     g = checker([[(0, 0, top), (0, 1, top + 4096), (1, 0, top + 8192 - 4096 + 4096)]])[0]
     assert g is not None and _reproduces([(0, 0, top), (0, 1, top + 4096), (1, 0, top + 8192)], g)
+
+
+def test_adversarial_extremes(checker):
+    """Entries with addresses anywhere in the 64-bit space, block indices up to
+    2^40 and shard indices up to 255, random or on extreme grids: the solver's
+    exact-integer steps run under UBSan without a report, and every grid it
+    returns reproduces the table."""
+    rng = np.random.default_rng(33)
+    cases = []
+    for i in range(2000):
+        n = int(rng.integers(2, 9))
+        bs = sorted(set(int(x) for x in rng.integers(0, 1 << 40, size=n)))
+        if i % 2:                                   # on a grid with huge pitches, wrapping mod 2^64
+            base = int(rng.integers(0, 1 << 63)) * 2
+            bp, sp = int(rng.integers(0, 1 << 62)), int(rng.integers(0, 1 << 62))
+            case = [(b, int(j), (base + b * bp + int(j) * sp) & M64) for b in bs for j in sorted(
+                set(int(x) for x in rng.integers(0, 256, size=2)))]
+        else:                                       # random addresses
+            case = [(b, int(rng.integers(0, 256)), int(rng.integers(0, 1 << 63)) * 2 + int(rng.integers(0, 2)))
+                    for b in bs]
+        cases.append(case)
+    for c, g in zip(cases, checker(cases)):
+        if g is not None:
+            assert _reproduces(c, g), c[:4]
