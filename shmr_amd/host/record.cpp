@@ -417,8 +417,13 @@ Status VirtualFile::from_yaml(const std::string& text, VirtualFile* out, std::st
             if (!sh || sh->kind != Node::Seq) throw ParseError{"missing field shards"};
             for (const Node& sn : sh->items) {
                 if (sn.kind != Node::Map) throw ParseError{"shard is not a mapping"};
-                b.shards.push_back({as_str(sn.get("pool"), "pool"), as_str(sn.get("bucket"), "bucket"),
-                                    as_str(sn.get("filename"), "filename")});
+                // named locals, not one braced list: GCC 11 leaks the members a
+                // braced aggregate initialiser already built when a later one
+                // throws (found by LeakSanitizer on the record fuzz)
+                std::string pool = as_str(sn.get("pool"), "pool");
+                std::string bucket = as_str(sn.get("bucket"), "bucket");
+                std::string filename = as_str(sn.get("filename"), "filename");
+                b.shards.push_back({std::move(pool), std::move(bucket), std::move(filename)});
             }
             size_t need = 1;
             if (b.topology.kind == BlockTopology::Mirror) need = b.topology.n;
