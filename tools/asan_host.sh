@@ -5,6 +5,7 @@
 #
 #   tools/asan_host.sh build
 #   tools/asan_host.sh run [out_dir]      # every case of shmr_vfs_test
+#   LEAKS=1 tools/asan_host.sh run [dir]  # with LeakSanitizer (ROCm runtime suppressed)
 set -euo pipefail
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
 BIN="$ROOT/tools/_probe/vfs_test_asan"
@@ -47,23 +48,32 @@ run)
     OUT="${2:-$ROOT/gpurun_out/asan}"
     mkdir -p "$OUT"
     # protect_shadow_gap=0: the ROCm runtime maps GPU apertures in the low shadow gap
-    export ASAN_OPTIONS=detect_leaks=0:protect_shadow_gap=0:halt_on_error=1
+    # LEAKS=1: LeakSanitizer on, the ROCm runtime's own allocations suppressed
+    # (tools/lsan_rocm.supp); this repository's code stays checked
+    if [ "${LEAKS:-0}" = 1 ]; then
+        export ASAN_OPTIONS=detect_leaks=1:protect_shadow_gap=0:halt_on_error=1
+        export LSAN_OPTIONS="suppressions=$ROOT/tools/lsan_rocm.supp:print_suppressions=0"
+    else
+        export ASAN_OPTIONS=detect_leaks=0:protect_shadow_gap=0:halt_on_error=1
+    fi
     export UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1
     fail=0
-    if timeout -k 10 120 "$ROOT/tools/_probe/abi_check_asan" > "$OUT/abi_check.log" 2>&1; then
+    T="${CASE_TIMEOUT:-120}"     # seconds per case (LeakSanitizer's exit scan adds to the long cases)
+    if timeout -k 10 "$T" "$ROOT/tools/_probe/abi_check_asan" > "$OUT/abi_check.log" 2>&1; then
         echo "abi_check PASS"
     else
         echo "abi_check FAIL (see $OUT/abi_check.log)"; exit 1
     fi
     for cs in $CPU_CASES $GPU_CASES; do
         c="${cs%%:*}"
+        if [ -n "${ONLY:-}" ] && [[ " $ONLY " != *" $c "* ]]; then continue; fi
         rm -rf "$OUT/b" && mkdir -p "$OUT/b"
         input=()
         if [ "$c" != "$cs" ]; then
             python3 -c "import numpy as np; np.random.default_rng(7).integers(0, 256, ${cs#*:}, dtype=np.uint8).tofile('$OUT/input.bin')"
             input=("$OUT/input.bin")
         fi
-        if timeout -k 10 120 "$BIN" "$c" "$OUT/b" "${input[@]}" > "$OUT/$c.log" 2>&1 && [ "$(tail -1 "$OUT/$c.log")" = PASS ]; then
+        if timeout -k 10 "$T" "$BIN" "$c" "$OUT/b" "${input[@]}" > "$OUT/$c.log" 2>&1 && [ "$(tail -1 "$OUT/$c.log")" = PASS ]; then
             echo "$c PASS"
         else
             echo "$c FAIL (see $OUT/$c.log)"; fail=1
