@@ -53,7 +53,7 @@ std::atomic<int> g_alias_devices{0};   // tools build: alias device IDs (see ec_
 // Reconstructs over device shard-pointer tables take segment launches (plans in
 // the kernel arguments) when they fit; 0 = always the uploaded block/plan table
 std::atomic<int> g_ptrs_segs{1};
-// Pointer tables that name a slot grid (ptrs_dev_grid) take the strided kernels
+// Pointer tables that name a slot grid (ec_api.cpp ptrs_as_grid) take the strided kernels
 // of the *_batch_dev calls; 0 = always the table kernels
 std::atomic<int> g_ptrs_grid{1};
 // Misaligned device-resident shards: kAuto = the vector kernels (modes 0 / 1)
