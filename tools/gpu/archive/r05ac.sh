@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 5 (session 26): the final binaries (record-parser leak fix rebuilt into libshmr_vfs.so)
+# -- the whole GPU suite, smoke and the default bench line.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+O=gpurun_out/r05ac
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || exit $?
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
+timeout -k 10 300 python bench.py > $O/bench_default.jsonl 2>> $O/bench.err || exit $?
+echo done-ac
