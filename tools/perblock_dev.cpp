@@ -61,6 +61,32 @@ __global__ void nop_kernel(uint8_t* p) {
     if (p && threadIdx.x == 1024) p[0] = 0;   // never true: an empty 256-lane workgroup
 }
 
+// The same empty kernel with a kernel-argument block the size of the GF
+// kernels' ApplyArgs (~1 KiB: the segment table travels in the arguments).
+struct BigArgs {
+    uint8_t* p;
+    uint64_t pad[127];
+};
+__global__ void nop_big_kernel(const BigArgs a) {
+    if (a.p && threadIdx.x == 1024) a.p[a.pad[threadIdx.x & 127] & 7] = 0;   // never true
+}
+
+// GPU time of the empty kernels vs a single-block GF launch: kCalls of each,
+// back to back on one stream (a kernel trace separates them by name).
+void kernel_floor(shmr_ec_t* rs, uint8_t* slab, hipStream_t s) {
+    constexpr int kCalls = 256;
+    BigArgs big{};
+    big.p = slab;
+    for (int i = 0; i < kCalls; ++i) hipLaunchKernelGGL(nop_kernel, dim3(128), dim3(256), 0, s, slab);
+    for (int i = 0; i < kCalls; ++i) hipLaunchKernelGGL(nop_big_kernel, dim3(128), dim3(256), 0, s, big);
+    for (int i = 0; i < kCalls; ++i)
+        if (encode_one(rs, slab, 0, 1, s) != 0) std::exit(1);
+    CHECK_HIP(hipGetLastError());
+    CHECK_HIP(hipStreamSynchronize(s));
+    std::printf("{\"mode\": \"kernel_floor\", \"calls\": %d, \"sizeof_BigArgs\": %zu}\n", kCalls, sizeof(BigArgs));
+    std::fflush(stdout);
+}
+
 // Host time per enqueue, one thread, one stream, nothing waited for: the
 // library's per-block call against a bare hipLaunchKernelGGL of an empty
 // kernel with the same grid (128 workgroups of 256 lanes).
@@ -127,6 +153,8 @@ int main(int argc, char** argv) {
     }
     const std::vector<uint8_t> want = parity_of(slab, blocks);
     enqueue_cost(rs, slab, blocks, s0);
+    kernel_floor(rs, slab, s0);
+    if (std::getenv("SHMR_PB_FLOOR_ONLY")) return 0;
     std::printf("{\"mode\": \"batch\", \"blocks\": %zu, \"GiBps\": %.1f, \"us_per_block\": %.2f}\n", blocks,
                 data_gib / best_batch, best_batch / blocks * 1e6);
     std::fflush(stdout);
