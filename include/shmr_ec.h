@@ -143,6 +143,55 @@ int shmr_ec_reconstruct_start(shmr_ec_t* rs, uint8_t* const* shards, const size_
                               const uint8_t* present, size_t nshards, int data_only, shmr_ec_op_t** op);
 int shmr_ec_op_wait(shmr_ec_op_t* op);
 
+/* ---- one block per call on device buffers: the submission queue ----------- *
+ * The crate's encode / reconstruct of ONE block (ReedSolomon::encode at
+ * src/vfs/block.rs:427, reconstruct at :560) whose shards are device buffers
+ * on `device`: the same arguments, checks and errors as shmr_ec_encode /
+ * shmr_ec_reconstruct, with d_shards[i] device pointers.  The inputs must be
+ * complete when the call is made (written by synchronous copies, or by work
+ * the caller has waited for): these calls take no stream.
+ *
+ * The reference makes one such call per block from rayon workers
+ * (src/vfs/mod.rs:91-97).  One launch per block leaves the GPU launch-bound,
+ * so per device ID the library keeps a submission queue: a call's block is
+ * launched at once when fewer than "coalesce_depth" (default 2) batches are in
+ * flight on the queue's stream, and otherwise merges with every call that
+ * arrives meanwhile (from any thread, any codec; knob "coalesce_us": an idle
+ * queue waits that long for company) into the next launch -- one pointer-
+ * table call per (codec, operation, length, data_only) group, whose shards,
+ * if they sit on a slot lattice (a slab, a shmr_ec_pool), run the strided
+ * kernels over their slots.  The call returns when its own block is written,
+ * with its own status (a group's device error is its members' status).
+ * Completion is a word in pinned host memory that a one-wave kernel behind
+ * every batch advances: a waiting caller spins on it for "coalesce_spin_us"
+ * (default 30) and then sleeps until the queue's watcher thread (which
+ * follows the oldest batch, asleep on its event after "coalesce_watch_us",
+ * default 200) wakes it; a call waited for while still held back launches
+ * everything pending at once.  "coalesce_target" (default 64): that many pending
+ * calls launch even with "coalesce_depth" batches in flight.  The *_start forms return with the
+ * block queued (*op); shmr_ec_op_wait completes it.  While pending, inputs
+ * may be read, outputs must not be touched. */
+int shmr_ec_encode_dev(shmr_ec_t* rs, uint8_t* const* d_shards, const size_t* shard_lens, size_t nshards,
+                       int device);
+int shmr_ec_reconstruct_dev(shmr_ec_t* rs, uint8_t* const* d_shards, const size_t* shard_lens, const uint8_t* present,
+                            size_t nshards, int data_only, int device);
+int shmr_ec_encode_dev_start(shmr_ec_t* rs, uint8_t* const* d_shards, const size_t* shard_lens, size_t nshards,
+                             int device, shmr_ec_op_t** op);
+int shmr_ec_reconstruct_dev_start(shmr_ec_t* rs, uint8_t* const* d_shards, const size_t* shard_lens,
+                                  const uint8_t* present, size_t nshards, int data_only, int device,
+                                  shmr_ec_op_t** op);
+
+/* Submission-queue counters of a device ID since load: out[i] for i < n in
+ * the order below. */
+enum {
+    SHMR_EC_Q_REQUESTS = 0,   /* blocks submitted (device calls, and mapped host calls under "coalesce") */
+    SHMR_EC_Q_BATCHES = 1,    /* launch groups taken from the queue */
+    SHMR_EC_Q_MAX_BATCH = 2,  /* the most blocks one launch group merged */
+    SHMR_EC_Q_SLEEPS = 3,     /* waits that ended in a blocking event synchronize */
+    SHMR_EC_Q_COUNTERS = 4
+};
+int shmr_ec_queue_stats(int device, uint64_t* out, size_t n);
+
 /* ---- device-resident batched entry points ------------------------------ *
  * All pointers are device pointers on `device`; `stream` is a hipStream_t
  * (NULL = the null stream).  Block b's shard i lives at
@@ -309,6 +358,29 @@ int shmr_ec_device_alloc_shards(int device, size_t nblocks, size_t shards_per_bl
                                 uint8_t** out_ptrs);
 int shmr_ec_device_free_shards(int device, uint8_t* first);
 
+/* A device Block Cache of per-block slots (r06).  The reference's Block Cache
+ * takes and drops one block's buffers at a time (src/vfs/block.rs:148-152,
+ * :586-608); a shmr_ec_device_alloc_shards slab is freed only whole.  A pool
+ * carves block slots -- shards_per_block shard buffers of shard_len bytes at
+ * the slot pitch P of the device-resident batches (shard_len rounded up to 4
+ * KiB, one page more for a multiple of 64 KiB) -- from device slabs of
+ * slots_per_slab slots (allocated on demand, blocking), and hands them out one
+ * block at a time, the lowest free slot first:
+ *     out_ptrs[i] = slab + slot * shards_per_block * P + i * P.
+ * Pointer tables over pool blocks, in any order and with holes, lie on the
+ * slab's slot lattice: the *_ptrs_dev calls and the submission queue run them
+ * through the strided kernels over their slots.  shmr_ec_pool_free takes
+ * out_ptrs[0] of an alloc (anything else, or a second free: INVALID_ARGUMENT);
+ * shmr_ec_pool_destroy frees every slab (no kernel may still use them).  The
+ * bytes are not initialised. */
+typedef struct shmr_ec_pool shmr_ec_pool_t;
+int shmr_ec_pool_new(int device, size_t shards_per_block, size_t shard_len, size_t slots_per_slab,
+                     shmr_ec_pool_t** out);
+int shmr_ec_pool_alloc(shmr_ec_pool_t* pool, uint8_t** out_ptrs);
+int shmr_ec_pool_free(shmr_ec_pool_t* pool, uint8_t* first);
+int shmr_ec_pool_destroy(shmr_ec_pool_t* pool);
+int shmr_ec_pool_stats(shmr_ec_pool_t* pool, uint64_t* slabs, uint64_t* slots, uint64_t* in_use);
+
 /* ---- configuration -------------------------------------------------------- */
 
 /* Device used by the host-buffer entry points (default 0; negative ->
@@ -323,7 +395,12 @@ int shmr_ec_set_device(shmr_ec_t* rs, int device);
 /* Tuning knobs (process-wide).
  *
  * Host-path knobs (both flavours; they choose how bytes move, never what
- * the kernels compute): "bounce_kib": pageable single-block calls whose
+ * the kernels compute): "coalesce" (0/1, default 1): shmr_ec_encode /
+ * shmr_ec_reconstruct (and *_start) whose shards all lie in mapped memory go
+ * through the device's submission queue (above), merged with concurrent
+ * calls, instead of one zero-copy launch per call; "coalesce_depth",
+ * "coalesce_target", "coalesce_us", "coalesce_max" (blocks per launch, default
+ * 1024), "coalesce_spin_us" and "coalesce_watch_us": the queue (above).  "bounce_kib": pageable single-block calls whose
  * (k+p) x shard bytes fit in this many KiB go through one mapped bounce
  * buffer and a single zero-copy launch instead of per-shard DMA copies
  * (default 8192; 0 disables).  "mirror_zc" (0/1, default 1): pageable host

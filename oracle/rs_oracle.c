@@ -231,6 +231,15 @@ int oracle_reconstruct(uint32_t k, uint32_t p, uint8_t* const* shards, const uin
     return reconstruct_impl(0, k, p, shards, present, len, data_only);
 }
 
+/* The same with the encode loop's variant (1: the crate's x86 simd_c nibble
+ * loop, AVX2): the CPU baseline's reconstruct (tools/ref_cpu_vfs.cpp). */
+int oracle_reconstruct_v(int variant, uint32_t k, uint32_t p, uint8_t* const* shards, const uint8_t* present,
+                         size_t len, int data_only) {
+    tables();
+    if (variant == 1 && !have_avx2()) variant = 0;
+    return reconstruct_impl(variant, k, p, shards, present, len, data_only);
+}
+
 /* The crate's reconstruct (galois_8 ReedSolomon::reconstruct_internal): the
  * first k present shards in index order, decode matrix = inv(M[valid]),
  * absent data rows rebuilt with the SIMD mul_slice loop, absent parity

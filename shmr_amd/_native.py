@@ -90,6 +90,22 @@ SIGNATURES = [
     ("shmr_ec_reconstruct_start", ctypes.c_int,
      [ctypes.c_void_p, _u8pp, ctypes.POINTER(_sz), _u8p, _sz, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     ("shmr_ec_op_wait", ctypes.c_int, [ctypes.c_void_p]),
+    ("shmr_ec_encode_dev", ctypes.c_int, [ctypes.c_void_p, _u8pp, ctypes.POINTER(_sz), _sz, ctypes.c_int]),
+    ("shmr_ec_reconstruct_dev", ctypes.c_int,
+     [ctypes.c_void_p, _u8pp, ctypes.POINTER(_sz), _u8p, _sz, ctypes.c_int, ctypes.c_int]),
+    ("shmr_ec_encode_dev_start", ctypes.c_int,
+     [ctypes.c_void_p, _u8pp, ctypes.POINTER(_sz), _sz, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    ("shmr_ec_reconstruct_dev_start", ctypes.c_int,
+     [ctypes.c_void_p, _u8pp, ctypes.POINTER(_sz), _u8p, _sz, ctypes.c_int, ctypes.c_int,
+      ctypes.POINTER(ctypes.c_void_p)]),
+    ("shmr_ec_queue_stats", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), _sz]),
+    ("shmr_ec_pool_new", ctypes.c_int, [ctypes.c_int, _sz, _sz, _sz, ctypes.POINTER(ctypes.c_void_p)]),
+    ("shmr_ec_pool_alloc", ctypes.c_int, [ctypes.c_void_p, _u8pp]),
+    ("shmr_ec_pool_free", ctypes.c_int, [ctypes.c_void_p, _u8p]),
+    ("shmr_ec_pool_destroy", ctypes.c_int, [ctypes.c_void_p]),
+    ("shmr_ec_pool_stats", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+      ctypes.POINTER(ctypes.c_uint64)]),
 ]
 
 

@@ -13,13 +13,14 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <vector>
 
 #include "ec_core.hpp"
 #include "host_engine.hpp"
-#include "ptr_grid.hpp"
+#include "submit.hpp"
 
 using shmr::core::Codec;
 using shmr::core::Plan;
@@ -40,76 +41,6 @@ int guarded(F&& f) noexcept {
         return SHMR_EC_DEVICE_ERROR;
     }
 }
-// ---- slot grids in shard-pointer tables -----------------------------------------
-// A *_ptrs_dev table whose shards sit on a grid -- entry (b, j) at base +
-// b * block_pitch + j * shard_pitch, as the buffers of a Block-Cache slab do
-// (shmr_ec_device_alloc_shards, or any [blocks][shards][pitch] array) -- names
-// exactly the addresses the strided kernels of the *_batch_dev calls compute
-// from (base, pitches): those run instead, with no table to upload or chase
-// (the table kernels' first loads wait on a scalar load of the block's table
-// row).  The fit is checked against every entry, so the
-// kernels touch the same bytes either way.
-using GridEntry = shmr::grid::Entry;
-using shmr::grid::Grid;
-using shmr::grid::fit_grid;
-uint8_t* grid_ptr(const Grid& g) { return reinterpret_cast<uint8_t*>(uintptr_t(g.base)); }
-
-// The strided equivalent of a pointer-table call, if its table is a grid:
-// *handled = true and the status of the strided call; else nothing enqueued.
-int ptrs_as_grid(Codec& c, uint8_t* const* tab, const uint8_t* present, size_t nblocks, size_t len, bool data_only,
-                 int device, hipStream_t stream, core::OpClass op, bool* handled) {
-    *handled = false;
-    const unsigned k = c.k(), t = k + c.p();
-    auto addr = [&](size_t b, unsigned i) { return uint64_t(uintptr_t(tab[b * t + i])); };
-    std::vector<GridEntry> in, out;
-    in.reserve(nblocks * k);
-    out.reserve(nblocks * (t - k));
-    Grid gi, go;
-    if (op == core::kEncode) {
-        for (size_t b = 0; b < nblocks; ++b)
-            for (unsigned i = 0; i < t; ++i) (i < k ? in : out).push_back({b, i < k ? i : i - k, addr(b, i)});
-        if (!fit_grid(in, &gi) || !fit_grid(out, &go)) return SHMR_EC_OK;
-        *handled = true;
-        core::count_device(device, core::kDevPtrTableGrids);
-        const core::Layout L{grid_ptr(gi), grid_ptr(go), uint64_t(gi.bpitch), uint64_t(gi.spitch),
-                             uint64_t(go.bpitch), uint64_t(go.spitch), k};
-        return core::encode_on_device(c, device, L, nblocks, len, stream);
-    }
-    // reconstruct: every shard the call touches on one grid -> in place
-    std::vector<GridEntry> all;
-    all.reserve(nblocks * t);
-    for (size_t b = 0; b < nblocks; ++b) {
-        const uint8_t* pr = present + b * t;
-        unsigned np = 0;
-        for (unsigned i = 0; i < t; ++i) np += pr[i] ? 1 : 0;
-        unsigned j = 0;
-        for (unsigned i = 0; i < t; ++i) {
-            if (pr[i]) {
-                in.push_back({b, i, addr(b, i)});
-                all.push_back({b, i, addr(b, i)});
-            } else if (np != t && (i < k || !data_only)) {   // written
-                out.push_back({b, j++, addr(b, i)});
-                all.push_back({b, i, addr(b, i)});
-            }
-        }
-    }
-    Grid ga;
-    if (fit_grid(all, &ga)) {
-        *handled = true;
-        core::count_device(device, core::kDevPtrTableGrids);
-        return core::reconstruct_on_device(c, device, grid_ptr(ga), uint64_t(ga.spitch), uint64_t(ga.bpitch), present,
-                                           nblocks, len, data_only, stream);
-    }
-    // present shards on one grid, rebuilt shards on another -> compact output
-    if (!fit_grid(in, &gi) || !fit_grid(out, &go)) return SHMR_EC_OK;
-    *handled = true;
-    core::count_device(device, core::kDevPtrTableGrids);
-    core::Layout L{grid_ptr(gi), grid_ptr(go), uint64_t(gi.bpitch), uint64_t(gi.spitch),
-                   uint64_t(go.bpitch), uint64_t(go.spitch), 0};
-    L.compact = true;
-    return core::reconstruct_on_device(c, device, L, present, nblocks, len, data_only, stream);
-}
-
 // Slabs handed out by shmr_ec_device_alloc_shards (base -> device).
 std::mutex g_slab_mu;
 std::map<uintptr_t, int> g_slabs;
@@ -235,10 +166,26 @@ int shmr_ec_set_device(shmr_ec_t* rs, int device) {
 }
 
 int shmr_ec_set_tuning(const char* key, int value) {
-    return guarded([&] { return core::set_tuning(key, value); });
+    return guarded([&]() -> int {
+        if (!key) return SHMR_EC_INVALID_ARGUMENT;
+        bool known = false;
+        const int rc = core::set_submit_tuning(key, value, &known);
+        return known ? rc : core::set_tuning(key, value);
+    });
 }
 int shmr_ec_get_tuning(const char* key) {
-    return guarded([&] { return core::get_tuning(key); });
+    return guarded([&]() -> int {
+        if (!key) return SHMR_EC_INVALID_ARGUMENT;
+        bool known = false;
+        const int v = core::get_submit_tuning(key, &known);
+        return known ? v : core::get_tuning(key);
+    });
+}
+
+int shmr_ec_queue_stats(int device, uint64_t* out, size_t n) {
+    if (!out || device < 0) return SHMR_EC_INVALID_ARGUMENT;
+    core::submit_stats(device, out, n);
+    return SHMR_EC_OK;
 }
 
 int shmr_ec_describe_variant(int decode, uint32_t data_shards, uint32_t rows, char* buf, size_t len) {
@@ -472,27 +419,114 @@ int shmr_ec_host_unregister(void* p) {
     });
 }
 
+}  // extern "C"
+
+// ---- validation in the crate's order (shared by host and device forms) -------------
+namespace {
+// ReedSolomon::encode: check_piece_count!(all), then check_slices!(multi).
+int check_encode(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_lens, size_t nshards, size_t* len) {
+    if (!rs || !shards || !shard_lens) return SHMR_EC_INVALID_ARGUMENT;
+    const unsigned t = rs->codec->k() + rs->codec->p();
+    if (nshards < t) return SHMR_EC_TOO_FEW_SHARDS;
+    if (nshards > t) return SHMR_EC_TOO_MANY_SHARDS;
+    *len = shard_lens[0];
+    if (*len == 0) return SHMR_EC_EMPTY_SHARD;
+    for (unsigned i = 0; i < t; ++i)
+        if (shard_lens[i] != *len) return SHMR_EC_INCORRECT_SHARD_SIZE;
+    for (unsigned i = 0; i < t; ++i)
+        if (!shards[i]) return SHMR_EC_INVALID_ARGUMENT;
+    return SHMR_EC_OK;
+}
+
+// ReedSolomon::reconstruct{,_data}: per present shard len 0 -> EmptyShard,
+// mismatch -> IncorrectShardSize, in index order; then the presence count.
+// *plan = nullptr: every shard present (the crate returns Ok without work).
+int check_reconstruct(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_lens, const uint8_t* present,
+                      size_t nshards, int data_only, size_t* len, std::shared_ptr<Plan>* plan) {
+    if (!rs || !shards || !shard_lens || !present) return SHMR_EC_INVALID_ARGUMENT;
+    Codec& c = *rs->codec;
+    const unsigned k = c.k(), t = k + c.p();
+    if (nshards < t) return SHMR_EC_TOO_FEW_SHARDS;
+    if (nshards > t) return SHMR_EC_TOO_MANY_SHARDS;
+    unsigned np = 0;
+    bool have_len = false;
+    *len = 0;
+    for (unsigned i = 0; i < t; ++i) {
+        if (!present[i]) continue;
+        if (shard_lens[i] == 0) return SHMR_EC_EMPTY_SHARD;
+        ++np;
+        if (have_len && shard_lens[i] != *len) return SHMR_EC_INCORRECT_SHARD_SIZE;
+        *len = shard_lens[i];
+        have_len = true;
+    }
+    plan->reset();
+    if (np == t) return SHMR_EC_OK;
+    if (np < k) return SHMR_EC_TOO_FEW_SHARDS_PRESENT;
+    std::vector<uint8_t> pr(present, present + t);
+    auto pl = c.reconstruct_plan(pr, data_only != 0);
+    for (unsigned m = 0; m < pl->m; ++m)
+        if (!shards[pl->out_idx[m]]) return SHMR_EC_INVALID_ARGUMENT;
+    for (unsigned i = 0; i < k; ++i)
+        if (!shards[pl->in_idx[i]]) return SHMR_EC_INVALID_ARGUMENT;
+    if (pl->m) *plan = pl;
+    return SHMR_EC_OK;
+}
+
+// A queue request for one validated block (row: device addresses, shard
+// index order, 0 where the call touches nothing).
+std::unique_ptr<core::SubmitReq> make_req(shmr_ec_t* rs, core::OpClass op, bool data_only, bool host_mapped,
+                                          size_t len, int dev, std::vector<uint64_t> row, const uint8_t* present) {
+    std::unique_ptr<core::SubmitReq> r(new core::SubmitReq);
+    r->codec = rs->codec;
+    r->op = op;
+    r->data_only = data_only;
+    r->host_mapped = host_mapped;
+    r->len = len;
+    r->dev = dev;
+    r->row = std::move(row);
+    if (present) r->present.assign(present, present + r->row.size());
+    return r;
+}
+
+// Submits r; with `queued` (a *_start call) hands it over pending, else waits.
+int run_req(std::unique_ptr<core::SubmitReq> r, core::SubmitReq** queued) {
+    const int rc = core::submit(r.get());
+    if (rc) return rc;
+    if (queued) {
+        *queued = r.release();
+        return SHMR_EC_OK;
+    }
+    return core::wait(r.get());
+}
+}  // namespace
+
+extern "C" {
+
 // ---- host-buffer encode (ReedSolomon::encode) --------------------------------------
 // async != nullptr (shmr_ec_encode_start): shards in mapped memory are coded by
-// kernels left running on *async's stream; every other path finishes here.
+// kernels left running (a pooled stream in *async, or -- through the
+// submission queue, knob "coalesce" -- a request in *queued); every other path
+// finishes here.
 static int encode_impl(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_lens, size_t nshards,
-                       core::Staging** async) {
+                       core::Staging** async, core::SubmitReq** queued) {
     return guarded([&]() -> int {
-        if (!rs || !shards || !shard_lens) return SHMR_EC_INVALID_ARGUMENT;
+        size_t len = 0;
+        int rc = check_encode(rs, shards, shard_lens, nshards, &len);
+        if (rc) return rc;
         Codec& c = *rs->codec;
         const unsigned k = c.k(), p = c.p(), t = k + p;
-        // crate check_piece_count!(all) then check_slices!(multi)
-        if (nshards < t) return SHMR_EC_TOO_FEW_SHARDS;
-        if (nshards > t) return SHMR_EC_TOO_MANY_SHARDS;
-        const size_t len = shard_lens[0];
-        if (len == 0) return SHMR_EC_EMPTY_SHARD;
-        for (unsigned i = 0; i < t; ++i)
-            if (shard_lens[i] != len) return SHMR_EC_INCORRECT_SHARD_SIZE;
-        for (unsigned i = 0; i < t; ++i)
-            if (!shards[i]) return SHMR_EC_INVALID_ARGUMENT;
         const int dev = rs->device;
-        int rc = core::check_device(dev);
+        rc = core::check_device(dev);
         if (rc) return rc;
+        if (core::coalesce_host()) {   // mapped shards: merged with concurrent calls, coded in place
+            const core::HostJob job{c, core::kEncode, false, shards, nullptr, 1, len, 0, 1};
+            std::vector<uint64_t> row;
+            if (core::map_rows(job, &row)) {
+                core::count_blocks(true, 1);
+                return run_req(make_req(rs, core::kEncode, false, true, len, dev, std::move(row), nullptr),
+                               async ? queued : nullptr);
+            }
+        }
         {   // shards in mapped memory: the kernel encodes them in place (zero-copy)
             const core::HostJob job{c, core::kEncode, false, shards, nullptr, 1, len, 0, 1};
             bool handled = false;
@@ -525,38 +559,26 @@ static int encode_impl(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shar
 
 // ---- host-buffer reconstruct (ReedSolomon::reconstruct{,_data}) ---------------------
 static int reconstruct_impl(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_lens, const uint8_t* present,
-                            size_t nshards, int data_only, core::Staging** async) {
+                            size_t nshards, int data_only, core::Staging** async, core::SubmitReq** queued) {
     return guarded([&]() -> int {
-        if (!rs || !shards || !shard_lens || !present) return SHMR_EC_INVALID_ARGUMENT;
-        Codec& c = *rs->codec;
-        const unsigned k = c.k(), p = c.p(), t = k + p;
-        if (nshards < t) return SHMR_EC_TOO_FEW_SHARDS;
-        if (nshards > t) return SHMR_EC_TOO_MANY_SHARDS;
-        // crate reconstruct_internal: per present shard, len 0 -> EmptyShard,
-        // mismatch -> IncorrectShardSize, in index order.
-        unsigned np = 0;
         size_t len = 0;
-        bool have_len = false;
-        for (unsigned i = 0; i < t; ++i) {
-            if (!present[i]) continue;
-            if (shard_lens[i] == 0) return SHMR_EC_EMPTY_SHARD;
-            ++np;
-            if (have_len && shard_lens[i] != len) return SHMR_EC_INCORRECT_SHARD_SIZE;
-            len = shard_lens[i];
-            have_len = true;
-        }
-        if (np == t) return SHMR_EC_OK;
-        if (np < k) return SHMR_EC_TOO_FEW_SHARDS_PRESENT;
-        std::vector<uint8_t> pr(present, present + t);
-        auto plan = c.reconstruct_plan(pr, data_only != 0);
-        for (unsigned m = 0; m < plan->m; ++m)
-            if (!shards[plan->out_idx[m]]) return SHMR_EC_INVALID_ARGUMENT;
-        for (unsigned i = 0; i < k; ++i)
-            if (!shards[plan->in_idx[i]]) return SHMR_EC_INVALID_ARGUMENT;
-        if (plan->m == 0) return SHMR_EC_OK;
+        std::shared_ptr<Plan> plan;
+        int rc = check_reconstruct(rs, shards, shard_lens, present, nshards, data_only, &len, &plan);
+        if (rc || !plan) return rc;
+        Codec& c = *rs->codec;
+        const unsigned k = c.k(), t = k + c.p();
         const int dev = rs->device;
-        int rc = core::check_device(dev);
+        rc = core::check_device(dev);
         if (rc) return rc;
+        if (core::coalesce_host()) {   // mapped shards: merged with concurrent calls, rebuilt in place
+            const core::HostJob job{c, core::kDecode, data_only != 0, shards, present, 1, len, 0, 1};
+            std::vector<uint64_t> row;
+            if (core::map_rows(job, &row)) {
+                core::count_blocks(true, 1);
+                return run_req(make_req(rs, core::kDecode, data_only != 0, true, len, dev, std::move(row), present),
+                               async ? queued : nullptr);
+            }
+        }
         {   // shards in mapped memory: rebuilt in place by the kernel (zero-copy)
             const core::HostJob job{c, core::kDecode, data_only != 0, shards, present, 1, len, 0, 1};
             bool handled = false;
@@ -590,33 +612,85 @@ static int reconstruct_impl(shmr_ec_t* rs, uint8_t* const* shards, const size_t*
     });
 }
 
+// ---- one block on device buffers, through the submission queue -----------------
+// The crate's encode / reconstruct of ONE block (block.rs:427, :560) whose
+// shards are device buffers; concurrent calls on the device merge into batch
+// launches (submit.hpp).
+static int encode_dev_impl(shmr_ec_t* rs, uint8_t* const* d_shards, const size_t* shard_lens, size_t nshards,
+                           int device, core::SubmitReq** queued) {
+    return guarded([&]() -> int {
+        size_t len = 0;
+        int rc = check_encode(rs, d_shards, shard_lens, nshards, &len);
+        if (rc) return rc;
+        if ((rc = core::check_device(device))) return rc;
+        std::vector<uint64_t> row(nshards);
+        for (size_t i = 0; i < nshards; ++i) row[i] = uint64_t(uintptr_t(d_shards[i]));
+        return run_req(make_req(rs, core::kEncode, false, false, len, device, std::move(row), nullptr), queued);
+    });
+}
+
+static int reconstruct_dev_impl(shmr_ec_t* rs, uint8_t* const* d_shards, const size_t* shard_lens,
+                                const uint8_t* present, size_t nshards, int data_only, int device,
+                                core::SubmitReq** queued) {
+    return guarded([&]() -> int {
+        size_t len = 0;
+        std::shared_ptr<Plan> plan;
+        int rc = check_reconstruct(rs, d_shards, shard_lens, present, nshards, data_only, &len, &plan);
+        if (rc || !plan) return rc;
+        if ((rc = core::check_device(device))) return rc;
+        std::vector<uint64_t> row(nshards, 0);
+        for (unsigned i = 0; i < plan->k; ++i) row[plan->in_idx[i]] = uint64_t(uintptr_t(d_shards[plan->in_idx[i]]));
+        for (unsigned m = 0; m < plan->m; ++m) row[plan->out_idx[m]] = uint64_t(uintptr_t(d_shards[plan->out_idx[m]]));
+        return run_req(make_req(rs, core::kDecode, data_only != 0, false, len, device, std::move(row), present), queued);
+    });
+}
+
 int shmr_ec_encode(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_lens, size_t nshards) {
-    return encode_impl(rs, shards, shard_lens, nshards, nullptr);
+    return encode_impl(rs, shards, shard_lens, nshards, nullptr, nullptr);
 }
 
 int shmr_ec_reconstruct(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_lens, const uint8_t* present,
                         size_t nshards, int data_only) {
-    return reconstruct_impl(rs, shards, shard_lens, present, nshards, data_only, nullptr);
+    return reconstruct_impl(rs, shards, shard_lens, present, nshards, data_only, nullptr, nullptr);
+}
+
+int shmr_ec_encode_dev(shmr_ec_t* rs, uint8_t* const* d_shards, const size_t* shard_lens, size_t nshards,
+                       int device) {
+    return encode_dev_impl(rs, d_shards, shard_lens, nshards, device, nullptr);
+}
+
+int shmr_ec_reconstruct_dev(shmr_ec_t* rs, uint8_t* const* d_shards, const size_t* shard_lens, const uint8_t* present,
+                            size_t nshards, int data_only, int device) {
+    return reconstruct_dev_impl(rs, d_shards, shard_lens, present, nshards, data_only, device, nullptr);
 }
 
 // ---- asynchronous single-block calls -----------------------------------------------
 struct shmr_ec_op {
-    core::Staging* s = nullptr;   // pending zero-copy kernels' stream, or none
+    core::Staging* s = nullptr;     // pending zero-copy kernels' stream, or none
+    core::SubmitReq* req = nullptr; // or a request of the submission queue
 };
 
-static int start_op(int rc, core::Staging* s, shmr_ec_op_t** op) {
-    if (rc != SHMR_EC_OK) {
+static int start_op(int rc, core::Staging* s, core::SubmitReq* req, shmr_ec_op_t** op) {
+    auto drop = [&] {
         if (s) (void)core::finish_async(s);
+        if (req) {
+            (void)core::wait(req);
+            delete req;
+        }
+    };
+    if (rc != SHMR_EC_OK) {
+        drop();
         return rc;
     }
     return guarded([&]() -> int {
         try {
             *op = new shmr_ec_op;
         } catch (...) {
-            if (s) (void)core::finish_async(s);
+            drop();
             throw;
         }
         (*op)->s = s;
+        (*op)->req = req;
         return SHMR_EC_OK;
     });
 }
@@ -626,8 +700,9 @@ int shmr_ec_encode_start(shmr_ec_t* rs, uint8_t* const* shards, const size_t* sh
     if (!op) return SHMR_EC_INVALID_ARGUMENT;
     *op = nullptr;
     core::Staging* s = nullptr;
-    const int rc = encode_impl(rs, shards, shard_lens, nshards, &s);
-    return start_op(rc, s, op);
+    core::SubmitReq* q = nullptr;
+    const int rc = encode_impl(rs, shards, shard_lens, nshards, &s, &q);
+    return start_op(rc, s, q, op);
 }
 
 int shmr_ec_reconstruct_start(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard_lens, const uint8_t* present,
@@ -635,13 +710,38 @@ int shmr_ec_reconstruct_start(shmr_ec_t* rs, uint8_t* const* shards, const size_
     if (!op) return SHMR_EC_INVALID_ARGUMENT;
     *op = nullptr;
     core::Staging* s = nullptr;
-    const int rc = reconstruct_impl(rs, shards, shard_lens, present, nshards, data_only, &s);
-    return start_op(rc, s, op);
+    core::SubmitReq* q = nullptr;
+    const int rc = reconstruct_impl(rs, shards, shard_lens, present, nshards, data_only, &s, &q);
+    return start_op(rc, s, q, op);
+}
+
+int shmr_ec_encode_dev_start(shmr_ec_t* rs, uint8_t* const* d_shards, const size_t* shard_lens, size_t nshards,
+                             int device, shmr_ec_op_t** op) {
+    if (!op) return SHMR_EC_INVALID_ARGUMENT;
+    *op = nullptr;
+    core::SubmitReq* q = nullptr;
+    const int rc = encode_dev_impl(rs, d_shards, shard_lens, nshards, device, &q);
+    return start_op(rc, nullptr, q, op);
+}
+
+int shmr_ec_reconstruct_dev_start(shmr_ec_t* rs, uint8_t* const* d_shards, const size_t* shard_lens,
+                                  const uint8_t* present, size_t nshards, int data_only, int device,
+                                  shmr_ec_op_t** op) {
+    if (!op) return SHMR_EC_INVALID_ARGUMENT;
+    *op = nullptr;
+    core::SubmitReq* q = nullptr;
+    const int rc = reconstruct_dev_impl(rs, d_shards, shard_lens, present, nshards, data_only, device, &q);
+    return start_op(rc, nullptr, q, op);
 }
 
 int shmr_ec_op_wait(shmr_ec_op_t* op) {
     if (!op) return SHMR_EC_INVALID_ARGUMENT;
-    const int rc = op->s ? guarded([&] { return core::finish_async(op->s); }) : SHMR_EC_OK;
+    int rc = SHMR_EC_OK;
+    if (op->s) rc = guarded([&] { return core::finish_async(op->s); });
+    if (op->req) {
+        rc = guarded([&] { return core::wait(op->req); });
+        delete op->req;
+    }
     delete op;
     return rc;
 }
@@ -711,11 +811,10 @@ int shmr_ec_reconstruct_batch_dev_out(shmr_ec_t* rs, const uint8_t* d_shards, si
 
 // ---- device-resident shards anywhere: shard-pointer tables --------------------------
 // The crate's own shape (block.rs:408-427: every shard its own Vec<u8>; :556-565:
-// every None shard rebuilt into a fresh buffer) on device memory.  The host
-// table d_shards[b * total + i] goes up on the caller's stream into the
-// device's pointer-table cache (a table the stream passed before is reused
-// without an upload; a busy cache falls back to the pointer ring); inside a
-// capture it goes to permanent arena memory, which every replay re-reads.
+// every None shard rebuilt into a fresh buffer) on device memory: validation
+// here, dispatch in core::ptrs_launch (a slot lattice -> the strided kernels over
+// its slots; else the table, from the device's table cache or uploaded on the
+// caller's stream; inside a capture into the capture reserve).
 static int ptrs_dev(shmr_ec_t* rs, uint8_t* const* d_shards, const uint8_t* present, size_t nblocks,
                     size_t shard_len, int data_only, int device, void* stream_, core::OpClass op) {
     return guarded([&]() -> int {
@@ -727,95 +826,19 @@ static int ptrs_dev(shmr_ec_t* rs, uint8_t* const* d_shards, const uint8_t* pres
         const unsigned k = c.k(), t = k + c.p();
         int rc = SHMR_EC_OK;
         if (op == core::kDecode && (rc = core::validate_presence(c, present, nblocks))) return rc;
-        bool aligned = true;   // every shard the launch touches 16-byte aligned
         for (size_t b = 0; b < nblocks; ++b)
             for (unsigned i = 0; i < t; ++i) {
-                const uint8_t* p = d_shards[b * t + i];
                 // absent parity under data_only is neither read nor written
                 const bool needed = op == core::kEncode || present[b * t + i] || i < k || !data_only;
-                if (!p) {
-                    if (needed) return SHMR_EC_INVALID_ARGUMENT;
-                    continue;
-                }
-                aligned = aligned && (uintptr_t(p) & 15u) == 0;
+                if (needed && !d_shards[b * t + i]) return SHMR_EC_INVALID_ARGUMENT;
             }
         rc = core::check_device(device);
         if (rc) return rc;
         core::DeviceScope scope(device);
         if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
-        const hipStream_t stream = static_cast<hipStream_t>(stream_);
-        if (core::ptrs_grid()) {
-            bool handled = false;
-            rc = ptrs_as_grid(c, d_shards, present, nblocks, shard_len, data_only != 0, device, stream, op, &handled);
-            if (handled || rc) return rc;
-        }
-        rc = core::device_init(device, stream);
-        if (rc) return rc;
-        // The kernels read each block's row in plan order (input t at [t],
-        // output r at [k + r]): a reconstruct's rows are permuted here, once per
-        // call, so no shard address in the kernel waits on a plan index load.
-        // An encode table is already in plan order.
-        const uint64_t* table = reinterpret_cast<const uint64_t*>(d_shards);
-        std::vector<uint64_t> permuted;
-        if (op == core::kDecode) {
-            permuted.resize(nblocks * t);
-            core::permute_ptr_rows(table, present, nblocks, k, t, data_only != 0, permuted.data());
-            table = permuted.data();
-        }
-        auto run = [&](const uint8_t* d_tab, size_t b0, size_t n) -> int {
-            core::Layout L{nullptr, nullptr, 0, 0, 0, 0, 0};
-            L.d_ptrs = reinterpret_cast<const uint64_t*>(d_tab);
-            L.total = t;
-            L.ptrs_aligned = aligned;
-            if (op == core::kEncode) return core::encode_on_device(c, device, L, n, shard_len, stream);
-            return core::reconstruct_on_device(c, device, L, present + b0 * t, n, shard_len, data_only != 0, stream);
-        };
         static_assert(sizeof(uint8_t*) == sizeof(uint64_t), "64-bit device pointers");
-        bool capturing = false;
-        if ((rc = core::capture_state(stream, &capturing))) return rc;
-        if (capturing) {   // a block of the capture reserve, returned when the graph is destroyed
-            const size_t bytes = nblocks * t * sizeof(uint64_t);
-            uint8_t *h = nullptr, *d = nullptr;
-            rc = core::capture_alloc(device, stream, bytes, &h, &d);
-            if (rc) return rc;
-            std::memcpy(h, table, bytes);
-            if (hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream) != hipSuccess) {
-                (void)hipGetLastError();
-                return SHMR_EC_DEVICE_ERROR;
-            }
-            return run(d, 0, nblocks);
-        }
-        core::PtrTableCache* cache = core::PtrTableCache::for_device(device, &rc);
-        if (!cache) return rc;
-        core::UploadRing* ring = nullptr;
-        const size_t per_chunk = core::UploadRing::kSlotBytes / (sizeof(uint64_t) * t);
-        for (size_t b0 = 0; b0 < nblocks; b0 += per_chunk) {
-            const size_t n = std::min(per_chunk, nblocks - b0);
-            // a table this stream passed before (same bytes): its device copy, no upload
-            const uint8_t* dtab = nullptr;
-            int entry = -1;
-            rc = cache->lookup(table + b0 * t, n * t * sizeof(uint64_t), stream, &dtab, &entry);
-            if (rc) return rc;
-            if (dtab) {
-                rc = run(dtab, b0, n);
-                const int rc2 = cache->release_after(entry, stream);
-                if (rc) return rc;
-                if (rc2) return rc2;
-                continue;
-            }
-            if (!ring && !(ring = core::UploadRing::for_device(device, &rc, core::UploadRing::kPointers))) return rc;
-            uint8_t *hslot = nullptr, *dslot = nullptr;
-            int slot = -1;
-            rc = ring->acquire(&hslot, &dslot, &slot);
-            if (rc) return rc;
-            std::memcpy(hslot, table + b0 * t, n * t * sizeof(uint64_t));
-            rc = ring->upload(slot, n * t * sizeof(uint64_t), stream);
-            if (rc == SHMR_EC_OK) rc = run(dslot, b0, n);
-            const int rc2 = ring->release_after(slot, stream);
-            if (rc) return rc;
-            if (rc2) return rc2;
-        }
-        return SHMR_EC_OK;
+        return core::ptrs_launch(c, reinterpret_cast<const uint64_t*>(d_shards), present, nblocks, shard_len,
+                                 data_only != 0, device, static_cast<hipStream_t>(stream_), op, false, true);
     });
 }
 

@@ -63,6 +63,14 @@ std::atomic<int> g_ptrs_grid{1};
 // fallback kernels of the product library this way), 1 = always modes 0 / 1
 // (tools build only: wrong on a device without the unaligned mode).
 std::atomic<int> g_uvec{kAuto};
+// Slot lists (launch_slots): 1 = always the uploaded block list, even for one
+// arithmetic run or segment runs (tools build only: measures the list's cost)
+std::atomic<int> g_slots_list{0};
+// Reconstructs whose patterns' blocks fit no 32 segment runs: 0 = one multi-plan
+// launch set (block list + per-block plan index uploaded: each workgroup's plan
+// is two dependent loads away), 1 = one single-plan launch set per pattern over
+// its blocks (launch_slots: a run, segment runs or a block list)
+std::atomic<int> g_pattern_launches{0};
 
 // The launch policy itself is kern::policy_variant (gf_apply.hpp): constexpr,
 // so the product library compiles exactly the kernels it can select.  Its
@@ -149,6 +157,20 @@ int set_tuning(const char* key, int value) {
 #endif
         g_uvec = value;
         return SHMR_EC_OK;
+    }
+    if (k == "pattern_launches") {   // not per op class
+        g_pattern_launches = value == kAuto ? 0 : (value != 0);
+        return SHMR_EC_OK;
+    }
+    if (k == "slots_list") {   // not per op class; tools build only
+        const int v = value == kAuto ? 0 : value;
+#ifdef SHMR_EC_TOOLS
+        if (v != 0 && v != 1) return SHMR_EC_INVALID_ARGUMENT;
+        g_slots_list = v;
+        return SHMR_EC_OK;
+#else
+        return v == 0 ? SHMR_EC_OK : SHMR_EC_INVALID_ARGUMENT;
+#endif
     }
     if (k == "alias_devices") {   // not per op class; tools build only (see ec_core.hpp)
         const int v = value == kAuto ? 0 : value;
@@ -246,6 +268,8 @@ int get_tuning(const char* key) {
     if (k == "ptrs_direct") return g_ptrs_direct;
     if (k == "sync_spin_us") return g_sync_spin;
     if (k == "alias_devices") return g_alias_devices;
+    if (k == "slots_list") return g_slots_list;
+    if (k == "pattern_launches") return g_pattern_launches;
     if (k == "uvec") return g_uvec;
     if (k == "chunks") return T.u;
     if (k == "nt_load") return T.nt_load;
@@ -320,7 +344,7 @@ kern::LaunchShape shape_of(OpClass op, unsigned k, unsigned rows, bool host_mapp
     s.rows = rows;
     s.host_mapped = host_mapped;
     s.ptrs = ptrs;
-    s.segs = segs && s.decode;
+    s.segs = segs && (s.decode || (!ptrs && !host_mapped));
     s.compact = compact && s.decode && !ptrs && !host_mapped;
     s.sc1_ok = sc1_ok && !host_mapped;
     s.fused = fused;
@@ -328,6 +352,7 @@ kern::LaunchShape shape_of(OpClass op, unsigned k, unsigned rows, bool host_mapp
 }
 
 bool segs_supported(OpClass op, unsigned k, bool host_mapped, bool ptrs, bool compact) {
+    if (op == kEncode && (host_mapped || ptrs || compact)) return false;   // device pitch layouts only (shape_valid)
 #ifdef SHMR_EC_TOOLS
     for (unsigned rows = 1; rows <= kern::kMaxRowsPerLaunch; ++rows)
         for (bool sc1_ok : {false, true}) {
@@ -390,8 +415,17 @@ hipError_t sync_stream(hipStream_t stream) {
 // Devices and plans
 // ===========================================================================
 int device_count() {
+    // asked at every compute call (check_device): the count a process sees does
+    // not change once it is known, so it is read from HIP until it is
+    static std::atomic<int> known{-1};
+    const int k = known.load(std::memory_order_relaxed);
+    if (k > 0) return k;
     int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    if (n > 0) known.store(n, std::memory_order_relaxed);
     return n;
 }
 
@@ -983,10 +1017,108 @@ int launch_set(Plan& plan, int dev, const Layout& L, const BlockSet& bs, uint64_
     return SHMR_EC_OK;
 }
 
-int encode_on_device(Codec& c, int dev, const Layout& L, uint64_t nblocks, uint64_t len, hipStream_t stream) {
+namespace {
+// A launch's table in device memory: inside a capture a block of the capture
+// reserve (every replay re-reads it; returned when the graph is destroyed),
+// else a slot of the device's table ring, released behind the launch.
+// fill(host) writes the bytes; launch(device copy) enqueues the kernels.
+template <class Fill, class Launch>
+int with_table(int dev, hipStream_t stream, size_t bytes, Fill fill, Launch launch) {
+    bool capturing = false;
+    int rc = capture_state(stream, &capturing);
+    if (rc) return rc;
+    uint8_t *h = nullptr, *d = nullptr;
+    if (capturing) {
+        rc = capture_alloc(dev, stream, bytes, &h, &d);
+        if (rc) return rc;
+        fill(h);
+        if (hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream) != hipSuccess) {
+            (void)hipGetLastError();
+            return SHMR_EC_DEVICE_ERROR;
+        }
+        return launch(d);
+    }
+    if (bytes > UploadRing::kSlotBytes) return SHMR_EC_INVALID_ARGUMENT;
+    UploadRing* ring = UploadRing::for_device(dev, &rc);
+    if (!ring) return rc;
+    int slot = -1;
+    rc = ring->acquire(&h, &d, &slot);
+    if (rc) return rc;
+    fill(h);
+    rc = ring->upload(slot, bytes, stream);
+    if (rc == SHMR_EC_OK) rc = launch(d);
+    const int rc2 = ring->release_after(slot, stream);
+    return rc ? rc : rc2;
+}
+}  // namespace
+
+int launch_slots(Plan& plan, int dev, const Layout& L, const uint64_t* slots, uint64_t n, uint64_t len,
+                 hipStream_t stream, OpClass op) {
+    if (n == 0) return SHMR_EC_OK;
+    // maximal arithmetic runs of the (ascending) slots
+    std::vector<kern::Seg> segs;
+    bool fits = true;
+    for (uint64_t i = 0; i < n;) {
+        uint64_t e = i + 1;
+        const uint64_t st = e < n ? slots[e] - slots[i] : 1;
+        while (e < n && slots[e] - slots[e - 1] == st) ++e;
+        if (segs.size() == kern::kMaxSegs) {
+            fits = false;
+            break;
+        }
+        kern::Seg sg{};
+        sg.start = uint32_t(i);
+        sg.first = uint32_t(slots[i]);
+        sg.stride = e - i > 1 ? uint32_t(st) : 1u;
+        segs.push_back(sg);
+        i = e;
+    }
+    if (g_slots_list.load(std::memory_order_relaxed)) fits = false;   // (tools: the list, measured)
+    if (fits && segs.size() == 1) {   // one run: the plain strided launch
+        BlockSet bs;
+        bs.first = slots[0];
+        bs.stride = segs[0].stride;
+        bs.n = n;
+        return launch_set(plan, dev, L, bs, len, stream, op);
+    }
+    if (fits && segs_supported(op, plan.k, L.host_mapped, L.d_ptrs != nullptr, L.compact)) {
+        const uint8_t* dp = nullptr;
+        const int rc = plan_on_device(plan, dev, stream, L.compact, &dp);
+        if (rc) return rc;
+        for (auto& sg : segs) sg.plan = dp;
+        BlockSet bs;
+        bs.n = n;
+        bs.segs = segs.data();
+        bs.nseg = uint32_t(segs.size());
+        return launch_set(plan, dev, L, bs, len, stream, op);
+    }
+    // an uploaded block list, a ring slot per chunk
+    const uint64_t per = UploadRing::kSlotBytes / sizeof(uint32_t);
+    for (uint64_t c0 = 0; c0 < n; c0 += per) {
+        const uint64_t cnt = std::min(per, n - c0);
+        const int rc = with_table(
+            dev, stream, size_t(cnt) * sizeof(uint32_t),
+            [&](uint8_t* h) {
+                uint32_t* l = reinterpret_cast<uint32_t*>(h);
+                for (uint64_t j = 0; j < cnt; ++j) l[j] = uint32_t(slots[c0 + j]);
+            },
+            [&](const uint8_t* d) {
+                BlockSet bs;
+                bs.n = cnt;
+                bs.d_list = reinterpret_cast<const uint32_t*>(d);
+                return launch_set(plan, dev, L, bs, len, stream, op);
+            });
+        if (rc) return rc;
+    }
+    return SHMR_EC_OK;
+}
+
+int encode_on_device(Codec& c, int dev, const Layout& L, uint64_t nblocks, uint64_t len, hipStream_t stream,
+                     const uint64_t* slots) {
+    count_device(dev, kDevBlocksEncoded, nblocks);
+    if (slots) return launch_slots(*c.encode_plan(), dev, L, slots, nblocks, len, stream, kEncode);
     BlockSet bs;
     bs.n = nblocks;
-    count_device(dev, kDevBlocksEncoded, nblocks);
     return launch_set(*c.encode_plan(), dev, L, bs, len, stream, kEncode);
 }
 
@@ -1008,7 +1140,7 @@ int reconstruct_on_device(Codec& c, int dev, uint8_t* d_shards, uint64_t shard_p
 }
 
 int reconstruct_on_device(Codec& c, int dev, const Layout& L, const uint8_t* present, uint64_t nblocks, uint64_t len,
-                          bool data_only, hipStream_t stream) {
+                          bool data_only, hipStream_t stream, const uint64_t* slots) {
     const unsigned k = c.k(), t = k + c.p();
     int rc = device_init(dev, stream);
     if (rc) return rc;
@@ -1021,7 +1153,7 @@ int reconstruct_on_device(Codec& c, int dev, const Layout& L, const uint8_t* pre
         if (np < k) return SHMR_EC_TOO_FEW_SHARDS_PRESENT;
         std::vector<uint8_t> key(t);
         for (unsigned i = 0; i < t; ++i) key[i] = pr[i] ? 1 : 0;
-        groups[key].push_back(b);
+        groups[key].push_back(slots ? slots[b] : b);
     }
     if (groups.empty()) return SHMR_EC_OK;
     for (auto& g : groups) count_device(dev, kDevBlocksReconstructed, g.second.size());
@@ -1105,6 +1237,15 @@ int reconstruct_on_device(Codec& c, int dev, const Layout& L, const uint8_t* pre
                 if (rc) return rc;
                 continue;
             }
+        }
+        if (g_pattern_launches.load(std::memory_order_relaxed)) {   // a single-plan launch set per pattern
+            std::vector<std::vector<uint64_t>> per(grp.plans.size());
+            for (size_t i = 0; i < grp.blocks.size(); ++i) per[grp.plan_idx[i]].push_back(grp.blocks[i]);
+            for (size_t pi = 0; pi < per.size(); ++pi) {
+                rc = launch_slots(*grp.plans[pi], dev, L, per[pi].data(), per[pi].size(), len, stream, kDecode);
+                if (rc) return rc;
+            }
+            continue;
         }
         if (grp.plans.size() > 65535) return SHMR_EC_INVALID_ARGUMENT;
         std::vector<const uint8_t*> dplans(grp.plans.size());

@@ -245,7 +245,16 @@ int launch_set(Plan& shape, int dev, const Layout& L, const BlockSet& bs, uint64
                OpClass op);
 
 // Encode nblocks blocks laid out per `L` (plan = the codec's parity rows).
-int encode_on_device(Codec& c, int dev, const Layout& L, uint64_t nblocks, uint64_t len, hipStream_t stream);
+// slots (r06, nullable): batch block j is layout block slots[j] (ascending,
+// distinct, < 2^32) -- a slot lattice (ptr_grid.hpp) of a pool or of merged
+// per-block calls; one arithmetic run is one strided launch, several runs travel
+// in the kernel arguments where the op's segment kernels exist, else an
+// uploaded block list (launch_slots).
+int encode_on_device(Codec& c, int dev, const Layout& L, uint64_t nblocks, uint64_t len, hipStream_t stream,
+                     const uint64_t* slots = nullptr);
+// The blocks slots[0 .. n) (ascending, distinct) of a single-plan launch set.
+int launch_slots(Plan& plan, int dev, const Layout& L, const uint64_t* slots, uint64_t n, uint64_t len,
+                 hipStream_t stream, OpClass op);
 
 // Reconstruct in place: all shards of block b at base + b*block_pitch +
 // i*shard_pitch; present = host flags [nblocks][total].  Validates every block
@@ -255,8 +264,20 @@ int reconstruct_on_device(Codec& c, int dev, uint8_t* d_shards, uint64_t shard_p
                           hipStream_t stream);
 
 // Same over any layout (e.g. a shard-pointer table, or a compact output).
+// slots (r06, nullable): batch block b is layout block slots[b] (ascending,
+// distinct, < 2^32), as encode_on_device.
 int reconstruct_on_device(Codec& c, int dev, const Layout& L, const uint8_t* present, uint64_t nblocks, uint64_t len,
-                          bool data_only, hipStream_t stream);
+                          bool data_only, hipStream_t stream, const uint64_t* slots = nullptr);
+
+// A shard-pointer table call (ptrs.cpp): tab[b * total + i] is the device
+// address of shard i of block b (0 for a shard the call does not touch),
+// validated by the caller.  A table on a slot lattice runs the strided kernels
+// over its slots (*lattice = true; counted as SHMR_EC_DEV_PTR_TABLE_GRIDS),
+// any other the table kernels, its table uploaded on `stream` (use_cache: the
+// device's table cache first; capture reserve inside a capture).  host_mapped:
+// the addresses are mapped host memory (zero-copy across PCIe).
+int ptrs_launch(Codec& c, const uint64_t* tab, const uint8_t* present, size_t nblocks, uint64_t len, bool data_only,
+                int device, hipStream_t stream, OpClass op, bool host_mapped, bool use_cache, bool* lattice = nullptr);
 
 // Validation shared by every reconstruct entry point.
 int validate_presence(const Codec& c, const uint8_t* present, uint64_t nblocks);

@@ -199,6 +199,19 @@ hipError_t probe_unaligned_vector(bool* ok, uint8_t* d_scratch, uint8_t* h_scrat
     return e;
 }
 
+namespace {
+// One lane stores: a vector memory (global) atomic store at system scope, so
+// the host sees it only after every byte the batch's kernels wrote before it.
+__global__ void queue_mark_kernel(uint64_t* word, uint64_t seq) {
+    if (threadIdx.x == 0) __hip_atomic_store(word + threadIdx.x, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+}  // namespace
+
+hipError_t launch_mark(uint64_t* word, uint64_t seq, hipStream_t stream) {
+    hipLaunchKernelGGL(queue_mark_kernel, dim3(1), dim3(64), 0, stream, word, seq);
+    return hipGetLastError();
+}
+
 hipError_t launch_apply(const ApplyArgs& a, unsigned rows, const Variant& v, int mode, int grid_cap,
                         hipStream_t stream) {
     if (rows < 1 || rows > kMaxRowsPerLaunch) return hipErrorInvalidValue;

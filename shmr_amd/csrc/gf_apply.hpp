@@ -175,17 +175,19 @@ struct LaunchShape {
     unsigned rows = 1;         // output rows of the launch, 1 .. kMaxRowsPerLaunch
     bool host_mapped = false;  // shards in mapped host memory (zero-copy across PCIe)
     bool ptrs = false;         // shards named by a pointer table (ApplyArgs::shard_ptrs)
-    bool segs = false;         // segment launch (decode: plans in the kernel arguments)
+    bool segs = false;         // segment launch (block runs, decode: their plans, in the kernel arguments)
     bool compact = false;      // decode into a compact output (shmr_ec_reconstruct_batch_dev_out)
     bool sc1_ok = false;       // outputs in device memory, 16-byte aligned, shorter than 2 GiB - 4 KiB
     bool fused = false;        // the shard length leaves a partial last tile after >= 1 full tile
 };
 
-// The shapes a call can produce: encodes take no segment launch and no compact
-// output; compact outputs are device pitch layouts; sc1 needs device memory.
+// The shapes a call can produce: encodes take no compact output, and segment
+// launches only over device pitch layouts (r06: the slot runs of a pool or of
+// merged per-block calls, launch_slots); compact outputs are device pitch
+// layouts; sc1 needs device memory.
 constexpr bool shape_valid(const LaunchShape& s) {
     if (s.rows < 1 || s.rows > kMaxRowsPerLaunch) return false;
-    if (!s.decode && (s.segs || s.compact)) return false;
+    if (!s.decode && (s.compact || (s.segs && (s.ptrs || s.host_mapped)))) return false;
     if (s.compact && (s.ptrs || s.host_mapped)) return false;
     if (s.sc1_ok && s.host_mapped) return false;
     return true;
@@ -203,7 +205,7 @@ constexpr Variant policy_variant(const LaunchShape& s) {
     v.nt_store = true;
     v.fuse_tail = s.fused;              // partial tiles at the head of the full-tile grid
     v.ptrs = s.ptrs;
-    v.segs = dec && s.segs;
+    v.segs = s.segs;
     // early prologue: encodes with k <= 8 (short workgroups) and 4-row encodes
     // (with the per-dword math order, fewer live VGPRs at U = 2)
     v.early = !dec && (s.small_k || s.rows >= 4) && !hm;
@@ -271,6 +273,12 @@ struct KernelInfo {
     uint64_t launches;
 };
 size_t kernel_inventory(KernelInfo* out, size_t cap);
+
+// The submission queue's completion mark (submit.cpp): a one-wave kernel on
+// `stream` that stores `seq` to `word` -- pinned host memory, a system-scope
+// release store -- once every earlier kernel of the stream has completed, so
+// waiting callers poll a host word instead of the HIP runtime.
+hipError_t launch_mark(uint64_t* word, uint64_t seq, hipStream_t stream);
 
 // Runs a one-wave kernel on `stream` (current device) that loads and stores 16
 // bytes at addresses off 16-byte alignment (plain and nontemporal), waits for

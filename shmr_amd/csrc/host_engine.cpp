@@ -494,6 +494,11 @@ int finish_async(Staging* s) {
     return sync_stream(s->stream) == hipSuccess ? SHMR_EC_OK : SHMR_EC_DEVICE_ERROR;
 }
 
+bool map_rows(const HostJob& job, std::vector<uint64_t>* dptrs) {
+    bool aligned = true;
+    return map_job(job, dptrs, &aligned);
+}
+
 int run_mapped_job(const HostJob& job, const int* devices, int ndev, bool* handled, bool count, Staging** async) {
     *handled = false;
     if (async && ndev != 1) return SHMR_EC_INVALID_ARGUMENT;

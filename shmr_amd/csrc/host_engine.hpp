@@ -3,6 +3,7 @@
 #pragma once
 
 #include <cstdint>
+#include <vector>
 
 #include "ec_core.hpp"
 
@@ -36,6 +37,9 @@ int run_host_job(const HostJob& job, const int* devices, int ndev);
 // releases it (finish_async); nothing is kept when the job is not handled.
 int run_mapped_job(const HostJob& job, const int* devices, int ndev, bool* handled, bool count = true,
                    Staging** async = nullptr);
+// Device addresses of every shard the job touches (0 for the others), if every
+// one of them lies in mapped host memory (the zero-copy precondition).
+bool map_rows(const HostJob& job, std::vector<uint64_t>* dptrs);
 // Waits for an async mapped job's stream and returns it to the pool.
 int finish_async(Staging* s);
 

@@ -111,5 +111,118 @@ inline bool fit_grid(const std::vector<Entry>& e, Grid* g) {
     return true;
 }
 
+// ---- slot lattices (r06) ------------------------------------------------------
+// fit_grid takes a block's position in the table as its index.  A Block Cache
+// that takes and drops blocks one at a time (a slot pool, shmr_ec_pool_*), or a
+// batch merged from concurrent per-block calls, hands over rows in any order
+// and with holes.  The block order of a batch does not change any byte, so a
+// lattice instead FINDS each row's slot: row r's touched entries (j, addr) lie
+// at base + s_r * bpitch + j * spitch, the slots s_r distinct.  The strided
+// kernels then run over the slots (one arithmetic run, segment runs in the
+// kernel arguments, or an uploaded block list: ec_core launch_slots).
+
+struct RowEntry {
+    uint64_t row, j;   // row of the table; shard position within the row
+    uint64_t addr;
+};
+
+// The common shard pitch of the rows and each row's anchor (the address of its
+// j = 0 position): entries grouped by row (ascending), every row 0 .. nrows-1
+// with at least one entry.  The pitch comes from the first row holding two
+// positions (exact, non-negative); rows that never hold two leave it 0 (the
+// kernels then multiply it only by the one position each row touches).
+inline bool row_anchors(const std::vector<RowEntry>& e, size_t nrows, uint64_t* spitch, std::vector<uint64_t>* anchor) {
+    *spitch = 0;
+    anchor->assign(nrows, 0);
+    bool have = false;
+    for (size_t i = 1; i < e.size() && !have; ++i) {
+        if (e[i].row != e[i - 1].row || e[i].j == e[i - 1].j) continue;
+        const __int128 dj = __int128(e[i].j) - __int128(e[i - 1].j);
+        const __int128 da = __int128(e[i].addr) - __int128(e[i - 1].addr);
+        if (da % dj != 0 || da / dj < 0 || da / dj > __int128(UINT64_MAX)) return false;
+        *spitch = uint64_t(da / dj);
+        have = true;
+    }
+    std::vector<bool> seen(nrows, false);
+    for (const RowEntry& x : e) {
+        if (x.row >= nrows) return false;
+        const uint64_t a = x.addr - x.j * *spitch;   // wrapping, as the kernels compute
+        if (!seen[x.row]) {
+            seen[x.row] = true;
+            (*anchor)[x.row] = a;
+        } else if ((*anchor)[x.row] != a) {
+            return false;
+        }
+    }
+    for (bool s : seen)
+        if (!s) return false;
+    return true;
+}
+
+inline uint64_t gcd_u64(uint64_t a, uint64_t b) {
+    while (b) {
+        const uint64_t t = a % b;
+        a = b;
+        b = t;
+    }
+    return a;
+}
+
+// Slots from anchors: base = the lowest anchor, bpitch = the gcd of every
+// anchor's distance from it, slot = distance / bpitch.  Distinct anchors only
+// (two rows on one slot would be one block coded twice); slots < 2^32 (the
+// kernels' block lists and segment runs are 32-bit).
+inline bool fit_slots(const std::vector<uint64_t>& anchor, Grid* g, std::vector<uint64_t>* slot) {
+    const size_t n = anchor.size();
+    *g = Grid{};
+    slot->assign(n, 0);
+    if (n == 0) return false;
+    uint64_t lo = anchor[0];
+    for (uint64_t a : anchor) lo = std::min(lo, a);
+    uint64_t gg = 0;
+    for (uint64_t a : anchor) gg = gcd_u64(gg, a - lo);
+    if (n > 1 && gg == 0) return false;
+    for (size_t r = 0; r < n; ++r) {
+        const uint64_t s = gg ? (anchor[r] - lo) / gg : 0;
+        if (s >> 32) return false;
+        (*slot)[r] = s;
+    }
+    std::vector<uint64_t> sorted(*slot);
+    std::sort(sorted.begin(), sorted.end());
+    for (size_t i = 1; i < n; ++i)
+        if (sorted[i] == sorted[i - 1]) return false;
+    g->base = lo;
+    g->bpitch = gg;
+    return true;
+}
+
+// A second lattice over the SAME slots (an encode's parity rows, a rebuild's
+// compact output): anchor_r = base + slot_r * bpitch for every row, bpitch
+// non-negative (from the lowest and the highest slot, exact), checked for
+// every row in wrapping 64-bit arithmetic.
+inline bool fit_with_slots(const std::vector<uint64_t>& anchor, const std::vector<uint64_t>& slot, Grid* g) {
+    *g = Grid{};
+    const size_t n = anchor.size();
+    if (n == 0 || slot.size() != n) return false;
+    size_t lo = 0, hi = 0;
+    for (size_t r = 1; r < n; ++r) {
+        if (slot[r] < slot[lo]) lo = r;
+        if (slot[r] > slot[hi]) hi = r;
+    }
+    uint64_t bp = 0;
+    if (slot[hi] != slot[lo]) {
+        const __int128 d = __int128(anchor[hi]) - __int128(anchor[lo]);
+        const __int128 ds = __int128(slot[hi]) - __int128(slot[lo]);
+        if (d < 0 || d % ds != 0) return false;
+        bp = uint64_t(d / ds);
+    }
+    const uint64_t base = anchor[lo] - slot[lo] * bp;
+    for (size_t r = 0; r < n; ++r)
+        if (anchor[r] != base + slot[r] * bp) return false;
+    g->base = base;
+    g->bpitch = bp;
+    return true;
+}
+
 }  // namespace grid
 }  // namespace shmr

@@ -1,0 +1,72 @@
+// Submission queue (submit.cpp): per-block calls from concurrent threads merged
+// into batch launches.  Not part of the public interface.
+//
+// The reference codes one block per call from rayon workers
+// (src/vfs/mod.rs:91-97 -> VirtualBlock::sync_data -> ReedSolomon::encode at
+// src/vfs/block.rs:427; load_block -> reconstruct at :560).  One launch per
+// 4 MiB block leaves the GPU launch-bound (a single-block RS(8,3) kernel is
+// ~6 us on the GPU for 0.9 us of HBM work), so per device ID the
+// library keeps one queue: a call whose inputs are ready submits its block's
+// shard row; a launch group is taken whenever fewer than `coalesce_depth`
+// batches are in flight on the queue's stream, so calls that arrive while one
+// is running (or, knob coalesce_us, within a window) merge into the next
+// launch -- every pending request of every codec, grouped per (codec, op,
+// length, data_only, memory kind), each group one pointer-table call (a slot
+// lattice runs the strided kernels, core::ptrs_launch).  Completion is in
+// launch order on the one stream: a mark kernel behind every batch stores its
+// sequence number into a pinned host word, on which the batch's callers spin
+// before they sleep; a watcher thread per queue wakes them and launches the
+// calls held back for merging.
+#pragma once
+
+#include <atomic>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "ec_core.hpp"
+
+namespace shmr {
+namespace core {
+
+struct SubmitReq {
+    std::shared_ptr<Codec> codec;
+    OpClass op = kEncode;
+    bool data_only = false;
+    bool host_mapped = false;       // row addresses are mapped host memory
+    uint64_t len = 0;
+    int dev = 0;
+    std::vector<uint64_t> row;      // total device addresses, shard index order (0: not touched)
+    std::vector<uint8_t> present;   // reconstruct: total flags
+    // completion: the batch's sequence number (its completion mark), set
+    // when the request is launched; done = 1 when its status is final without
+    // a mark (a failed launch)
+    std::atomic<uint64_t> seq{0};
+    std::atomic<int> done{0};
+    int rc = SHMR_EC_OK;
+};
+
+// Queues r (validated by the caller: crate checks, non-NULL touched shards,
+// device ID) on its device's queue; may launch.  On an error nothing is
+// queued.  The caller keeps r alive until wait(r) returns.
+int submit(SubmitReq* r);
+// Waits until r's batch has completed on the GPU; returns r's status.
+int wait(SubmitReq* r);
+
+// Knobs (set_tuning): "coalesce" (0/1: the host-buffer entry points on mapped
+// memory go through the queue), "coalesce_depth" (batches in flight before
+// calls wait to merge), "coalesce_target" (pending calls that launch anyway),
+// "coalesce_us" (window a launch from an idle queue waits for more calls),
+// "coalesce_max" (blocks per launch), "coalesce_spin_us" (a waiter spins on
+// the completion word this long before it sleeps), "coalesce_watch_us" (the
+// watcher spins this long before it blocks on the batch's event).
+bool coalesce_host();
+int set_submit_tuning(const std::string& key, int value, bool* known);
+int get_submit_tuning(const std::string& key, bool* known);
+
+// Queue statistics of a device ID: requests, launches (batches), the largest
+// batch, waits that slept (blocking event sync) -- shmr_ec_queue_stats.
+void submit_stats(int dev, uint64_t* out, size_t n);
+
+}  // namespace core
+}  // namespace shmr

@@ -32,21 +32,32 @@ public:
     ~EcOp() {
         if (op_) (void)shmr_ec_op_wait(op_);
     }
+    // The op's status; a device error of an earlier op that out() had to wait
+    // for is reported here (once) if this op itself succeeded.
     EcStatus wait() {
         shmr_ec_op_t* o = op_;
         op_ = nullptr;
-        return EcStatus{o ? shmr_ec_op_wait(o) : SHMR_EC_OK};
+        int rc = o ? shmr_ec_op_wait(o) : SHMR_EC_OK;
+        if (rc == SHMR_EC_OK) rc = carried_;
+        carried_ = SHMR_EC_OK;
+        return EcStatus{rc};
     }
     // For a *_start call: an op still pending from an earlier start is waited
     // for first (its kernels may still use that call's buffers; handing out
-    // &op_ would make the C call overwrite it with NULL and lose it).
+    // &op_ would make the C call overwrite it with NULL and lose it).  Its
+    // status is kept for the next wait(), not dropped.
     shmr_ec_op_t** out() {
-        if (op_) (void)wait();
+        if (op_) {
+            const int rc = shmr_ec_op_wait(op_);
+            op_ = nullptr;
+            if (carried_ == SHMR_EC_OK) carried_ = rc;
+        }
         return &op_;
     }
 
 private:
     shmr_ec_op_t* op_ = nullptr;
+    int carried_ = SHMR_EC_OK;
 };
 
 class ReedSolomon {

@@ -818,15 +818,31 @@ Status VirtualBlock::sync_data(bool force, int device, PhaseTimes* times) const 
             if (!es.ok()) {
                 // The data shard files already hold the new bytes while the parity
                 // files hold the old parity: the stripe is no codeword.  Make that
-                // detectable -- every parity file truncated to 0 bytes (a short
-                // shard: an erasure under VfsOptions::short_shard_is_erasure /
-                // missing_shard_is_erasure), never a silent rebuild from stale
-                // parity -- and leave the block dirty so the next flush re-encodes.
-                // (The reference unwraps the encode before any write, block.rs:427.)
+                // detectable under every option set -- every parity file unlinked
+                // (its handles closed; the next flush recreates it, ensure_fd): a
+                // later load fails to open it (reference rule) or, under
+                // missing_shard_is_erasure, counts it as an erasure, never as a
+                // present shard (a truncated file would be zero-padded and kept
+                // present when short_shard_is_erasure is off, block.rs:548-551,
+                // and a lost data shard then rebuilt from zeros) -- and leave the
+                // block dirty so the next flush re-encodes.  (The reference
+                // unwraps the encode before any write, block.rs:427.)
                 for (size_t i = k; i < nw; ++i) {
-                    if (st_->ensure_fd(i, *cfg_)) continue;
-                    const int fd = st_->handles[i].second;
-                    if (::ftruncate(fd, 0) == 0 && opt_.fsync_shards) (void)::fsync(fd);
+                    fs::path file;
+                    if (!st_->handles[i].first.resolve(*cfg_, &file, nullptr) && ::unlink(file.c_str()) == 0 &&
+                        opt_.fsync_shards) {   // the unlink reaches the directory
+                        const int dfd = ::open(file.parent_path().c_str(), O_RDONLY | O_DIRECTORY);
+                        if (dfd >= 0) {
+                            (void)::fsync(dfd);
+                            ::close(dfd);
+                        }
+                    }
+                    if (st_->handles[i].second >= 0) ::close(st_->handles[i].second);
+                    st_->handles[i].second = -1;
+                    if (i < st_->dfds.size()) {
+                        if (st_->dfds[i] >= 0) ::close(st_->dfds[i]);
+                        st_->dfds[i] = -1;
+                    }
                 }
                 st_->should_flush.store(true);
             }

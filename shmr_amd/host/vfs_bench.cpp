@@ -100,6 +100,9 @@ Result run_once(const std::shared_ptr<const ShmrFsConfig>& cfg, uint64_t ino, co
     }
     DIE_IF(vf.drop_buffers());   // repairs the lost shard files
     DIE_IF(vf.drop_handles());
+    // SHMR_VFS_KEEP_FILES=1: the shard files stay (tools/ref_cpu_vfs.cpp compares
+    // the reference CPU path's files of the same (ino, idx) with them)
+    if (std::getenv("SHMR_VFS_KEEP_FILES")) return r;
     for (auto& b : vf.blocks)
         for (auto& s : b.shards) {
             fs::path p;

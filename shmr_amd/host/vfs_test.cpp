@@ -550,7 +550,7 @@ void test_erasure_block_missing_shards() {
 
 // A per-block flush whose encode fails at the wait, after the data shard
 // files went out (mapped Block Cache: started encode): the parity files are
-// truncated (the stripe is detectably no codeword), the block stays dirty,
+// unlinked (the stripe is detectably no codeword), the block stays dirty,
 // and the next flush -- forced or not -- re-encodes and rewrites the stripe.
 void test_erasure_flush_encode_failure() {
     auto cfg = test_config();
@@ -582,7 +582,34 @@ void test_erasure_flush_encode_failure() {
         f.read(reinterpret_cast<char*>(got.data()), std::streamsize(S));
         CHECK(std::equal(got.begin(), got.end(), in.begin() + size + i * S));
     }
-    for (size_t i = 8; i < 11; ++i) CHECK(fsize(shard_file(*cfg, b, i)) == 0);   // no stale parity
+    for (size_t i = 8; i < 11; ++i) CHECK(!fs::exists(shard_file(*cfg, b, i)));   // no stale parity
+    {   // a crash here, then a lost data shard, under the reference's short-
+        // shard rule (zero-padded and kept present, block.rs:548-551): the
+        // unlinked parity counts as missing -- never rebuilt from zeros
+        VirtualBlock crashed;
+        crashed.size = b.size;
+        crashed.topology = b.topology;
+        crashed.shards = b.shards;
+        crashed.populate(cfg);
+        VfsOptions lax;
+        lax.missing_shard_is_erasure = true;
+        lax.short_shard_is_erasure = false;
+        crashed.set_options(lax);
+        const fs::path lost = shard_file(*cfg, b, 3);
+        const fs::path saved = lost.string() + ".saved";
+        fs::rename(lost, saved);
+        std::vector<uint8_t> rb(size);
+        Status cs = crashed.read(0, rb.data(), rb.size(), &n);
+        CHECK(cs && cs->kind == ShmrError::EcError && cs->code == SHMR_EC_TOO_FEW_SHARDS_PRESENT);
+        VirtualBlock strict;   // the reference's rule: a missing shard file fails the open
+        strict.size = b.size;
+        strict.topology = b.topology;
+        strict.shards = b.shards;
+        strict.populate(cfg);
+        fs::rename(saved, lost);
+        cs = strict.read(0, rb.data(), rb.size(), &n);
+        CHECK(cs && cs->kind == ShmrError::FsError && cs->code == ENOENT);
+    }
     // the block is still dirty: an unforced flush re-encodes
     o.fault_encode_wait = false;
     b.set_options(o);

@@ -104,6 +104,7 @@ class ReedSolomon:
         h = ctypes.c_void_p()
         _check(self._L.shmr_ec_new(data_shards, parity_shards, ctypes.byref(h)))
         self._h = h
+        self.device = int(device)
         if device:
             _check(self._L.shmr_ec_set_device(self._h, device))
 
@@ -130,6 +131,7 @@ class ReedSolomon:
         return out.reshape(t, k)
 
     def set_device(self, device: int) -> None:
+        self.device = int(device)
         _check(self._L.shmr_ec_set_device(self._h, device))
 
     def cache_stats(self):
@@ -406,6 +408,66 @@ class ReedSolomon:
                     blk[i] = fresh[b][i]
         del keep
 
+    # -- one block per call on device buffers: the submission queue ------------------
+    def _one_block(self, shards, present=None):
+        """One block's shards -> (ctypes pointer array, lengths, device).  Entries
+        are uint8 CUDA tensors or raw device addresses (ints, with ``shard_len``
+        given through ``present``-free calls); None = a NULL pointer."""
+        import torch
+        t = len(shards)
+        ptrs = (_u8p * max(t, 1))()
+        lens = (ctypes.c_size_t * max(t, 1))()
+        dev = None
+        for i, s in enumerate(shards):
+            if s is None:
+                continue
+            if isinstance(s, torch.Tensor):
+                if s.dtype != torch.uint8 or not s.is_cuda or not s.is_contiguous():
+                    raise TypeError("shards must be contiguous torch.uint8 GPU tensors")
+                ptrs[i] = ctypes.cast(s.data_ptr(), _u8p)
+                lens[i] = s.numel()
+                dev = s.device.index if dev is None else dev
+            else:
+                addr, n = s
+                ptrs[i] = ctypes.cast(int(addr), _u8p)
+                lens[i] = int(n)
+        return ptrs, lens, dev
+
+    def encode_dev(self, shards, device: Optional[int] = None, start: bool = False):
+        """``ReedSolomon::encode`` (reference src/vfs/block.rs:427) of ONE block whose
+        shards are GPU buffers (tensors, or (address, length) pairs), through the
+        device's submission queue (shmr_ec_encode_dev): concurrent calls merge into
+        batch launches.  Inputs must be complete (synchronised) before the call.
+        start=True returns an ``Op`` (shmr_ec_encode_dev_start)."""
+        ptrs, lens, dev = self._one_block(shards)
+        dev = int(device) if device is not None else (dev if dev is not None else self.device)
+        if start:
+            op = ctypes.c_void_p()
+            _check(self._L.shmr_ec_encode_dev_start(self._h, ptrs, lens, len(shards), dev, ctypes.byref(op)))
+            return Op(self._L, op, (ptrs, lens, shards))
+        _check(self._L.shmr_ec_encode_dev(self._h, ptrs, lens, len(shards), dev))
+        return None
+
+    def reconstruct_dev(self, shards, present, data_only: bool = False, device: Optional[int] = None,
+                        start: bool = False):
+        """``ReedSolomon::reconstruct{,_data}`` (block.rs:560) of ONE block of GPU
+        buffers through the submission queue (shmr_ec_reconstruct_dev): ``present``
+        flags per shard; absent shards name the buffers that receive the rebuilt
+        bytes (absent parity may be None with data_only)."""
+        ptrs, lens, dev = self._one_block(shards)
+        pr = np.ascontiguousarray(np.asarray(present, dtype=np.uint8))
+        for i in range(len(shards)):
+            if not pr[i]:
+                lens[i] = 0
+        dev = int(device) if device is not None else (dev if dev is not None else self.device)
+        if start:
+            op = ctypes.c_void_p()
+            _check(self._L.shmr_ec_reconstruct_dev_start(self._h, ptrs, lens, _ptr(pr), len(shards), int(data_only),
+                                                          dev, ctypes.byref(op)))
+            return Op(self._L, op, (ptrs, lens, pr, shards))
+        _check(self._L.shmr_ec_reconstruct_dev(self._h, ptrs, lens, _ptr(pr), len(shards), int(data_only), dev))
+        return None
+
     def _host_ptrs(self, blocks):
         t = self.total_shard_count()
         if isinstance(blocks, np.ndarray):
@@ -462,6 +524,26 @@ class ReedSolomon:
         _check(self._L.shmr_ec_reconstruct_blocks_host(self._h, ptrs, _ptr(pr), n, L, int(data_only), devs,
                                                      len(devices)))
         del keep
+
+
+class Op:
+    """A started call (shmr_ec_*_start): ``wait()`` completes it and raises on
+    its status; the arguments are kept alive until then."""
+
+    def __init__(self, L, op, keep):
+        self._L, self._op, self._keep = L, op, keep
+
+    def wait(self) -> None:
+        op, self._op = self._op, None
+        if op:
+            rc = self._L.shmr_ec_op_wait(op)
+            self._keep = None
+            _check(rc)
+
+    def __del__(self):
+        op = getattr(self, "_op", None)
+        if op:
+            self._L.shmr_ec_op_wait(op)
 
 
 class PinnedBuffer:
@@ -574,6 +656,48 @@ class ShardSlab:
             self._first = None
 
 
+class ShardPool:
+    """A device Block Cache of per-block slots (shmr_ec_pool_*): ``alloc()``
+    hands out one block's ``shards_per_block`` shard buffers (the lowest free
+    slot of a slab of ``slots_per_slab``), ``free(block)`` takes them back.
+    A block is a numpy uint64 address array; ``shard(block, i)`` a 1-D uint8
+    tensor view.  Tables over pool blocks in any order run the strided kernels
+    (the slab's slot lattice)."""
+
+    def __init__(self, shards_per_block: int, shard_len: int, slots_per_slab: int, device: int = 0):
+        self._L = lib()
+        h = ctypes.c_void_p()
+        _check(self._L.shmr_ec_pool_new(int(device), int(shards_per_block), int(shard_len), int(slots_per_slab),
+                                        ctypes.byref(h)))
+        self._h = h
+        self.shards_per_block, self.shard_len, self.device = shards_per_block, shard_len, device
+
+    def alloc(self) -> np.ndarray:
+        arr = (_u8p * self.shards_per_block)()
+        _check(self._L.shmr_ec_pool_alloc(self._h, arr))
+        return np.array([ctypes.cast(arr[i], ctypes.c_void_p).value for i in range(self.shards_per_block)],
+                        dtype=np.uint64)
+
+    def free(self, block: np.ndarray) -> None:
+        _check(self._L.shmr_ec_pool_free(self._h, ctypes.cast(int(block[0]), _u8p)))
+
+    def shard(self, block: np.ndarray, i: int):
+        import torch
+        view = _RawView(self, int(block[i]), (self.shard_len,))
+        return torch.as_tensor(view, device=torch.device("cuda", self.device))
+
+    def stats(self) -> dict:
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        _check(self._L.shmr_ec_pool_stats(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return {"slabs": int(a.value), "slots": int(b.value), "in_use": int(c.value)}
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._L.shmr_ec_pool_destroy(h)
+            self._h = None
+
+
 class _RawView:
     """``__cuda_array_interface__`` over part of a ShardSlab (keeps it alive)."""
 
@@ -623,6 +747,16 @@ def capture_reserve(bytes_: int, device: int = 0) -> None:
     the device's capture reserve (the tables of captured calls; a capture never
     grows it).  Blocking; call it before the capture."""
     _check(lib().shmr_ec_capture_reserve(int(device), int(bytes_)))
+
+
+QUEUE_COUNTERS = ("requests", "batches", "max_batch", "sleeps")
+
+
+def queue_stats(device: int = 0) -> dict:
+    """Submission-queue counters of a device ID (include/shmr_ec.h SHMR_EC_Q_*)."""
+    out = (ctypes.c_uint64 * len(QUEUE_COUNTERS))()
+    _check(lib().shmr_ec_queue_stats(int(device), out, len(QUEUE_COUNTERS)))
+    return {name: int(out[i]) for i, name in enumerate(QUEUE_COUNTERS)}
 
 
 def device_stats(device: int) -> dict:

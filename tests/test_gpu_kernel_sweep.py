@@ -21,7 +21,9 @@ Shape parameters (gf_apply.hpp LaunchShape) and how a call produces them:
              / mapped host slab (*_blocks_host over shmr_ec_host_alloc memory,
              zero-copy pointer tables) / pageable host slab (*_blocks_host,
              coded in place in the mapped pinned mirror)
-  segs       two erasure patterns in two block runs / one pattern
+  segs       reconstruct: two erasure patterns in two block runs / one pattern;
+             encode (r06): pointer-table blocks on a slot lattice in two runs
+             (slots 0-2 and 5-7: launch_slots' segment launch) / a pitch batch
   compact    reconstruct_batch_dev_out / in place
   sc1_ok     16-byte aligned outputs / an output (or, for pointer tables, a
              shard) off alignment
@@ -46,7 +48,7 @@ def _shapes():
     for decode, small_k, hm, ptrs, segs, compact, sc1_ok, fused, rows in itertools.product(
             (False, True), (False, True), (False, True), (False, True), (False, True), (False, True),
             (False, True), (False, True), (1, 2, 3, 4)):
-        if not decode and (segs or compact):
+        if not decode and (compact or (segs and (ptrs or hm))):
             continue
         if compact and (ptrs or hm):
             continue
@@ -80,20 +82,23 @@ def _patterns(k, t, rows, segs):
     return pr
 
 
-def _dev_views(gpu, arr, misalign_one):
+def _dev_views(gpu, arr, misalign_one, idx=None):
     """Separate GPU buffers per shard (slices of one arena); one shard off
-    16-byte alignment when misalign_one: the last shard of block 1, which no
-    erasure pattern here removes (a removed shard would be replaced by a fresh,
-    aligned buffer)."""
+    16-byte alignment when misalign_one: shard `idx` (default the last) of block
+    1 -- a shard the call touches (an encode's last parity row; a rebuild's
+    input `rows`, the first present shard after the erased ones: removed shards
+    are replaced by fresh, aligned buffers, and present shards past the first k
+    are never read)."""
     import torch
     Bn, t, L = arr.shape
     slot = (L + 64 + 255) // 256 * 256
     arena = torch.zeros(Bn * t * slot + 256, dtype=torch.uint8, device=gpu)
+    idx = t - 1 if idx is None else idx
     views = []
     for b in range(Bn):
         row = []
         for i in range(t):
-            off = (b * t + i) * slot + (3 if misalign_one and b == 1 and i == t - 1 else 0)
+            off = (b * t + i) * slot + (3 if misalign_one and b == 1 and i == idx else 0)
             v = arena[off:off + L]
             v.copy_(torch.from_numpy(np.ascontiguousarray(arr[b, i])).to(gpu))
             row.append(v)
@@ -129,6 +134,23 @@ def _run_case(gpu, s, seed):
             rs.encode_ptrs_dev(views)
             torch.cuda.synchronize()
             got = np.stack([np.stack([v.cpu().numpy() for v in row]) for row in views])
+        elif s["segs"]:   # block slots of one arena in two runs (a pool with a hole)
+            pitch = (L + 255) // 256 * 256
+            arena = torch.full(((B + 4) * t * pitch,), 0x77, dtype=torch.uint8, device=gpu)
+            slots = list(range(B // 2)) + list(range(B // 2 + 2, B + 2))
+            views = [[arena[(sl * t + i) * pitch:(sl * t + i) * pitch + L] for i in range(t)] for sl in slots]
+            for b in range(B):
+                for i in range(k):
+                    views[b][i].copy_(torch.from_numpy(cw[b, i].copy()).to(gpu))
+            shmr_amd.set_tuning(ptrs_grid=1)   # (the module runs with the table kernels)
+            try:
+                g0 = shmr_amd.device_stats(0)["ptr_table_grids"]
+                rs.encode_ptrs_dev(views)
+                assert shmr_amd.device_stats(0)["ptr_table_grids"] == g0 + 1
+            finally:
+                shmr_amd.set_tuning(ptrs_grid=0)
+            torch.cuda.synchronize()
+            got = np.stack([np.stack([v.cpu().numpy() for v in row]) for row in views])
         else:
             pitch = (L + 255) // 256 * 256
             data = torch.zeros((B, k, pitch), dtype=torch.uint8, device=gpu)
@@ -154,7 +176,7 @@ def _run_case(gpu, s, seed):
         rs.reconstruct_blocks_host(arr, pr)
         assert np.array_equal(np.array(arr), cw), s
     elif s["ptrs"]:
-        _, views = _dev_views(gpu, erased, not s["sc1_ok"])
+        _, views = _dev_views(gpu, erased, not s["sc1_ok"], idx=rows)
         blocks = [[(v if pr[b, i] else None) for i, v in enumerate(row)] for b, row in enumerate(views)]
         rs.reconstruct_ptrs_dev(blocks)
         torch.cuda.synchronize()

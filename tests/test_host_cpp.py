@@ -123,8 +123,12 @@ def test_erasure_block_missing_shards(tmp_path, gpu):
 def test_erasure_flush_encode_failure(tmp_path, gpu):
     """A per-block flush (mapped Block Cache: started encode, data shard files
     written while the GPU runs) whose encode fails at the wait (test hook
-    VfsOptions::fault_encode_wait): the parity files are truncated, the block
-    stays dirty, and the next unforced flush writes the oracle's stripe."""
+    VfsOptions::fault_encode_wait): the parity files are unlinked (a reload
+    that then loses a data shard fails -- TooFewShardsPresent under
+    missing_shard_is_erasure with the reference's zero-pad rule for short
+    shards, ENOENT without it -- instead of rebuilding from stale or zero
+    parity), the block stays dirty, and the next unforced flush writes the
+    oracle's stripe."""
     k, p = 8, 3
     data = np.concatenate([O.seeded_block(O.BENCH_SEED, 150 + i, MiB) for i in range(2)])
     files = run_case("erasure_flush_encode_failure", tmp_path, data)[0]

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -47,6 +48,18 @@ constexpr size_t BLOCK = T * PITCH;
 int encode_one(shmr_ec_t* rs, uint8_t* slab, size_t b, size_t n, hipStream_t s) {
     uint8_t* blk = slab + b * BLOCK;
     return shmr_ec_encode_batch_dev(rs, blk, PITCH, BLOCK, blk + K * PITCH, PITCH, BLOCK, n, S, 0, s);
+}
+
+// The crate's call on one block through the submission queue (r06):
+// shmr_ec_encode_dev, or the started form (*op set) waited later.
+int encode_queued(shmr_ec_t* rs, uint8_t* slab, size_t b, shmr_ec_op_t** op) {
+    uint8_t* ptrs[T];
+    size_t lens[T];
+    for (uint32_t i = 0; i < T; ++i) {
+        ptrs[i] = slab + b * BLOCK + i * PITCH;
+        lens[i] = S;
+    }
+    return op ? shmr_ec_encode_dev_start(rs, ptrs, lens, T, 0, op) : shmr_ec_encode_dev(rs, ptrs, lens, T, 0);
 }
 
 std::vector<uint8_t> parity_of(const uint8_t* slab, size_t blocks) {
@@ -119,6 +132,20 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "no device\n");
         return 1;
     }
+    if (const char* tune = std::getenv("SHMR_PB_TUNE")) {   // "key=value,key=value": library knobs
+        std::string spec(tune);
+        size_t pos = 0;
+        while (pos < spec.size()) {
+            const size_t end = std::min(spec.find(',', pos), spec.size());
+            const std::string kv = spec.substr(pos, end - pos);
+            const size_t eq = kv.find('=');
+            if (eq == std::string::npos || shmr_ec_set_tuning(kv.substr(0, eq).c_str(), std::atoi(kv.c_str() + eq + 1)) != 0) {
+                std::fprintf(stderr, "bad knob %s\n", kv.c_str());
+                return 1;
+            }
+            pos = end + 1;
+        }
+    }
     shmr_ec_t* rs = nullptr;
     if (shmr_ec_new(K, P, &rs) != 0) return 1;
     uint8_t* slab = nullptr;
@@ -160,10 +187,13 @@ int main(int argc, char** argv) {
     std::fflush(stdout);
     struct Mode {
         int wait_each, threads;
+        bool queue = false;   // r06: shmr_ec_encode_dev (submission queue) instead of a stream call
     };
     std::vector<Mode> modes;
-    for (int wait_each = 1; wait_each >= 0; --wait_each)
-        for (int threads : {1, 2, 4, 8, 16, 32}) modes.push_back({wait_each, threads});
+    const bool queue_only = std::getenv("SHMR_PB_QUEUE_ONLY") != nullptr;
+    for (int q = queue_only ? 1 : 0; q <= 1; ++q)
+        for (int wait_each = 1; wait_each >= 0; --wait_each)
+            for (int threads : {1, 2, 4, 8, 16, 32}) modes.push_back({wait_each, threads, q == 1});
     // variant sweep (tools build): knob sets, each over the latency / throughput modes
     std::vector<std::vector<std::pair<const char*, int>>> variants = {{}};
     if (std::getenv("SHMR_PB_SWEEP")) {
@@ -198,14 +228,30 @@ int main(int argc, char** argv) {
             for (auto& s : ss) CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
             double best = 1e30;
             bool ok = true;
+            uint64_t q0[SHMR_EC_Q_COUNTERS] = {}, q1[SHMR_EC_Q_COUNTERS] = {};
             for (int r = 0; r < reps + 1; ++r) {
                 CHECK_HIP(hipMemset2D(slab + K * PITCH, BLOCK, 0, P * PITCH, blocks));   // parity cleared
                 CHECK_HIP(hipDeviceSynchronize());
                 std::vector<int> rc(size_t(threads), 0);
-                const auto t0 = std::chrono::steady_clock::now();
+                // r06: the workers are started before the clock and released
+                // together (a rayon pool exists before the flush it serves);
+                // r05's figures included the thread creation
+                std::atomic<int> go{0};
                 std::vector<std::thread> ts;
                 for (int t = 0; t < threads; ++t)
                     ts.emplace_back([&, t] {
+                        while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
+                        if (md.queue) {
+                            std::vector<shmr_ec_op_t*> ops;
+                            for (size_t b = size_t(t); b < blocks; b += size_t(threads)) {
+                                shmr_ec_op_t* op = nullptr;
+                                if (encode_queued(rs, slab, b, wait_each ? nullptr : &op) != 0) rc[size_t(t)] = 1;
+                                if (op) ops.push_back(op);
+                            }
+                            for (shmr_ec_op_t* op : ops)
+                                if (shmr_ec_op_wait(op) != 0) rc[size_t(t)] = 1;
+                            return;
+                        }
                         hipStream_t s = ss[size_t(t)];
                         for (size_t b = size_t(t); b < blocks; b += size_t(threads)) {
                             if (encode_one(rs, slab, b, 1, s) != 0) rc[size_t(t)] = 1;
@@ -213,18 +259,26 @@ int main(int argc, char** argv) {
                         }
                         if (hipStreamSynchronize(s) != hipSuccess) rc[size_t(t)] = 1;
                     });
+                (void)shmr_ec_queue_stats(0, q0, SHMR_EC_Q_COUNTERS);
+                const auto t0 = std::chrono::steady_clock::now();
+                go.store(1, std::memory_order_release);
                 for (auto& th : ts) th.join();
                 const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+                (void)shmr_ec_queue_stats(0, q1, SHMR_EC_Q_COUNTERS);
                 for (int x : rc) ok = ok && x == 0;
                 if (r >= 1) best = std::min(best, sec);   // rep 0 warms the streams' state
             }
             const bool same = parity_of(slab, blocks) == want;
-            std::printf("{\"mode\": \"per_block\", \"knobs\": \"%s\", \"variant\": \"%s\", "
+            const uint64_t nb = q1[SHMR_EC_Q_BATCHES] - q0[SHMR_EC_Q_BATCHES];
+            std::printf("{\"mode\": \"per_block\", \"api\": \"%s\", \"knobs\": \"%s\", \"variant\": \"%s\", "
                         "\"wait_each_call\": %s, \"threads\": %d, \"blocks\": %zu, "
                         "\"GiBps\": %.1f, \"us_per_block\": %.2f, \"of_batch\": %.3f, \"ok\": %s, "
-                        "\"parity_equals_batch\": %s}\n",
-                        label.c_str(), variant, wait_each ? "true" : "false", threads, blocks, data_gib / best,
-                        best / blocks * 1e6, best_batch / best, ok ? "true" : "false", same ? "true" : "false");
+                        "\"parity_equals_batch\": %s, \"tune\": \"%s\", \"queue_batches_last_rep\": %llu, "
+                        "\"blocks_per_launch_last_rep\": %.2f}\n",
+                        md.queue ? "encode_dev (queue)" : "encode_batch_dev (stream)", label.c_str(), variant,
+                        wait_each ? "true" : "false", threads, blocks, data_gib / best,
+                        best / blocks * 1e6, best_batch / best, ok ? "true" : "false", same ? "true" : "false",
+                        std::getenv("SHMR_PB_TUNE") ? std::getenv("SHMR_PB_TUNE") : "", (unsigned long long)nb, nb ? double(blocks) / double(nb) : 0.0);
             std::fflush(stdout);
             for (auto& s : ss) CHECK_HIP(hipStreamDestroy(s));
             if (!ok || !same) return 1;

@@ -24,6 +24,14 @@ can get:
   ptrs_page      per-shard allocations spaced by S + 4 KiB, 16 B past a page, as
                  glibc's mmap-served Vec<u8> allocations of these sizes are
                  (reference src/vfs/block.rs:408-419)
+  pool_dense     r06: shmr_ec_pool slots, every slot live, blocks in shuffled order
+                 (the table sorts into one lattice run); rebuilds in place
+  pool_holed     r06: a pool after churn: B + B/4 slots, a random quarter freed,
+                 the B live blocks in shuffled order (lattice runs -> segment runs
+                 or a block list); _tab: the same with ptrs_grid=0; _pl (rebuilds):
+                 one launch set per erasure pattern (knob pattern_launches)
+  joint_padNk    r06, encode: one torch slab, block b's k + p shards at b * (t*P + N KiB)
+                 + i * P (the pool's slot layout, with N KiB between slots)
 
     python tools/ptrs_ab.py --config encode83 --rounds 11
 """
@@ -163,6 +171,51 @@ def main():
     else:
         runs["smajor"] = ptrs_run(sm_tab)
         runs["smajor_tab"] = ptrs_run(sm_tab, grid=False)
+
+    # -- r06: a slot pool (shmr_ec_pool_*), blocks taken in shuffled order ------------
+    # pool_dense: B slots, all live (one lattice run once sorted); pool_holed: B + B/4
+    # slots, a random quarter freed again (holes), the other B blocks in shuffled
+    # order -- a Block Cache after churn.  Encodes write parity into the block's
+    # own slot; rebuilds write the lost shard in place.  _tab: ptrs_grid=0.
+    prng = np.random.default_rng(17)
+    for name, extra in (("pool_dense", 0), ("pool_holed", B // 4)):
+        pool = shmr_amd.ShardPool(t, S, B + extra)
+        blocks = [pool.alloc() for _ in range(B + extra)]
+        for j in sorted(prng.choice(B + extra, size=extra, replace=False).tolist(), reverse=True):
+            pool.free(blocks.pop(j))
+        order = prng.permutation(B)
+        rows_ = np.stack([blocks[int(j)] for j in order])
+        for r in rows_:
+            for i in range(k):
+                pool.shard(r, i).copy_(torch.randint(0, 256, (S,), dtype=torch.uint8, device=dev, generator=g))
+        ptab = table(rows_)
+        assert rs._L.shmr_ec_encode_ptrs_dev(rs._h, ptab, B, S, 0, sp) == 0
+        runs[name] = ptrs_run(ptab)
+        runs[name + "_tab"] = ptrs_run(ptab, grid=False)
+        if er:   # the rebuild's patterns as one launch set each (knob pattern_launches)
+            def pl(f=ptrs_run(ptab)):
+                shmr_amd.set_tuning(pattern_launches=1)
+                try:
+                    return f()
+                finally:
+                    shmr_amd.set_tuning(pattern_launches=-2)
+            runs[name + "_pl"] = pl
+        keep.append(pool)
+    # -- r06: one joint slab per block slot (k + p shards at P), block pitch t*P + pad --
+    if er == 0:
+        for pad in (0, 4096, 8192, 65536, 69632, 1 << 20):
+            BP = t * P + pad
+            jt = torch.zeros((B * BP,), dtype=torch.uint8, device=dev)
+            jv = jt.view(B, BP)
+            for i in range(k):
+                jv[:, i * P:i * P + S] = torch.randint(0, 256, (B, S), dtype=torch.uint8, device=dev, generator=g)
+            keep.append(jt)
+
+            def joint(jt=jt, BP=BP):
+                b0 = jt.data_ptr()
+                return rs._L.shmr_ec_encode_batch_dev(rs._h, ctypes.c_void_p(b0), P, BP, ctypes.c_void_p(b0 + k * P),
+                                                      P, BP, B, S, 0, sp)
+            runs[f"joint_pad{pad // 1024}k"] = joint
 
     # -- one hipMalloc per shard (shmr_ec_device_alloc) ------------------------------
     bufs = [[shmr_amd.DeviceBuffer(S, device=0, contiguous=False) for _ in range(t)] for _ in range(B)]
