@@ -154,7 +154,7 @@ int shmr_ec_op_wait(shmr_ec_op_t* op);
  * The reference makes one such call per block from rayon workers
  * (src/vfs/mod.rs:91-97).  One launch per block leaves the GPU launch-bound,
  * so per device ID the library keeps a submission queue: a call's block is
- * launched at once when fewer than "coalesce_depth" (default 2) batches are in
+ * launched at once when fewer than "coalesce_depth" (default 1) batches are in
  * flight on the queue's stream, and otherwise merges with every call that
  * arrives meanwhile (from any thread, any codec; knob "coalesce_us": an idle
  * queue waits that long for company) into the next launch -- one pointer-
@@ -395,7 +395,8 @@ int shmr_ec_set_device(shmr_ec_t* rs, int device);
 /* Tuning knobs (process-wide).
  *
  * Host-path knobs (both flavours; they choose how bytes move, never what
- * the kernels compute): "coalesce" (0/1, default 1): shmr_ec_encode /
+ * the kernels compute): "coalesce" (0/1, default 0 -- measured no faster on
+ * PCIe-bound mapped blocks): shmr_ec_encode /
  * shmr_ec_reconstruct (and *_start) whose shards all lie in mapped memory go
  * through the device's submission queue (above), merged with concurrent
  * calls, instead of one zero-copy launch per call; "coalesce_depth",

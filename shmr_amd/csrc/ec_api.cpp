@@ -41,6 +41,21 @@ int guarded(F&& f) noexcept {
         return SHMR_EC_DEVICE_ERROR;
     }
 }
+// The submission queue's per-block entry points make no HIP call in the
+// caller's thread except through the queue (whose launches, watcher and
+// creation enter the relaxed mode themselves): no mode switch per call -- two
+// runtime calls per block that the 16-thread per-block shape pays in
+// contention (r06, tools/perblock_dev.cpp).
+template <class F>
+int guarded_light(F&& f) noexcept {
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        return SHMR_EC_OUT_OF_MEMORY;
+    } catch (...) {
+        return SHMR_EC_DEVICE_ERROR;
+    }
+}
 // Slabs handed out by shmr_ec_device_alloc_shards (base -> device).
 std::mutex g_slab_mu;
 std::map<uintptr_t, int> g_slabs;
@@ -618,7 +633,7 @@ static int reconstruct_impl(shmr_ec_t* rs, uint8_t* const* shards, const size_t*
 // launches (submit.hpp).
 static int encode_dev_impl(shmr_ec_t* rs, uint8_t* const* d_shards, const size_t* shard_lens, size_t nshards,
                            int device, core::SubmitReq** queued) {
-    return guarded([&]() -> int {
+    return guarded_light([&]() -> int {
         size_t len = 0;
         int rc = check_encode(rs, d_shards, shard_lens, nshards, &len);
         if (rc) return rc;
@@ -632,7 +647,7 @@ static int encode_dev_impl(shmr_ec_t* rs, uint8_t* const* d_shards, const size_t
 static int reconstruct_dev_impl(shmr_ec_t* rs, uint8_t* const* d_shards, const size_t* shard_lens,
                                 const uint8_t* present, size_t nshards, int data_only, int device,
                                 core::SubmitReq** queued) {
-    return guarded([&]() -> int {
+    return guarded_light([&]() -> int {
         size_t len = 0;
         std::shared_ptr<Plan> plan;
         int rc = check_reconstruct(rs, d_shards, shard_lens, present, nshards, data_only, &len, &plan);
@@ -682,7 +697,7 @@ static int start_op(int rc, core::Staging* s, core::SubmitReq* req, shmr_ec_op_t
         drop();
         return rc;
     }
-    return guarded([&]() -> int {
+    return guarded_light([&]() -> int {
         try {
             *op = new shmr_ec_op;
         } catch (...) {
@@ -739,7 +754,7 @@ int shmr_ec_op_wait(shmr_ec_op_t* op) {
     int rc = SHMR_EC_OK;
     if (op->s) rc = guarded([&] { return core::finish_async(op->s); });
     if (op->req) {
-        rc = guarded([&] { return core::wait(op->req); });
+        rc = guarded_light([&] { return core::wait(op->req); });
         delete op->req;
     }
     delete op;

@@ -5,6 +5,7 @@
 #include <chrono>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <unordered_set>
 
 namespace shmr {
@@ -485,10 +486,14 @@ struct CaptureChunk {
     std::map<size_t, size_t> free_;   // offset -> length, coalesced
 };
 
+constexpr size_t kMirrorStreams = 32;   // per device: caller streams with a mirror stream of their own
+
 struct DeviceState {
     int dev = -1;
     bool uvec = false;             // probe verdict of the physical GPU
     hipStream_t priv = nullptr;    // private stream of init-time work
+    std::mutex mmu;                // guards mirrors
+    std::unordered_map<hipStream_t, hipStream_t> mirrors;   // caller stream -> its mirror stream
     std::mutex mu;                 // guards chunks
     std::vector<ArenaChunk> chunks;
     std::mutex cmu;                // guards cchunks and their free lists
@@ -622,6 +627,15 @@ bool own_stream(hipStream_t s) {
     return g_own_streams->count(s) != 0;
 }
 
+hipError_t create_priority_stream(hipStream_t* s) {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) {
+        (void)hipGetLastError();
+        return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    }
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
+}
+
 int record_mirrored(int dev, hipStream_t stream, hipEvent_t on_caller, hipEvent_t mirror) {
     if (own_stream(stream)) {
         if (hipEventRecord(mirror, stream) == hipSuccess) return SHMR_EC_OK;
@@ -634,8 +648,30 @@ int record_mirrored(int dev, hipStream_t stream, hipEvent_t on_caller, hipEvent_
         if (rc) return rc;
         ds = state_of(dev);
     }
-    if (hipEventRecord(on_caller, stream) != hipSuccess || hipStreamWaitEvent(ds->priv, on_caller, 0) != hipSuccess ||
-        hipEventRecord(mirror, ds->priv) != hipSuccess) {
+    // r06: the caller stream's own mirror stream (the private stream once the
+    // per-device cap is reached): a caller stream held up by something outside
+    // the library then delays only its own mirrors, not every other stream's
+    // (before, all of them queued on the one private stream behind its wait)
+    hipStream_t ms = ds->priv;
+    {
+        std::lock_guard<std::mutex> lock(ds->mmu);
+        auto it = ds->mirrors.find(stream);
+        if (it != ds->mirrors.end()) {
+            ms = it->second;
+        } else if (ds->mirrors.size() < kMirrorStreams) {
+            hipStream_t m = nullptr;
+            if (create_priority_stream(&m) == hipSuccess) {
+                ds->mirrors[stream] = m;
+                register_own_stream(m);
+                count_device(dev, kDevStagingStreams);
+                ms = m;
+            } else {
+                (void)hipGetLastError();
+            }
+        }
+    }
+    if (hipEventRecord(on_caller, stream) != hipSuccess || hipStreamWaitEvent(ms, on_caller, 0) != hipSuccess ||
+        hipEventRecord(mirror, ms) != hipSuccess) {
         (void)hipGetLastError();
         return SHMR_EC_DEVICE_ERROR;
     }
@@ -661,7 +697,7 @@ int device_init(int dev, hipStream_t caller) {
     auto* ds = new DeviceState;
     ds->dev = dev;
     count_device(dev, kDevBlockingCalls);
-    if (hipStreamCreateWithFlags(&ds->priv, hipStreamNonBlocking) != hipSuccess) {
+    if (create_priority_stream(&ds->priv) != hipSuccess) {
         (void)hipGetLastError();
         delete ds;
         return SHMR_EC_DEVICE_ERROR;
@@ -856,10 +892,13 @@ int plan_on_device(Plan& plan, int dev, hipStream_t stream, bool compact, const 
             pd->state = PlanDev::kDone;
         } else if (q == hipErrorNotReady) {
             (void)hipGetLastError();
-            // still in flight on another stream: order this stream after it
-            if (pd->stream != stream && hipStreamWaitEvent(stream, pd->mready, 0) != hipSuccess) {
-                (void)hipGetLastError();
-                return SHMR_EC_DEVICE_ERROR;
+            // still in flight on another stream (which may be held up by
+            // anything): upload the same bytes again on this one rather than
+            // wait for it (r06; the permanent pinned image, the same device
+            // slot -- a second copy of identical bytes)
+            if (pd->stream != stream) {
+                const int rc = upload_plan(*pd, dev, stream, false);
+                if (rc) return rc;
             }
         } else {
             (void)hipGetLastError();
@@ -1362,9 +1401,30 @@ UploadRing* UploadRing::for_device(int dev, int* rc, Kind kind) {
 int UploadRing::acquire(uint8_t** host, uint8_t** dev, int* slot) {
     std::unique_lock<std::mutex> lock(mu_);
     for (;;) {
-        for (int n = 0; n < kSlots; ++n) {
+        // r06: a free slot whose last reader has finished, if there is one --
+        // never wait behind a reader held up on some stream while other slots
+        // are ready (a caller stream held by a host-released wait)
+        int ready = -1, any = -1;
+        for (int n = 0; n < kSlots && ready < 0; ++n) {
             const int i = (next_ + n) % kSlots;
             if (inuse_[i]) continue;
+            if (any < 0) any = i;
+            if (!armed_[i]) {
+                ready = i;
+            } else {
+                const hipError_t q = hipEventQuery(mev_[i]);
+                if (q == hipSuccess) {
+                    armed_[i] = false;
+                    ready = i;
+                } else if (q == hipErrorNotReady) {
+                    (void)hipGetLastError();
+                } else {
+                    (void)hipGetLastError();
+                    ready = i;   // (an error surfaces below, on the slot's own wait)
+                }
+            }
+        }
+        for (int i = ready >= 0 ? ready : any; i >= 0;) {
             inuse_[i] = true;
             next_ = (i + 1) % kSlots;
             const bool armed = armed_[i];

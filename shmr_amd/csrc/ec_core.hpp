@@ -331,6 +331,12 @@ private:
 // captured) records `mirror` itself -- no private-stream wait, which would put
 // a barrier on a shared hardware queue for every per-block host call.
 int record_mirrored(int dev, hipStream_t stream, hipEvent_t on_caller, hipEvent_t mirror);
+// A library stream at the device's greatest stream priority (r06): the
+// runtime multiplexes streams of one priority onto a few hardware queues, so a
+// caller's stream held by a host-released wait blocks whatever else shares
+// its queue; the library's own queue, mirror and private streams sit in the
+// high-priority pool instead (tests/test_gpu_hol.py).  Current device.
+hipError_t create_priority_stream(hipStream_t* s);
 // Streams the library creates (registered once, never destroyed).
 void register_own_stream(hipStream_t s);
 bool own_stream(hipStream_t s);

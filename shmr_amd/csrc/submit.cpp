@@ -32,14 +32,15 @@ namespace {
 
 using Clock = std::chrono::steady_clock;
 
-std::atomic<int> g_coalesce{1};      // host-buffer entry points on mapped memory through the queue
-std::atomic<int> g_depth{2};         // batches in flight before pending calls wait to merge
+std::atomic<int> g_coalesce{0};      // host-buffer entry points on mapped memory through the queue
+std::atomic<int> g_depth{1};         // batches in flight before pending calls wait to merge
 std::atomic<int> g_target{64};       // ... unless this many are pending (a launch of its own)
 std::atomic<int> g_window_us{0};     // an idle queue's launch waits this long for more calls
 std::atomic<int> g_max{1024};        // blocks per launch
 std::atomic<int> g_spin_us{30};      // a waiter spins this long before it sleeps
 std::atomic<int> g_watch_us{200};    // the watcher spins this long before it sleeps on the event
-constexpr int kDepthDefault = 2, kTargetDefault = 64, kWindowDefault = 0, kMaxDefault = 1024, kSpinDefault = 30,
+std::atomic<int> g_mark{1};          // 1: a mark kernel advances the word; 0: the watcher does, from the event
+constexpr int kDepthDefault = 1, kTargetDefault = 64, kWindowDefault = 0, kMaxDefault = 1024, kSpinDefault = 30,
               kWatchDefault = 200;
 
 constexpr int kMaxQueues = 64;   // device IDs (ec_core kMaxDevIds)
@@ -53,12 +54,12 @@ public:
     explicit Queue(int dev) : dev_(dev) {}
 
     int init() {
+        RelaxedCapture relaxed;
         int rc = device_init(dev_, nullptr);
         if (rc) return rc;
         DeviceScope scope(dev_);
         if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
-        RelaxedCapture relaxed;
-        if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) {
+        if (create_priority_stream(&stream_) != hipSuccess) {
             (void)hipGetLastError();
             return SHMR_EC_DEVICE_ERROR;
         }
@@ -117,6 +118,11 @@ private:
     };
 
     uint64_t completed() const { return __atomic_load_n(word_, __ATOMIC_ACQUIRE); }
+    // The host's own advance of the word (knob coalesce_mark=0; only the
+    // watcher writes it then, in launch order).
+    void advance(uint64_t seq) {
+        if (completed() < seq) __atomic_store_n(word_, seq, __ATOMIC_RELEASE);
+    }
 
     bool finished(const SubmitReq* r) const {
         if (r->done.load(std::memory_order_acquire)) return true;   // failed launch, or a broken queue
@@ -234,6 +240,22 @@ private:
         uint64_t m = g_stats[dev_][kMaxBatch].load(std::memory_order_relaxed);
         while (reqs.size() > m && !g_stats[dev_][kMaxBatch].compare_exchange_weak(m, reqs.size())) {
         }
+        const bool mark = g_mark.load(std::memory_order_relaxed) != 0;
+        if (!mark) {   // the watcher advances the word once the batch's event completes
+            if (!*ev && hipEventCreateWithFlags(ev, hipEventDisableTiming | hipEventBlockingSync) != hipSuccess) {
+                (void)hipGetLastError();
+                *ev = nullptr;
+            }
+            if (*ev && hipEventRecord(*ev, stream_) == hipSuccess) return true;
+            (void)hipGetLastError();
+            if (hipStreamSynchronize(stream_) != hipSuccess) {   // no event: drained, statuses final
+                (void)hipGetLastError();
+                broken_.store(true, std::memory_order_release);
+            }
+            for (SubmitReq* q : reqs)
+                if (q->rc == SHMR_EC_OK) q->rc = SHMR_EC_DEVICE_ERROR;
+            return false;
+        }
         if (kern::launch_mark(dword_, seq, stream_) != hipSuccess) {
             (void)hipGetLastError();
             // no mark: drain the stream so no request completes early
@@ -284,6 +306,19 @@ private:
                     seen = true;
                     break;
                 }
+                if (ev && !g_mark.load(std::memory_order_relaxed) && (i & 15) == 15) {   // no mark kernel:
+                    const hipError_t q = hipEventQuery(ev);                               // poll the event
+                    if (q == hipSuccess) {
+                        advance(target);
+                        seen = true;
+                        break;
+                    }
+                    if (q != hipErrorNotReady) {
+                        (void)hipGetLastError();
+                        break;   // (the blocking wait below reports it)
+                    }
+                    (void)hipGetLastError();
+                }
                 if ((i & 255) == 255 && Clock::now() - t0 >= spin) break;
                 cpu_relax();
             }
@@ -292,6 +327,8 @@ private:
                 if (hipEventSynchronize(ev) != hipSuccess) {
                     (void)hipGetLastError();
                     broken_.store(true, std::memory_order_release);
+                } else if (!g_mark.load(std::memory_order_relaxed)) {
+                    advance(target);
                 }
                 g_stats[dev_][kSleeps].fetch_add(1, std::memory_order_relaxed);
             }
@@ -378,13 +415,14 @@ int set_submit_tuning(const std::string& key, int value, bool* known) {
         v = value;
         return SHMR_EC_OK;
     };
-    if (key == "coalesce") return set(g_coalesce, 1, 0, 1);
+    if (key == "coalesce") return set(g_coalesce, 0, 0, 1);
     if (key == "coalesce_depth") return set(g_depth, kDepthDefault, 1, 64);
     if (key == "coalesce_target") return set(g_target, kTargetDefault, 1, 65536);
     if (key == "coalesce_us") return set(g_window_us, kWindowDefault, 0, 100000);
     if (key == "coalesce_max") return set(g_max, kMaxDefault, 1, 65536);
     if (key == "coalesce_spin_us") return set(g_spin_us, kSpinDefault, 0, 10000000);
     if (key == "coalesce_watch_us") return set(g_watch_us, kWatchDefault, 0, 10000000);
+    if (key == "coalesce_mark") return set(g_mark, 1, 0, 1);
     *known = false;
     return SHMR_EC_INVALID_ARGUMENT;
 }
@@ -398,6 +436,7 @@ int get_submit_tuning(const std::string& key, bool* known) {
     if (key == "coalesce_max") return g_max;
     if (key == "coalesce_spin_us") return g_spin_us;
     if (key == "coalesce_watch_us") return g_watch_us;
+    if (key == "coalesce_mark") return g_mark;
     *known = false;
     return SHMR_EC_INVALID_ARGUMENT;
 }

@@ -283,10 +283,10 @@ def test_validation_in_crate_order(gpu):
 
 def test_mapped_host_calls_coalesced(gpu):
     """The drop-in shmr_ec_encode / shmr_ec_reconstruct on mapped Block-Cache
-    buffers (shmr_ec_host_alloc) from 8 threads go through the queue (knob
-    "coalesce", default on): the oracle's bytes, counted zero-copy; with the
-    knob off the same calls take one zero-copy launch each and give the same
-    bytes."""
+    buffers (shmr_ec_host_alloc) from 8 threads go through the queue under knob
+    "coalesce" = 1 (default 0: measured no faster, tools/perblock_host.cpp):
+    the oracle's bytes, counted zero-copy; with the knob off the same calls
+    take one zero-copy launch each and give the same bytes."""
     k, p, S, B = 8, 3, 131072, 32
     t = k + p
     rs = shmr_amd.ReedSolomon(k, p)
@@ -349,6 +349,7 @@ def test_mapped_rebuild_in_place_coalesced(gpu):
         arr[b, pats[b] == 0] = 0xEE
     L = rs._L
     q0 = shmr_amd.queue_stats(0)
+    shmr_amd.set_tuning(coalesce=1)
 
     def worker(th):
         for b in range(th, B, 6):
@@ -358,25 +359,29 @@ def test_mapped_rebuild_in_place_coalesced(gpu):
             pr = pats[b].copy()
             assert L.shmr_ec_reconstruct(rs._h, ptrs, lens, pr.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), t,
                                          0) == 0
-    ths = [threading.Thread(target=worker, args=(i,)) for i in range(6)]
-    for x in ths:
-        x.start()
-    for x in ths:
-        x.join()
+    try:
+        ths = [threading.Thread(target=worker, args=(i,)) for i in range(6)]
+        for x in ths:
+            x.start()
+        for x in ths:
+            x.join()
+    finally:
+        shmr_amd.set_tuning(coalesce=-2)
     assert np.array_equal(arr, full)
     assert shmr_amd.queue_stats(0)["requests"] - q0["requests"] == B
 
 
 def test_alias_devices_have_queues_of_their_own(gpu):
-    """Tools build, 3 alias device IDs on the one GPU: concurrent per-block
+    """Tools build, alias device IDs on the one GPU: concurrent per-block
     calls spread over four IDs are merged per ID (each ID's queue counts its
     own requests) and every block is exact."""
     import torch
     with _native.tools():
         n = shmr_amd.device_count()
-        shmr_amd.set_tuning(alias_devices=3)
+        shmr_amd.set_tuning(alias_devices=7)
         try:
-            ids = list(range(n + 3))[-4:]
+            # (IDs past n + 3: test_gpu_capture needs alias ID n untouched)
+            ids = [0, n + 4, n + 5, n + 6]
             k, p, S, per = 8, 3, 32768, 12
             t = k + p
             rs = shmr_amd.ReedSolomon(k, p)

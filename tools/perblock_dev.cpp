@@ -191,9 +191,12 @@ int main(int argc, char** argv) {
     };
     std::vector<Mode> modes;
     const bool queue_only = std::getenv("SHMR_PB_QUEUE_ONLY") != nullptr;
+    const int only_threads = std::getenv("SHMR_PB_THREADS") ? std::atoi(std::getenv("SHMR_PB_THREADS")) : 0;
+    const bool async_only = std::getenv("SHMR_PB_ASYNC_ONLY") != nullptr;
     for (int q = queue_only ? 1 : 0; q <= 1; ++q)
-        for (int wait_each = 1; wait_each >= 0; --wait_each)
-            for (int threads : {1, 2, 4, 8, 16, 32}) modes.push_back({wait_each, threads, q == 1});
+        for (int wait_each = async_only ? 0 : 1; wait_each >= 0; --wait_each)
+            for (int threads : {1, 2, 4, 8, 16, 32})
+                if (!only_threads || threads == only_threads) modes.push_back({wait_each, threads, q == 1});
     // variant sweep (tools build): knob sets, each over the latency / throughput modes
     std::vector<std::vector<std::pair<const char*, int>>> variants = {{}};
     if (std::getenv("SHMR_PB_SWEEP")) {

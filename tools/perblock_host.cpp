@@ -9,6 +9,7 @@
 // Build: hipcc --offload-arch=gfx950 -O2 -std=c++17 -Iinclude -o tools/_abx/perblock_host tools/perblock_host.cpp
 //          -Lshmr_amd/_lib -lshmr_ec -Wl,-rpath,'$ORIGIN/../../shmr_amd/_lib' -lpthread   (one line)
 // Usage: perblock_host [blocks=128] [rounds=5]
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -56,6 +57,22 @@ int main(int argc, char** argv) {
     const size_t B = argc > 1 ? std::strtoul(argv[1], nullptr, 10) : 128;
     const int rounds = argc > 2 ? std::atoi(argv[2]) : 5;
     if (shmr_ec_device_init(0) != 0) return 1;
+    std::string tune_spec;
+    if (const char* tune = std::getenv("SHMR_PB_TUNE")) {   // "key=value,...": knobs for the coalesce=1 legs
+        tune_spec = tune;
+        size_t pos = 0;
+        while (pos < tune_spec.size()) {
+            const size_t end = std::min(tune_spec.find(',', pos), tune_spec.size());
+            const std::string kv = tune_spec.substr(pos, end - pos);
+            const size_t eq = kv.find('=');
+            if (eq == std::string::npos ||
+                shmr_ec_set_tuning(kv.substr(0, eq).c_str(), std::atoi(kv.c_str() + eq + 1)) != 0) {
+                std::fprintf(stderr, "bad knob %s\n", kv.c_str());
+                return 1;
+            }
+            pos = end + 1;
+        }
+    }
     shmr_ec_t* rs = nullptr;
     if (shmr_ec_new(K, P, &rs) != 0) return 1;
     void* mem = nullptr;
@@ -123,9 +140,10 @@ int main(int argc, char** argv) {
     (void)shmr_ec_queue_stats(0, q, SHMR_EC_Q_COUNTERS);
     for (const Leg& L : legs)
         std::printf("{\"op\": \"%s\", \"leg\": \"%s\", \"coalesce\": %d, \"threads\": %d, \"blocks\": %zu, "
-                    "\"GiBps\": %.2f, \"ms_per_block_per_thread\": %.3f, \"buffers\": \"mapped Block Cache\"}\n",
+                    "\"GiBps\": %.2f, \"ms_per_block_per_thread\": %.3f, \"buffers\": \"mapped Block Cache\", "
+                    "\"tune\": \"%s\"}\n",
                     L.decode ? "reconstruct" : "encode", L.name.c_str(), L.batch ? -1 : L.coalesce, L.threads, B,
-                    gib / L.best, L.best / double(B) * L.threads * 1e3);
+                    gib / L.best, L.best / double(B) * L.threads * 1e3, tune_spec.c_str());
     std::printf("{\"queue_requests\": %llu, \"queue_batches\": %llu, \"max_batch\": %llu}\n",
                 (unsigned long long)q[SHMR_EC_Q_REQUESTS], (unsigned long long)q[SHMR_EC_Q_BATCHES],
                 (unsigned long long)q[SHMR_EC_Q_MAX_BATCH]);
