@@ -12,6 +12,7 @@
 // kernels, which wait on a scalar load of each block's row.
 #include <algorithm>
 #include <cstring>
+#include <map>
 #include <numeric>
 #include <vector>
 
@@ -123,6 +124,41 @@ bool lattice_form(unsigned k, unsigned t, const uint64_t* tab, const uint8_t* pr
     return true;
 }
 
+// Whether a lattice rebuild would need the multi-plan block list -- several
+// erasure patterns of one row count whose blocks (slot order) fall into more
+// runs than the kernel arguments hold (ec_core reconstruct_on_device): every
+// workgroup's plan is then three dependent loads away (list, plan index, plan
+// table), and the table kernels, whose rows name the addresses directly, ran
+// 3-5 points faster (pool with mixed patterns, profiles/r06/s1, s2:
+// ptrs_ab decode83 pool_dense 0.666 / 0.656 vs pool_dense_tab 0.714 / 0.684).
+bool lattice_needs_plan_list(unsigned t, const uint8_t* present, const LatticeForm& F) {
+    std::map<std::vector<uint8_t>, std::vector<uint64_t>> by_pattern;   // pattern -> slots (ascending)
+    for (size_t i = 0; i < F.rows.size(); ++i) {
+        const uint8_t* pr = present + F.rows[i] * t;
+        by_pattern[std::vector<uint8_t>(pr, pr + t)].push_back(F.slots[i]);
+    }
+    std::map<unsigned, std::pair<size_t, size_t>> by_m;   // absent count -> (patterns, runs)
+    for (const auto& g : by_pattern) {
+        unsigned m = 0;
+        for (uint8_t x : g.first) m += x ? 0 : 1;
+        size_t runs = 0;
+        const auto& v = g.second;
+        for (size_t i = 0; i < v.size();) {
+            size_t e = i + 1;
+            const uint64_t st = e < v.size() ? v[e] - v[i] : 1;
+            while (e < v.size() && v[e] - v[e - 1] == st) ++e;
+            ++runs;
+            i = e;
+        }
+        auto& c = by_m[m];
+        c.first += 1;
+        c.second += runs;
+    }
+    for (const auto& kv : by_m)
+        if (kv.second.first > 1 && kv.second.second > kern::kMaxSegs) return true;
+    return false;
+}
+
 }  // namespace
 
 int ptrs_launch(Codec& c, const uint64_t* tab, const uint8_t* present, size_t nblocks, uint64_t len, bool data_only,
@@ -132,7 +168,8 @@ int ptrs_launch(Codec& c, const uint64_t* tab, const uint8_t* present, size_t nb
     if (nblocks == 0) return SHMR_EC_OK;
     if (ptrs_grid()) {
         LatticeForm F;
-        if (lattice_form(k, t, tab, present, nblocks, data_only, op, host_mapped, &F)) {
+        if (lattice_form(k, t, tab, present, nblocks, data_only, op, host_mapped, &F) &&
+            !(op == kDecode && lattice_needs_plan_list(t, present, F))) {
             int rc;
             if (op == kEncode) {
                 rc = encode_on_device(c, device, F.L, F.rows.size(), len, stream, F.slots.data());

@@ -62,7 +62,7 @@ def test_pool_alloc_free_rules(gpu):
 def test_pool_churn_encode_and_rebuild(gpu, k, p, S):
     """Rounds of churn (random frees and allocs), then an encode and an
     in-place rebuild of every live block (random erasures, mixed patterns) in
-    shuffled table order: the oracle's bytes, every call on the lattice path,
+    shuffled table order: the oracle's bytes, the encode on the lattice path,
     and free slots untouched."""
     import torch
     t = k + p
@@ -109,7 +109,9 @@ def test_pool_churn_encode_and_rebuild(gpu, k, p, S):
         torch.cuda.synchronize()
         assert rs._L.shmr_ec_reconstruct_ptrs_dev(rs._h, tab, _ptr(present), B, S, 0, 0, _stream()) == 0
         torch.cuda.synchronize()
-        assert shmr_amd.device_stats(0)["ptr_table_grids"] == g0 + 2
+        # (mixed patterns in more runs than the kernel arguments hold take the
+        # table kernels: ptrs.cpp lattice_needs_plan_list)
+        assert shmr_amd.device_stats(0)["ptr_table_grids"] in (g0 + 1, g0 + 2)
         for b in range(B):
             for i in range(t):
                 assert np.array_equal(pool.shard(rows[b], i).cpu().numpy(), full[b, i]), (rnd, b, i)
@@ -148,3 +150,37 @@ def test_pool_blocks_through_the_queue(gpu):
     for b in range(n):
         for r in range(p):
             assert np.array_equal(pool.shard(blocks[b], k + r).cpu().numpy(), want[b, r])
+
+
+def test_pool_failed_disk_rebuild_on_the_lattice(gpu):
+    """A failed disk: every live block of a holed pool lost the same shard --
+    one pattern, rebuilt in place over the slots (lattice path: a run list or
+    segment runs), exact, nothing else written."""
+    import torch
+    k, p, S = 8, 3, 65536
+    t = k + p
+    rs = shmr_amd.ReedSolomon(k, p)
+    pool = shmr_amd.ShardPool(t, S, 80)
+    live = [pool.alloc() for _ in range(80)]
+    rng = np.random.default_rng(8)
+    for j in sorted(rng.choice(80, size=20, replace=False).tolist(), reverse=True):
+        pool.free(live.pop(j))
+    rows = np.stack([live[int(j)] for j in rng.permutation(len(live))])
+    B = len(rows)
+    data = rng.integers(0, 256, (B, k, S), dtype=np.uint8)
+    full = np.concatenate([data, _parity(k, p, data)], axis=1)
+    for b in range(B):
+        for i in range(t):
+            pool.shard(rows[b], i).copy_(torch.from_numpy(full[b, i]).to(gpu))
+        pool.shard(rows[b], 5).fill_(0xEE)
+    torch.cuda.synchronize()
+    present = np.ones((B, t), np.uint8)
+    present[:, 5] = 0
+    g0 = shmr_amd.device_stats(0)["ptr_table_grids"]
+    keep, tab = _tab(rows)
+    assert rs._L.shmr_ec_reconstruct_ptrs_dev(rs._h, tab, _ptr(present), B, S, 0, 0, _stream()) == 0
+    torch.cuda.synchronize()
+    assert shmr_amd.device_stats(0)["ptr_table_grids"] == g0 + 1
+    for b in range(B):
+        for i in range(t):
+            assert np.array_equal(pool.shard(rows[b], i).cpu().numpy(), full[b, i]), (b, i)

@@ -6,7 +6,7 @@
 # interleaved twice; the CPU leg's shard files are compared byte for byte with
 # the GPU leg's (same ino / idx naming).
 set -o pipefail
-O=gpurun_out/r06cfg5
+O=gpurun_out/r06cfg5c
 mkdir -p $O
 B=/tmp/shmr_cfg5
 for round in 1 2; do
@@ -14,6 +14,7 @@ for round in 1 2; do
     rm -rf $B && mkdir -p $B/gpu $B/cpu || exit 1
     SHMR_VFS_KEEP_FILES=1 SHMR_VFS_PINNED_ONLY=1 timeout -k 10 300 shmr_amd/_lib/shmr_vfs_bench $B/gpu 256 4 $fs 3 >> $O/gpu_vfs.jsonl 2>> $O/gpu_vfs.err || exit 1
     timeout -k 10 300 tools/_abx/ref_cpu_vfs $B/cpu 256 4 $fs 3 16 $B/gpu 1003 >> $O/cpu_ref.jsonl 2>> $O/cpu_ref.err || exit 1
+    REF_CPU_REUSE=1 timeout -k 10 300 tools/_abx/ref_cpu_vfs $B/cpu 256 4 $fs 3 16 $B/gpu 1003 >> $O/cpu_ref.jsonl 2>> $O/cpu_ref.err || exit 1
   done
 done
 rm -rf $B

@@ -15,7 +15,8 @@
 //          buffer.chunks(S) -> to_vec, the last chunk zero-padded, zero shards up
 //          to k + p, ReedSolomon::encode, then write_path per shard in index order
 //          (block.rs:611-634: write_all_at(buf, 0), sync_all -- here pwrite at 0
-//          and fsync when fsync=1).
+//          and fsync when fsync=1) on the handle open_handles opens (the files
+//          themselves are created with the block, VirtualBlock::create, untimed).
 //   read   VirtualFile::read (mod.rs:140-175): blocks in sequence, each
 //          VirtualBlock::read -> load_block (block.rs:529-579): read_to_end of
 //          every shard file (a missing file: None -- the C++ mirror's
@@ -124,22 +125,49 @@ struct Block {
     std::vector<std::string> files;
 };
 
+// REF_CPU_REUSE=1: every thread keeps its shard Vecs across blocks (no fresh
+// allocation per flush / load) -- the CPU path's floor without the allocator;
+// off (default): fresh Vecs as the reference allocates them (to_vec, vec![0; S],
+// read_to_end, ec_data), through glibc malloc like Rust's default allocator.
+bool g_reuse = false;
+// thread time per phase of the last timed flush / parallel load (ns, summed over threads)
+std::atomic<uint64_t> g_t_copy{0}, g_t_code{0}, g_t_io{0}, g_t_concat{0};
+inline uint64_t ns_now() {
+    return uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                         std::chrono::steady_clock::now().time_since_epoch()).count());
+}
+
 // VirtualBlock::sync_data, Erasure arm (block.rs:404-440)
 void flush(Block& b, uint64_t size, bool do_fsync) {
     const size_t S = shard_size(size, K);
-    std::vector<std::vector<uint8_t>> shards;
-    for (size_t off = 0; off < b.buffer.size(); off += S) {   // buffer.chunks(S).map(to_vec)
+    const uint64_t t0 = ns_now();
+    thread_local std::vector<std::vector<uint8_t>> kept;
+    std::vector<std::vector<uint8_t>> fresh;
+    std::vector<std::vector<uint8_t>>& shards = g_reuse ? kept : fresh;
+    if (g_reuse) shards.resize(T);
+    size_t j = 0;
+    for (size_t off = 0; off < b.buffer.size(); off += S, ++j) {   // buffer.chunks(S).map(to_vec)
         const size_t n = std::min(S, b.buffer.size() - off);
-        std::vector<uint8_t> r(b.buffer.begin() + long(off), b.buffer.begin() + long(off + n));
-        if (r.size() < S) r.resize(S, 0);
-        shards.push_back(std::move(r));
+        if (g_reuse) {
+            shards[j].assign(b.buffer.begin() + long(off), b.buffer.begin() + long(off + n));
+        } else {
+            shards.emplace_back(b.buffer.begin() + long(off), b.buffer.begin() + long(off + n));
+        }
+        if (shards[j].size() < S) shards[j].resize(S, 0);
     }
-    while (shards.size() < T) shards.emplace_back(S, 0);
+    for (; j < T; ++j) {   // zero shards up to k + p
+        if (g_reuse) shards[j].assign(S, 0);
+        else shards.emplace_back(S, 0);
+    }
     uint8_t* ptrs[T];
     for (uint32_t i = 0; i < T; ++i) ptrs[i] = shards[i].data();
+    const uint64_t t1 = ns_now();
     if (oracle_encode(1, K, P, ptrs, S) != 0) die("encode");
+    const uint64_t t2 = ns_now();
+    g_t_copy += t1 - t0;
+    g_t_code += t2 - t1;
     for (uint32_t i = 0; i < T; ++i) {   // write_path: write_all_at(buf, 0) + sync_all
-        const int fd = ::open(b.files[i].c_str(), O_WRONLY | O_CREAT, 0644);
+        const int fd = ::open(b.files[i].c_str(), O_WRONLY);   // open_handles (block.rs:455-493)
         if (fd < 0) die("open for write");
         size_t done = 0;
         while (done < S) {
@@ -150,12 +178,17 @@ void flush(Block& b, uint64_t size, bool do_fsync) {
         if (do_fsync && ::fsync(fd) != 0) die("fsync");
         ::close(fd);
     }
+    g_t_io += ns_now() - t2;
 }
 
 // VirtualBlock::load_block, Erasure arm (block.rs:529-579), then the read's copy-out
 void load(Block& b, uint64_t size, uint8_t* out) {
     const size_t S = shard_size(size, K);
-    std::vector<std::vector<uint8_t>> shards(T);
+    const uint64_t t0 = ns_now();
+    thread_local std::vector<std::vector<uint8_t>> kept(T);
+    std::vector<std::vector<uint8_t>> fresh(T);
+    std::vector<std::vector<uint8_t>>& shards = g_reuse ? kept : fresh;
+    for (auto& v : shards) v.clear();
     uint8_t present[T];
     bool missing = false;
     for (uint32_t i = 0; i < T; ++i) {
@@ -182,6 +215,8 @@ void load(Block& b, uint64_t size, uint8_t* out) {
         }
         present[i] = 1;
     }
+    const uint64_t t1 = ns_now();
+    g_t_io += t1 - t0;
     if (missing) {   // r.reconstruct(&mut ec_shards): every None filled (vec![0; S])
         uint8_t* ptrs[T];
         for (uint32_t i = 0; i < T; ++i) {
@@ -190,10 +225,16 @@ void load(Block& b, uint64_t size, uint8_t* out) {
         }
         if (oracle_reconstruct_v(1, K, P, ptrs, present, S, 0) != 0) die("reconstruct");
     }
-    std::vector<uint8_t> ec_data;   // every shard concatenated
+    const uint64_t t2 = ns_now();
+    g_t_code += t2 - t1;
+    thread_local std::vector<uint8_t> kept_data;
+    std::vector<uint8_t> fresh_data;
+    std::vector<uint8_t>& ec_data = g_reuse ? kept_data : fresh_data;   // every shard concatenated
+    ec_data.clear();
     for (uint32_t i = 0; i < T; ++i) ec_data.insert(ec_data.end(), shards[i].begin(), shards[i].end());
     b.buffer.assign(ec_data.begin(), ec_data.begin() + long(size));   // buffer.copy_from_slice(&ec_data[..size])
     std::memcpy(out, b.buffer.data(), size);   // VirtualBlock::read into the FUSE buffer
+    g_t_concat += ns_now() - t2;
 }
 
 }  // namespace
@@ -213,6 +254,7 @@ int main(int argc, char** argv) {
     const std::string compare = argc > 7 ? argv[7] : "";
     const uint64_t ino = argc > 8 ? std::strtoull(argv[8], nullptr, 10) : 1000;
     fs::create_directories(bucket);
+    g_reuse = std::getenv("REF_CPU_REUSE") && std::atoi(std::getenv("REF_CPU_REUSE")) != 0;
     const uint64_t bsz = block_mib << 20;
     std::vector<uint8_t> src(file_mib << 20);   // shmr_vfs_bench's bytes (same generator and seed)
     std::mt19937_64 rng(0x53484D52);
@@ -225,19 +267,34 @@ int main(int argc, char** argv) {
     double best_w = 1e30, best_s = 1e30, best_rs = 1e30, best_rp = 1e30;
     bool verified = true;
     long compared = -1;
+    double flush_ms[3] = {0, 0, 0}, load_ms[3] = {0, 0, 0};
     for (int rep = 0; rep < reps + 1; ++rep) {   // rep 0 warms the page cache and the pool
         std::vector<Block> blocks(nblk);
         for (size_t i = 0; i < nblk; ++i)
             for (uint32_t s = 0; s < T; ++s) blocks[i].files.push_back(bucket + "/" + shard_name(ino, i + 1, s));
+        // VirtualBlock::create (block.rs:207-266): every shard file created (and
+        // truncated) when the block is made -- before the flush, as in the GPU leg
+        for (auto& b : blocks)
+            for (auto& f : b.files) {
+                const int fd = ::open(f.c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0644);
+                if (fd < 0) die("create");
+                ::close(fd);
+            }
         double t = now_s();
         for (size_t i = 0; i < nblk; ++i) {   // VirtualFile::write: bytes into each block's Vec
             blocks[i].buffer.resize(bsz);
             std::memcpy(blocks[i].buffer.data(), src.data() + i * bsz, bsz);
         }
         const double w = now_s() - t;
+        g_t_copy = g_t_code = g_t_io = 0;
         t = now_s();
         pool.run(nblk, [&](size_t i) { flush(blocks[i], bsz, do_fsync); });
         const double s = now_s() - t;
+        if (rep == reps) {
+            flush_ms[0] = g_t_copy / 1e6 / double(nblk);
+            flush_ms[1] = g_t_code / 1e6 / double(nblk);
+            flush_ms[2] = g_t_io / 1e6 / double(nblk);
+        }
         if (rep == reps && !compare.empty()) {   // byte equality with the GPU leg's files
             compared = 0;
             for (size_t i = 0; i < nblk; ++i)
@@ -266,9 +323,15 @@ int main(int argc, char** argv) {
         verified = verified && back == src;
         for (auto& b : blocks) std::vector<uint8_t>().swap(b.buffer);
         std::fill(back.begin(), back.end(), 0);
+        g_t_code = g_t_io = g_t_concat = 0;
         t = now_s();
         pool.run(nblk, [&](size_t i) { load(blocks[i], bsz, back.data() + i * bsz); });
         const double rp = now_s() - t;
+        if (rep == reps) {
+            load_ms[0] = g_t_io / 1e6 / double(nblk);
+            load_ms[1] = g_t_code / 1e6 / double(nblk);
+            load_ms[2] = g_t_concat / 1e6 / double(nblk);
+        }
         verified = verified && back == src;
         for (auto& b : blocks)
             for (auto& f : b.files) fs::remove(f);
@@ -279,14 +342,19 @@ int main(int argc, char** argv) {
         best_rp = std::min(best_rp, rp);
     }
     const double GiB = double(1ull << 30), bytes = double(src.size());
-    std::printf("{\"leg\": \"reference CPU path (oracle AVX2 restatement of the crate)\", \"avx2\": %s, "
+    std::printf("{\"leg\": \"reference CPU path (oracle AVX2 restatement of the crate)\", \"shard_vecs\": \"%s\", "
+                "\"avx2\": %s, "
                 "\"threads\": %d, \"file_MiB\": %llu, \"block_MiB\": %llu, \"topology\": \"Erasure(1, 8, 3)\", "
                 "\"fsync\": %d, \"reps\": %d, \"unit\": \"GiB/s of file data (best rep)\", "
                 "\"write_GiBps\": %.2f, \"sync_GiBps\": %.2f, \"read_with_erasure_sequential_GiBps\": %.2f, "
                 "\"read_with_erasure_parallel_GiBps\": %.2f, \"files_compared_with_gpu_leg\": %ld, "
-                "\"verified\": %s}\n",
+                "\"ms_per_block_thread_time\": {\"flush_chunk_copy\": %.3f, \"flush_encode\": %.3f, "
+                "\"flush_shard_writes\": %.3f, \"load_shard_reads\": %.3f, \"load_reconstruct\": %.3f, "
+                "\"load_concat_copy_out\": %.3f}, \"verified\": %s}\n",
+                g_reuse ? "kept per thread (allocator excluded)" : "fresh per block (the reference)",
                 oracle_has_avx2() ? "true" : "false", threads, (unsigned long long)file_mib,
                 (unsigned long long)block_mib, int(do_fsync), reps, bytes / best_w / GiB, bytes / best_s / GiB,
-                bytes / best_rs / GiB, bytes / best_rp / GiB, compared, verified ? "true" : "false");
+                bytes / best_rs / GiB, bytes / best_rp / GiB, compared, flush_ms[0], flush_ms[1], flush_ms[2],
+                load_ms[0], load_ms[1], load_ms[2], verified ? "true" : "false");
     return verified ? 0 : 1;
 }
