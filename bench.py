@@ -478,9 +478,9 @@ class Workload:
     def timed(self, steps):
         """K steps bracketed by two HIP events on this device's stream (nothing
         else between the launches: an event after every step measured 0.9 %
-        slower, profiles/r05/s8/gap_probe.txt); returns the K per-step times in
-        ms -- each the average over the region (the stream is drained on
-        return)."""
+        slower, profiles/r05/s8/gap_probe.txt); returns the region's
+        milliseconds, one figure for the K steps (no per-step spread is
+        measured; the stream is drained on return)."""
         with torch.cuda.device(self.dev), torch.cuda.stream(self.stream):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(self.stream)
@@ -488,7 +488,7 @@ class Workload:
                 self.step()
             e1.record(self.stream)
             self.stream.synchronize()
-        return [e0.elapsed_time(e1) / steps] * steps
+        return e0.elapsed_time(e1)
 
     def round_trip(self):
         """codec configs: the timed steps ran over already-consistent blocks --
@@ -577,7 +577,12 @@ def report(args, shape, world, ranks, elapsed, step_ms, ramp_steps, process_mode
         "dtype": "u8",
         "data": "synthetic uniform random bytes generated on-device (torch.randint, seeded per rank)",
         "config": {
-            "workload": WORKLOADS[args.config],
+            "workload": WORKLOADS[args.config] + ("" if args.layout != "ptrs" else
+                                                   " +ptrs_slab (pointer tables over shmr_ec_device_alloc_shards "
+                                                   "slabs: a slot grid, strided kernels)"
+                                                   if args.ptrs_alloc == "slab" else
+                                                   " +ptrs_torch (pointer tables over torch buffers: the table "
+                                                   "kernels)"),
             "data_shards": shape.k, "parity_shards": shape.p, "shard_bytes": shape.S, "blocks_per_gpu": B,
             "global_batch_blocks": B * world,
             "parallelism": (f"blocks round-robin over {world} GPU(s), no data-path collectives " +
@@ -711,15 +716,17 @@ def run(args):
     torch.cuda.synchronize(dev)
     grids0 = shmr_amd.device_stats(dev.index)["ptr_table_grids"]
     t0 = time.perf_counter()
-    step_ms = w.timed(args.steps)
+    region_ms = w.timed(args.steps)
+    step_ms = region_ms / args.steps
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     grid_calls = shmr_amd.device_stats(dev.index)["ptr_table_grids"] - grids0
     if world > 1:
         dist.barrier()
-    elapsed = max(wall, sum(step_ms) / 1e3)
+    elapsed = max(wall, region_ms / 1e3)
     elapsed = placement.max_over_ranks(elapsed, device=dev if args.backend == "nccl" else None)
     out = report(args, shape, world, ranks, elapsed, step_ms, ramp_steps, "process")
+    out["roofline"]["timed_region"] = {"steps": args.steps, "events_ms": round(region_ms, 4)}
     if args.layout == "ptrs":
         # pointer-table calls of the timed steps that ran as a slot grid (strided kernels)
         out["config"]["ptr_table_grid_calls_timed"] = grid_calls
@@ -769,8 +776,8 @@ def run_single(args):
     results, wall = placement.fan_out([w.ramp_and_warmup for w in works], [lambda w=w: w.timed(args.steps)
                                                                              for w in works])
     ramp_steps = max(r[0] for r in results)
-    per_dev_ms = [r[1] for r in results]
-    dev_s = [sum(ms) / 1e3 for ms in per_dev_ms]
+    per_dev_ms = [r[1] / args.steps for r in results]        # event-timed region / K steps
+    dev_s = [r[1] / 1e3 for r in results]
     slowest = int(np.argmax(dev_s))
     elapsed = max(wall, max(dev_s))
     extra = {"per_device": [{"device": ranks[d], "ms_per_step": round(dev_s[d] / args.steps * 1e3, 4),
@@ -837,7 +844,9 @@ def traffic_key(args) -> str:
     decode rebuilt in place (the compact output is the default)."""
     key = args.config
     if args.layout == "ptrs":
-        return key + ("+ptrs" if args.ptrs_alloc == "slab" else "+ptrs_torch")
+        # (r06: "+ptrs_slab" -- slab buffers on a slot grid, the strided kernels --
+        # is not the table-kernel workload that "+ptrs" named before r05)
+        return key + ("+ptrs_slab" if args.ptrs_alloc == "slab" else "+ptrs_torch")
     if args.pitch_align == 1:
         key += "+packed"
     elif args.pitch_pad == 0:

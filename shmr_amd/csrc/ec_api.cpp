@@ -56,9 +56,15 @@ int guarded_light(F&& f) noexcept {
         return SHMR_EC_DEVICE_ERROR;
     }
 }
-// Slabs handed out by shmr_ec_device_alloc_shards (base -> device).
+// Slabs handed out by shmr_ec_device_alloc_shards (base -> device; `freeing`
+// while a shmr_ec_device_free_shards of it runs: one of two racing frees wins,
+// and a failed free leaves the entry, so the slab can still be freed).
+struct SlabEntry {
+    int device;
+    bool freeing;
+};
 std::mutex g_slab_mu;
-std::map<uintptr_t, int> g_slabs;
+std::map<uintptr_t, SlabEntry> g_slabs;
 }  // namespace
 
 extern "C" {
@@ -303,18 +309,28 @@ int shmr_ec_device_free(int device, void* p) {
         if (!p) return SHMR_EC_OK;
         int rc = core::check_device(device);
         if (rc) return rc;
-        {   // a slab freed this way leaves no registry entry for a later
-            // allocation at the same address to inherit
+        // A slab freed this way leaves no registry entry for a later allocation
+        // at the same address to inherit: dropped now (the address is still
+        // ours) -- unless free_shards is freeing it, which keeps the entry until
+        // the memory is gone, so a failed free can be retried.
+        {
             std::lock_guard<std::mutex> lk(g_slab_mu);
             auto it = g_slabs.find(uintptr_t(p));
-            if (it != g_slabs.end() && it->second == device) g_slabs.erase(it);
+            if (it != g_slabs.end() && it->second.device == device && !it->second.freeing) g_slabs.erase(it);
         }
-        core::DeviceScope scope(device);
-        if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
-        core::RelaxedCapture relaxed;
-        if (hipFree(p) == hipSuccess) return SHMR_EC_OK;
-        (void)hipGetLastError();
-        return SHMR_EC_DEVICE_ERROR;
+        {
+            core::DeviceScope scope(device);
+            if (!scope.ok()) return SHMR_EC_DEVICE_ERROR;
+            core::RelaxedCapture relaxed;
+            if (hipFree(p) != hipSuccess) {
+                (void)hipGetLastError();
+                return SHMR_EC_DEVICE_ERROR;
+            }
+        }
+        std::lock_guard<std::mutex> lk(g_slab_mu);
+        auto it = g_slabs.find(uintptr_t(p));   // (an entry a new slab at this address made is not ours)
+        if (it != g_slabs.end() && it->second.device == device && it->second.freeing) g_slabs.erase(it);
+        return SHMR_EC_OK;
     });
 }
 
@@ -335,7 +351,7 @@ int shmr_ec_device_alloc_shards(int device, size_t nblocks, size_t shards_per_bl
         if (rc) return rc;
         try {
             std::lock_guard<std::mutex> lk(g_slab_mu);
-            g_slabs[uintptr_t(slab)] = device;
+            g_slabs[uintptr_t(slab)] = SlabEntry{device, false};
         } catch (...) {
             (void)shmr_ec_device_free(device, slab);
             throw;
@@ -352,10 +368,17 @@ int shmr_ec_device_free_shards(int device, uint8_t* first) {
         {
             std::lock_guard<std::mutex> lk(g_slab_mu);
             auto it = g_slabs.find(uintptr_t(first));
-            if (it == g_slabs.end() || it->second != device) return SHMR_EC_INVALID_ARGUMENT;
-            g_slabs.erase(it);   // under the lock: one of two racing frees wins
+            if (it == g_slabs.end() || it->second.device != device || it->second.freeing)
+                return SHMR_EC_INVALID_ARGUMENT;
+            it->second.freeing = true;   // under the lock: one of two racing frees wins
         }
-        return shmr_ec_device_free(device, first);
+        const int rc = shmr_ec_device_free(device, first);   // erases the entry once freed
+        if (rc) {
+            std::lock_guard<std::mutex> lk(g_slab_mu);
+            auto it = g_slabs.find(uintptr_t(first));
+            if (it != g_slabs.end()) it->second.freeing = false;   // still allocated: freeable again
+        }
+        return rc;
     });
 }
 

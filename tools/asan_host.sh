@@ -5,7 +5,8 @@
 #
 #   tools/asan_host.sh build
 #   tools/asan_host.sh run [out_dir]      # every case of shmr_vfs_test
-#   LEAKS=1 tools/asan_host.sh run [dir]  # with LeakSanitizer (ROCm runtime suppressed)
+#   (no LeakSanitizer here: leaks are checked on the CPU build, tests/test_host_asan.py -- r06,
+#   see the `run` case)
 set -euo pipefail
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
 BIN="$ROOT/tools/_probe/vfs_test_asan"
@@ -33,7 +34,7 @@ build)
     # pointer; launch_one now launches by kernel name, and
     # tests/test_isa.py checks every launch site still pops its configuration.
     $HIPCC $CXXF $SAN --offload-arch=gfx950 -x hip -c "$C/gf_apply.hip" -o "$L/gf_apply.o"
-    for f in gf256 ec_core host_engine ec_api; do
+    for f in gf256 ec_core host_engine ptrs submit pool ec_api; do
         $HIPCC $CXXF $SAN -c "$C/$f.cpp" -o "$L/$f.o"
     done
     $HIPCC --offload-arch=gfx950 -shared -fPIC $SAN -o "$L/libshmr_ec.so" "$L"/*.o -Wl,-soname,libshmr_ec.so -lpthread
@@ -50,12 +51,20 @@ run)
     # protect_shadow_gap=0: the ROCm runtime maps GPU apertures in the low shadow gap
     # LEAKS=1: LeakSanitizer on, the ROCm runtime's own allocations suppressed
     # (tools/lsan_rocm.supp); this repository's code stays checked
+    # LeakSanitizer stays off on the GPU box (r06): twice (r05, profiles/r05/s27) a
+    # case passed and then hung at exit with every thread stopped in
+    # ptrace_stop by LeakSanitizer's exit-time StopTheWorld, while the leak scan
+    # walked a process whose address space holds the ROCm runtime's device
+    # apertures; the record lacks the tracer task, so the hang is the checker's
+    # or the runtime's, not this code's, and re-running it costs GPU sessions
+    # for no finding.  Leaks are checked where no runtime mapping exists: the
+    # CPU build of every StorageBlock case under ASan + LSan + UBSan in the CPU
+    # suite (tests/test_host_asan.py), which found the one leak there was.
     if [ "${LEAKS:-0}" = 1 ]; then
-        export ASAN_OPTIONS=detect_leaks=1:protect_shadow_gap=0:halt_on_error=1
-        export LSAN_OPTIONS="suppressions=$ROOT/tools/lsan_rocm.supp:print_suppressions=0"
-    else
-        export ASAN_OPTIONS=detect_leaks=0:protect_shadow_gap=0:halt_on_error=1
+        echo "LEAKS=1 is not run on the GPU box (see the comment above; tests/test_host_asan.py checks leaks)" >&2
+        exit 2
     fi
+    export ASAN_OPTIONS=detect_leaks=0:protect_shadow_gap=0:halt_on_error=1
     export UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1
     fail=0
     T="${CASE_TIMEOUT:-120}"     # seconds per case (LeakSanitizer's exit scan adds to the long cases)

@@ -30,10 +30,10 @@ KEY=decode83+contig BENCH_EXTRA="--pitch-pad 0" bash "$D/profile.sh" "$T" decode
 fi
 # every shard its own buffer, named by a pointer table (the crate's shape, --layout ptrs): r05 slab
 # buffers from shmr_ec_device_alloc_shards (a slot grid: strided kernels), and torch allocations
-KEY=encode83+ptrs BENCH_EXTRA="--layout ptrs" bash "$D/profile.sh" "$T" encode83 512 2952790016
-KEY=decode83+ptrs BENCH_EXTRA="--layout ptrs" bash "$D/profile.sh" "$T" decode83 512 2415919104
-KEY=encode104+ptrs BENCH_EXTRA="--layout ptrs" bash "$D/profile.sh" "$T" encode104 64 $((64 * 14 * 1677722))
-KEY=decode104+ptrs BENCH_EXTRA="--layout ptrs" bash "$D/profile.sh" "$T" decode104 64 $((64 * 12 * 1677722))
+KEY=encode83+ptrs_slab BENCH_EXTRA="--layout ptrs" bash "$D/profile.sh" "$T" encode83 512 2952790016
+KEY=decode83+ptrs_slab BENCH_EXTRA="--layout ptrs" bash "$D/profile.sh" "$T" decode83 512 2415919104
+KEY=encode104+ptrs_slab BENCH_EXTRA="--layout ptrs" bash "$D/profile.sh" "$T" encode104 64 $((64 * 14 * 1677722))
+KEY=decode104+ptrs_slab BENCH_EXTRA="--layout ptrs" bash "$D/profile.sh" "$T" decode104 64 $((64 * 12 * 1677722))
 KEY=encode83+ptrs_torch BENCH_EXTRA="--layout ptrs --ptrs-alloc torch" bash "$D/profile.sh" "$T" encode83 512 2952790016
 KEY=decode83+ptrs_torch BENCH_EXTRA="--layout ptrs --ptrs-alloc torch" bash "$D/profile.sh" "$T" decode83 512 2415919104
 KEY=encode104+ptrs_torch BENCH_EXTRA="--layout ptrs --ptrs-alloc torch" bash "$D/profile.sh" "$T" encode104 64 $((64 * 14 * 1677722))
