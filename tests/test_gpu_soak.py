@@ -29,5 +29,7 @@ def test_soak_slice(gpu):
     for t in th:
         t.join(90)
     assert not any(t.is_alive() for t in th), "a soak thread did not finish"
+    for e in errors[:5]:
+        print(*e, sep="\n", flush=True)
     assert errors == [], errors[:5]
     assert sum(counts) > 100, counts

@@ -9,7 +9,8 @@
 #   see the `run` case)
 set -euo pipefail
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
-BIN="$ROOT/tools/_probe/vfs_test_asan"
+PROBE="${ASAN_DIR:-$ROOT/tools/_probe}"   # run: a copy of the build elsewhere (tools/_probe is not uploaded)
+BIN="$PROBE/vfs_test_asan"
 HIPCC=/opt/rocm/bin/hipcc
 CPU_CASES="block_topology_try_from virtual_block_new_block virtual_block_unbuffered_backing virtual_block_unbuffered
 virtual_block_buffered virtual_block_erasure_buffered block_errors virtual_file_1 virtual_file_2_4_mb virtual_file_errors
@@ -68,7 +69,7 @@ run)
     export UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1
     fail=0
     T="${CASE_TIMEOUT:-120}"     # seconds per case (LeakSanitizer's exit scan adds to the long cases)
-    if timeout -k 10 "$T" "$ROOT/tools/_probe/abi_check_asan" > "$OUT/abi_check.log" 2>&1; then
+    if timeout -k 10 "$T" "$PROBE/abi_check_asan" > "$OUT/abi_check.log" 2>&1; then
         echo "abi_check PASS"
     else
         echo "abi_check FAIL (see $OUT/abi_check.log)"; exit 1

@@ -6,7 +6,9 @@ buffers (zero-copy, bounce, staged DMA), host batches on pageable arrays
 torch streams, per-shard device buffers through pointer tables (reused, so
 the device's table cache hits), started per-block calls (shmr_ec_*_start) and
 pointer-table encodes captured into graphs and destroyed again (the capture
-reserve) -- several (k, p) codecs and shard lengths (aligned, tail,
+reserve), device Block Cache slots after churn (shmr_ec_pool_*) through the
+submission queue's merged per-block calls and through pointer-table batches --
+several (k, p) codecs and shard lengths (aligned, tail,
 byte-granular) at once.  Not part of the test suite (minutes of GPU time).
 
     python tools/soak.py [--seconds 120] [--threads 12]
@@ -42,10 +44,10 @@ def oracle_encode(k, p, data):
 class CaptureGate:
     """Graph captures (op 6) against the legacy default stream: torch work on the
     null stream (op 4's default-stream branch, the .cpu() reads and allocations
-    outside a stream context in ops 3-4) synchronises implicitly with every
+    outside a stream context in ops 3-4, 7-9) synchronises implicitly with every
     stream and would join -- and invalidate -- another thread's capture (a
     HIP / CUDA rule, not the library's).  Captures run exclusively against ops
-    3-4; the host-buffer ops (0-2, 5), which use only the library's own
+    3-4 and 7-9; the host-buffer ops (0-2, 5), which use only the library's own
     non-blocking streams, run alongside them."""
 
     def __init__(self):
@@ -95,7 +97,7 @@ class _Nothing:
         return False
 
 
-def worker(tid, deadline, errors, counts, ops=tuple(range(8)), shapes=tuple(range(len(SHAPES)))):
+def worker(tid, deadline, errors, counts, ops=tuple(range(10)), shapes=tuple(range(len(SHAPES)))):
     rng = np.random.default_rng([tid, 2024])
     stream = torch.cuda.Stream()
     slab = shmr_amd.PinnedBuffer(4 * 24 * 524288)
@@ -104,7 +106,7 @@ def worker(tid, deadline, errors, counts, ops=tuple(range(8)), shapes=tuple(rang
         k, p, L = SHAPES[shapes[int(rng.integers(0, len(shapes)))]]
         rs = shmr_amd.ReedSolomon(k, p)
         op = ops[int(rng.integers(0, len(ops)))]
-        gate = GATE.exclusive() if op == 6 else GATE.shared() if op in (3, 4, 7) else _Nothing()
+        gate = GATE.exclusive() if op == 6 else GATE.shared() if op in (3, 4, 7, 8, 9) else _Nothing()
         try:
             with gate:
                 if op == 0:        # per-block calls, pageable or mapped
@@ -281,6 +283,83 @@ def worker(tid, deadline, errors, counts, ops=tuple(range(8)), shapes=tuple(rang
                                    for j, i in enumerate(np.flatnonzero(present[b] == 0))):
                             errors.append((tid, "slab rebuild fresh", k, p, L, B))
                             break
+                elif op in (8, 9):  # device Block Cache slots (shmr_ec_pool_*) after churn, blocks in shuffled
+                    #                 order: per-block calls through the submission queue (8: plain or
+                    #                 started, merged with other threads' calls) or one pointer-table
+                    #                 batch on this thread's stream (9: the slot lattice or the table path)
+                    import ctypes
+                    from shmr_amd.reed_solomon import _ptr, _u8p
+                    key = ("pool", k, p, L)
+                    if key not in kept:
+                        kept[key] = (shmr_amd.ShardPool(k + p, L, 8), [])
+                    pool, live = kept[key]
+                    for _ in range(int(rng.integers(0, 6))):    # churn (past 8 live blocks: a second slab)
+                        if live and rng.integers(0, 2):
+                            pool.free(live.pop(int(rng.integers(0, len(live)))))
+                        elif len(live) < 12:
+                            live.append(pool.alloc())
+                    if not live:
+                        live.append(pool.alloc())
+                    order = [live[int(j)] for j in rng.permutation(len(live))]
+                    B = len(order)
+                    host = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+                    with torch.cuda.stream(stream):
+                        hd = torch.from_numpy(host).cuda()
+                        for b in range(B):
+                            for i in range(k):
+                                pool.shard(order[b], i).copy_(hd[b, i])
+                    stream.synchronize()                        # queue inputs complete before the call
+                    present = np.ones((B, k + p), np.uint8)
+                    for b in range(B):
+                        present[b, rng.choice(k + p, size=int(rng.integers(1, p + 1)), replace=False)] = 0
+                    data_only = op == 8 and bool(rng.integers(0, 4) == 0)
+                    start = bool(rng.integers(0, 2))
+                    tab = np.ascontiguousarray(np.stack(order))
+                    sp = ctypes.c_void_p(stream.cuda_stream)
+                    if op == 8:
+                        pend = [rs.encode_dev([(int(a), L) for a in blk], start=start) for blk in order]
+                        for o in pend:
+                            if o is not None:
+                                o.wait()
+                    else:
+                        assert rs._L.shmr_ec_encode_ptrs_dev(rs._h, tab.ctypes.data_as(ctypes.POINTER(_u8p)), B, L, 0,
+                                                             sp) == 0
+                    with torch.cuda.stream(stream):
+                        enc = torch.stack([torch.stack([pool.shard(blk, i) for i in range(k + p)]) for blk in order])
+                        full = enc.cpu().numpy()
+                        for b in range(B):
+                            for i in np.flatnonzero(present[b] == 0):
+                                pool.shard(order[b], int(i)).fill_(0xEE)
+                    stream.synchronize()
+                    bad = False
+                    for b in range(B):
+                        want = oracle_encode(k, p, list(host[b]))
+                        if not all(np.array_equal(full[b, i], want[i]) for i in range(k, k + p)):
+                            errors.append((tid, "pool encode", op, k, p, L, B))
+                            bad = True
+                            break
+                    if bad:
+                        continue
+                    if op == 8:
+                        pend = []
+                        for b, blk in enumerate(order):
+                            row = [None if (data_only and i >= k and not present[b, i]) else (int(blk[i]), L)
+                                   for i in range(k + p)]
+                            pend.append(rs.reconstruct_dev(row, present[b], data_only=data_only, start=start))
+                        for o in pend:
+                            if o is not None:
+                                o.wait()
+                    else:
+                        assert rs._L.shmr_ec_reconstruct_ptrs_dev(rs._h, tab.ctypes.data_as(ctypes.POINTER(_u8p)),
+                                                                  _ptr(present), B, L, 0, 0, sp) == 0
+                    with torch.cuda.stream(stream):
+                        got = torch.stack([torch.stack([pool.shard(blk, i) for i in range(k + p)])
+                                           for blk in order]).cpu().numpy()
+                    for b in range(B):
+                        rows = range(k) if data_only else range(k + p)
+                        if not all(np.array_equal(got[b, i], full[b, i]) for i in rows):
+                            errors.append((tid, "pool reconstruct", op, k, p, L, B, data_only))
+                            break
                 else:              # device-resident batch on this thread's stream: encode, in-place and compact rebuild
                     B = int(rng.integers(1, 9))
                     P = (L + 255) // 256 * 256
@@ -319,14 +398,15 @@ def worker(tid, deadline, errors, counts, ops=tuple(range(8)), shapes=tuple(rang
                         errors.append((tid, "batch_dev reconstruct", k, p, L, B))
                 counts[tid] += 1
         except Exception as e:   # surfaced by the main thread
-            errors.append((tid, "exception", op, k, p, L, repr(e)))
+            import traceback
+            errors.append((tid, "exception", op, k, p, L, repr(e), traceback.format_exc(limit=4)))
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=120)
     ap.add_argument("--threads", type=int, default=12)
-    ap.add_argument("--ops", default="0,1,2,3,4,5,6,7", help="subset of the operations (comma list)")
+    ap.add_argument("--ops", default="0,1,2,3,4,5,6,7,8,9", help="subset of the operations (comma list)")
     ap.add_argument("--shapes", default=",".join(str(i) for i in range(len(SHAPES))),
                     help="subset of SHAPES (indices)")
     a = ap.parse_args()
