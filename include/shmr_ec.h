@@ -157,7 +157,9 @@ int shmr_ec_op_wait(shmr_ec_op_t* op);
  * launched at once when fewer than "coalesce_depth" (default 1) batches are in
  * flight on the queue's stream, and otherwise merges with every call that
  * arrives meanwhile (from any thread, any codec; knob "coalesce_us": an idle
- * queue waits that long for company) into the next launch -- one pointer-
+ * queue waits that long for company) into the next launch, which the queue's
+ * watcher thread issues "coalesce_lead_us" (default 30; 0: at completion)
+ * before the running batch's estimated end, so it is queued behind it -- one pointer-
  * table call per (codec, operation, length, data_only) group, whose shards,
  * if they sit on a slot lattice (a slab, a shmr_ec_pool), run the strided
  * kernels over their slots.  The call returns when its own block is written,
@@ -188,7 +190,8 @@ enum {
     SHMR_EC_Q_BATCHES = 1,    /* launch groups taken from the queue */
     SHMR_EC_Q_MAX_BATCH = 2,  /* the most blocks one launch group merged */
     SHMR_EC_Q_SLEEPS = 3,     /* waits that ended in a blocking event synchronize */
-    SHMR_EC_Q_COUNTERS = 4
+    SHMR_EC_Q_EARLY = 4,      /* batches launched behind a running one, before its end (knob coalesce_lead_us) */
+    SHMR_EC_Q_COUNTERS = 5
 };
 int shmr_ec_queue_stats(int device, uint64_t* out, size_t n);
 
@@ -401,7 +404,7 @@ int shmr_ec_set_device(shmr_ec_t* rs, int device);
  * through the device's submission queue (above), merged with concurrent
  * calls, instead of one zero-copy launch per call; "coalesce_depth",
  * "coalesce_target", "coalesce_us", "coalesce_max" (blocks per launch, default
- * 1024), "coalesce_spin_us" and "coalesce_watch_us": the queue (above).  "bounce_kib": pageable single-block calls whose
+ * 1024), "coalesce_spin_us", "coalesce_watch_us" and "coalesce_lead_us": the queue (above).  "bounce_kib": pageable single-block calls whose
  * (k+p) x shard bytes fit in this many KiB go through one mapped bounce
  * buffer and a single zero-copy launch instead of per-shard DMA copies
  * (default 8192; 0 disables).  "mirror_zc" (0/1, default 1): pageable host

@@ -515,7 +515,7 @@ int check_reconstruct(shmr_ec_t* rs, uint8_t* const* shards, const size_t* shard
 std::unique_ptr<core::SubmitReq> make_req(shmr_ec_t* rs, core::OpClass op, bool data_only, bool host_mapped,
                                           size_t len, int dev, std::vector<uint64_t> row, const uint8_t* present) {
     std::unique_ptr<core::SubmitReq> r(new core::SubmitReq);
-    r->codec = rs->codec;
+    r->codec = rs->codec.get();
     r->op = op;
     r->data_only = data_only;
     r->host_mapped = host_mapped;

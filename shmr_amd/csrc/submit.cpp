@@ -1,6 +1,15 @@
 // Submission queue: concurrent per-block calls merged into batch launches (see
 // submit.hpp).
 //
+// Submission: a call pushes its request onto the queue's inbox, a lock-free
+// stack (one compare-exchange; r06 s13: 16 threads on one mutex convoyed, the
+// aggregate submission rate fell below one thread's).  A submitter launches
+// only when nothing is in flight (or `coalesce_depth` allows more, or
+// `coalesce_target` calls are pending); otherwise its call waits to merge.
+// One launcher at a time (the `launching_` flag): it drains the inbox, groups
+// the requests and enqueues them; after it drops the flag it looks again, so
+// a call pushed meanwhile is never left behind.
+//
 // Completion: after a batch's kernels the queue's stream runs a one-wave mark
 // kernel that stores the batch's sequence number into a pinned host word
 // (kern::launch_mark, a system-scope release store).  A waiting caller spins
@@ -8,9 +17,10 @@
 // and then sleeps on a condition.  One watcher thread per queue follows the
 // oldest batch in flight (spinning on the word for "coalesce_watch_us", then
 // asleep in hipEventSynchronize on a blocking-sync event recorded behind the
-// mark), wakes the sleepers when it completes, and
-// launches what was held back for merging -- so no caller's thread is spent
-// on other callers' completions.
+// mark), wakes the sleepers when it completes, and launches what was held
+// back for merging: `coalesce_lead_us` before the running batch's estimated
+// end (its bytes at a nominal rate), so that batch's successor is already
+// queued on the stream when it finishes, or at its completion.
 #include "submit.hpp"
 
 #include <algorithm>
@@ -33,21 +43,31 @@ namespace {
 using Clock = std::chrono::steady_clock;
 
 std::atomic<int> g_coalesce{0};      // host-buffer entry points on mapped memory through the queue
-std::atomic<int> g_depth{1};         // batches in flight before pending calls wait to merge
-std::atomic<int> g_target{64};       // ... unless this many are pending (a launch of its own)
+std::atomic<int> g_depth{1};         // batches in flight a submitter may add to
+std::atomic<int> g_target{64};       // ... or this many pending calls launch anyway
 std::atomic<int> g_window_us{0};     // an idle queue's launch waits this long for more calls
 std::atomic<int> g_max{1024};        // blocks per launch
 std::atomic<int> g_spin_us{30};      // a waiter spins this long before it sleeps
 std::atomic<int> g_watch_us{200};    // the watcher spins this long before it sleeps on the event
 std::atomic<int> g_mark{1};          // 1: a mark kernel advances the word; 0: the watcher does, from the event
+std::atomic<int> g_lead_us{30};      // the watcher's early launch, before the running batch's estimated end
 constexpr int kDepthDefault = 1, kTargetDefault = 64, kWindowDefault = 0, kMaxDefault = 1024, kSpinDefault = 30,
-              kWatchDefault = 200;
+              kWatchDefault = 200, kLeadDefault = 30;
+constexpr int kMaxInflight = 8;      // batches on the stream, whatever the target rule says
+// A batch's estimated GPU time: a launch's fixed cost plus its algorithmic
+// bytes at a nominal rate (device memory; mapped host memory crosses PCIe).
+constexpr int64_t kFixedNs = 5000;
+constexpr double kDevBytesPerNs = 6.4;    // 6.4 TB/s
+constexpr double kHostBytesPerNs = 50.0;                                     // 50 GB/s
 
 constexpr int kMaxQueues = 64;   // device IDs (ec_core kMaxDevIds)
-enum { kReqs = 0, kBatches, kMaxBatch, kSleeps, kStatCount };
+enum { kReqs = 0, kBatches, kMaxBatch, kSleeps, kAhead, kStatCount };
 std::atomic<uint64_t> g_stats[kMaxQueues][kStatCount];
 
 inline void cpu_relax() { __builtin_ia32_pause(); }
+inline int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count();
+}
 
 class Queue {
 public:
@@ -84,20 +104,23 @@ public:
 
     void submit(SubmitReq* r) {
         g_stats[dev_][kReqs].fetch_add(1, std::memory_order_relaxed);
-        std::unique_lock<std::mutex> lk(mu_);
-        if (pending_.empty()) first_arrival_ = Clock::now();
-        pending_.push_back(r);
-        pump(lk);
-        lk.unlock();
-        cv_work_.notify_one();
+        if (queued_.fetch_add(1, std::memory_order_seq_cst) == 0 && g_window_us.load(std::memory_order_relaxed) > 0)
+            first_arrival_ns_.store(now_ns(), std::memory_order_relaxed);
+        SubmitReq* head = inbox_.load(std::memory_order_relaxed);
+        do {
+            r->next = head;
+        } while (!inbox_.compare_exchange_weak(head, r, std::memory_order_seq_cst, std::memory_order_relaxed));
+        launch_some(kBySubmitter);
     }
 
     int wait(SubmitReq* r) {
-        if (!r->seq.load(std::memory_order_acquire) && !r->done.load(std::memory_order_acquire)) {
-            // waited for before it was launched (held back to merge): nothing
-            // else may come to merge with it -- launch what is pending now
-            std::unique_lock<std::mutex> lk(mu_);
-            pump(lk, true);
+        // waited for before it was launched (held back to merge): nothing else
+        // may come to merge with it -- launch what is pending now (or, while
+        // another thread launches, wait for that launch and look again)
+        while (!launched(r)) {
+            launch_some(kForced);
+            if (launched(r)) break;
+            cpu_relax();
         }
         const auto t0 = Clock::now();
         const auto spin = std::chrono::microseconds(g_spin_us.load(std::memory_order_relaxed));
@@ -106,15 +129,19 @@ public:
             if ((i & 63) == 63 && Clock::now() - t0 >= spin) break;
             cpu_relax();
         }
-        std::unique_lock<std::mutex> lk(mu_);   // sleep: the watcher wakes us
-        cv_done_.wait(lk, [&] { return finished(r); });
+        {
+            std::unique_lock<std::mutex> lk(mu_);   // sleep: the watcher wakes us
+            cv_done_.wait(lk, [&] { return finished(r); });
+        }
         return result(r);
     }
 
 private:
+    enum Mode { kBySubmitter, kForced, kByWatcher };
     struct Batch {
         uint64_t seq = 0;
         hipEvent_t ev = nullptr;
+        int64_t est_end_ns = 0;
     };
 
     uint64_t completed() const { return __atomic_load_n(word_, __ATOMIC_ACQUIRE); }
@@ -124,76 +151,130 @@ private:
         if (completed() < seq) __atomic_store_n(word_, seq, __ATOMIC_RELEASE);
     }
 
+    bool launched(const SubmitReq* r) const {
+        return r->seq.load(std::memory_order_acquire) || r->done.load(std::memory_order_acquire) ||
+               broken_.load(std::memory_order_acquire);
+    }
     bool finished(const SubmitReq* r) const {
-        if (r->done.load(std::memory_order_acquire)) return true;   // failed launch, or a broken queue
+        if (r->done.load(std::memory_order_acquire)) return true;   // failed launch
         const uint64_t s = r->seq.load(std::memory_order_acquire);
         return (s && completed() >= s) || broken_.load(std::memory_order_acquire);
     }
 
     // A finished request's status: its own, or DEVICE_ERROR when the queue
     // broke before its batch completed.
+    // (A request the queue still holds -- a launcher's, when the queue broke
+    // under it -- is returned only after that launcher let go: the caller
+    // frees it next.)
     int result(const SubmitReq* r) const {
         if (r->done.load(std::memory_order_acquire)) return r->rc;
         const uint64_t s = r->seq.load(std::memory_order_acquire);
-        return (s && completed() >= s) ? r->rc : SHMR_EC_DEVICE_ERROR;
+        if (s && completed() >= s) return r->rc;
+        while (launching_.load(std::memory_order_acquire)) std::this_thread::yield();
+        return SHMR_EC_DEVICE_ERROR;
+    }
+
+    // Whether a launcher of this kind should take the pending calls now.
+    bool wanted(Mode mode) const {
+        if (broken_.load(std::memory_order_acquire)) return false;
+        const int64_t q = queued_.load(std::memory_order_seq_cst);
+        if (q <= 0) return false;
+        if (mode == kForced) return true;
+        const int f = inflight_n_.load(std::memory_order_seq_cst);
+        if (f == 0) return true;
+        if (f < std::max(1, g_depth.load(std::memory_order_relaxed))) return true;
+        if (q >= std::max(1, g_target.load(std::memory_order_relaxed)) && f < kMaxInflight) return true;
+        return mode == kByWatcher && f == 1 && now_ns() >= ahead_at_ns_.load(std::memory_order_relaxed);
+    }
+
+    // Launches the pending calls while `wanted`: one launcher at a time; the
+    // others return (the launcher looks again after it drops the flag).
+    void launch_some(Mode mode) {
+        while (wanted(mode)) {
+            if (launching_.exchange(true, std::memory_order_seq_cst)) return;
+            const int f = inflight_n_.load(std::memory_order_seq_cst);
+            const int window = g_window_us.load(std::memory_order_relaxed);
+            if (mode != kForced && f == 0 && window > 0) {   // an idle queue: give other callers the window
+                const int64_t until = first_arrival_ns_.load(std::memory_order_relaxed) + int64_t(window) * 1000;
+                while (now_ns() < until && queued_.load(std::memory_order_relaxed) < g_max.load())
+                    std::this_thread::yield();
+            }
+            if (wanted(mode)) {
+                if (mode == kByWatcher && f == 1) g_stats[dev_][kAhead].fetch_add(1, std::memory_order_relaxed);
+                launch_pending();
+            }
+            launching_.store(false, std::memory_order_seq_cst);
+            if (mode == kForced) mode = kBySubmitter;   // one forced launch; then the usual rule
+        }
+    }
+
+    // Takes up to coalesce_max pending calls and enqueues them.  launching_ held.
+    void launch_pending() {
+        SubmitReq* h = inbox_.exchange(nullptr, std::memory_order_acq_rel);
+        const size_t first_new = pending_.size();
+        for (; h; h = h->next) pending_.push_back(h);
+        std::reverse(pending_.begin() + long(first_new), pending_.end());   // arrival order
+        if (pending_.empty()) return;
+        const size_t maxn = size_t(std::max(1, g_max.load(std::memory_order_relaxed)));
+        const size_t n = std::min(maxn, pending_.size());
+        take_.assign(pending_.begin(), pending_.begin() + long(n));
+        pending_.erase(pending_.begin(), pending_.begin() + long(n));
+        queued_.fetch_sub(int64_t(n), std::memory_order_seq_cst);
+        const uint64_t seq = ++launched_;
+        double bytes_ns = 0;   // the batch's estimated GPU time
+        for (const SubmitReq* q : take_) {
+            size_t touched = 0;
+            for (uint64_t a : q->row) touched += a != 0;
+            bytes_ns += double(touched) * double(q->len) / (q->host_mapped ? kHostBytesPerNs : kDevBytesPerNs);
+        }
+        hipEvent_t ev = nullptr;   // (a blocking-sync event from the pool, or made by launch)
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            if (!events_.empty()) {
+                ev = events_.back();
+                events_.pop_back();
+            }
+        }
+        const bool queued = launch(take_, seq, &ev);
+        const int64_t t = now_ns();
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            if (queued) {
+                const int64_t start = std::max(t, inflight_.empty() ? t : inflight_.back().est_end_ns);
+                inflight_.push_back(Batch{seq, ev, start + kFixedNs + int64_t(bytes_ns)});
+                publish_inflight();
+            } else {   // nothing left running (failed and drained): every status is final
+                if (ev) events_.push_back(ev);
+                for (SubmitReq* q : take_) q->done.store(1, std::memory_order_release);
+            }
+        }
+        take_.clear();
+        if (queued)
+            cv_work_.notify_one();
+        else
+            cv_done_.notify_all();
+    }
+
+    // inflight_ changed: its size and the watcher's early-launch time.  mu_ held.
+    void publish_inflight() {
+        inflight_n_.store(int(inflight_.size()), std::memory_order_seq_cst);
+        front_end_ns_.store(inflight_.empty() ? INT64_MAX : inflight_.front().est_end_ns, std::memory_order_relaxed);
+        const int lead = g_lead_us.load(std::memory_order_relaxed);
+        ahead_at_ns_.store(inflight_.size() == 1 && lead > 0 ? inflight_.front().est_end_ns - int64_t(lead) * 1000
+                                                            : INT64_MAX,
+                           std::memory_order_relaxed);
     }
 
     // Drops finished batches (their events back to the pool).  mu_ held.
     void reap() {
         const uint64_t c = completed();
+        bool changed = false;
         while (!inflight_.empty() && inflight_.front().seq <= c) {
             if (inflight_.front().ev) events_.push_back(inflight_.front().ev);
             inflight_.pop_front();
+            changed = true;
         }
-    }
-
-    // Launches pending requests: at once while fewer than `depth` batches are
-    // in flight, or when `target` requests are pending; otherwise they wait
-    // (and merge) until a batch completes.  One launcher at a time.  mu_ held.
-    // force: launch whatever is pending (a caller waits for a held-back call).
-    void pump(std::unique_lock<std::mutex>& lk, bool force = false) {
-        for (;;) {
-            if (launching_ || pending_.empty()) return;
-            reap();
-            const size_t depth = size_t(std::max(1, g_depth.load(std::memory_order_relaxed)));
-            const size_t target = size_t(std::max(1, g_target.load(std::memory_order_relaxed)));
-            if (!force && inflight_.size() >= depth && pending_.size() < target) return;
-            force = false;
-            const size_t maxn = size_t(std::max(1, g_max.load(std::memory_order_relaxed)));
-            const int window = g_window_us.load(std::memory_order_relaxed);
-            launching_ = true;
-            if (window > 0 && inflight_.empty() && pending_.size() < maxn) {
-                const auto until = first_arrival_ + std::chrono::microseconds(window);
-                if (Clock::now() < until) {   // an idle queue: give other callers the window
-                    lk.unlock();
-                    while (Clock::now() < until) std::this_thread::yield();
-                    lk.lock();
-                }
-            }
-            const size_t n = std::min(maxn, pending_.size());
-            take_.assign(pending_.begin(), pending_.begin() + long(n));
-            pending_.erase(pending_.begin(), pending_.begin() + long(n));
-            if (!pending_.empty()) first_arrival_ = Clock::now();
-            const uint64_t seq = ++launched_;
-            hipEvent_t ev = nullptr;   // (a blocking-sync event from the pool, or made by launch)
-            if (!events_.empty()) {
-                ev = events_.back();
-                events_.pop_back();
-            }
-            lk.unlock();
-            const bool queued = launch(take_, seq, &ev);
-            lk.lock();
-            launching_ = false;
-            if (queued) {
-                inflight_.push_back(Batch{seq, ev});
-                cv_work_.notify_one();
-            } else {   // nothing left running (failed and drained): every status is final
-                if (ev) events_.push_back(ev);
-                for (SubmitReq* q : take_) q->done.store(1, std::memory_order_release);
-                cv_done_.notify_all();
-            }
-            take_.clear();
-        }
+        if (changed) publish_inflight();
     }
 
     // Enqueues one batch on the queue's stream: one pointer-table call per
@@ -210,12 +291,12 @@ private:
         using Key = std::tuple<const Codec*, int, bool, bool, uint64_t>;
         std::map<Key, std::vector<SubmitReq*>> groups;
         for (SubmitReq* q : reqs) {
-            groups[Key{q->codec.get(), int(q->op), q->data_only, q->host_mapped, q->len}].push_back(q);
+            groups[Key{q->codec, int(q->op), q->data_only, q->host_mapped, q->len}].push_back(q);
             q->seq.store(seq, std::memory_order_release);   // the mark for seq comes after its kernels
         }
         for (auto& g : groups) {
             std::vector<SubmitReq*>& v = g.second;
-            Codec& c = *v[0]->codec;
+            Codec& c = *const_cast<Codec*>(v[0]->codec);
             const unsigned t = c.k() + c.p();
             const size_t n = v.size();
             tab_.resize(n * t);
@@ -284,17 +365,20 @@ private:
     }
 
     // The watcher: follows the oldest batch in flight -- the host word, then
-    // (after coalesce_watch_us) hipEventSynchronize on its event; an error
-    // there means the device failed: the queue is broken and every waiter
-    // returns DEVICE_ERROR -- wakes the sleeping callers when it completes, and
-    // launches what pump() held back.
+    // (after coalesce_watch_us, and past the early-launch time while calls
+    // wait) hipEventSynchronize on its event; an error there means the device
+    // failed: the queue is broken and every waiter returns DEVICE_ERROR --
+    // launches the waiting calls at the early-launch time and at completion,
+    // and wakes the sleeping callers.
     void watch() {
         RelaxedCapture relaxed;
         std::unique_lock<std::mutex> lk(mu_);
         for (;;) {
-            cv_work_.wait(lk, [&] { return !inflight_.empty() || (!pending_.empty() && !launching_); });
-            pump(lk);
-            if (inflight_.empty()) continue;
+            cv_work_.wait(lk, [&] { return !inflight_.empty() || broken_.load(std::memory_order_acquire); });
+            if (broken_.load(std::memory_order_acquire)) {
+                release_all(lk);
+                continue;
+            }
             const uint64_t target = inflight_.front().seq;
             const hipEvent_t ev = inflight_.front().ev;
             lk.unlock();
@@ -306,20 +390,33 @@ private:
                     seen = true;
                     break;
                 }
-                if (ev && !g_mark.load(std::memory_order_relaxed) && (i & 15) == 15) {   // no mark kernel:
-                    const hipError_t q = hipEventQuery(ev);                               // poll the event
-                    if (q == hipSuccess) {
-                        advance(target);
-                        seen = true;
-                        break;
-                    }
-                    if (q != hipErrorNotReady) {
+                if ((i & 15) == 15) {
+                    if (wanted(kByWatcher)) launch_some(kByWatcher);   // the early launch
+                    if (ev && !g_mark.load(std::memory_order_relaxed)) {   // no mark kernel: poll the event
+                        const hipError_t q = hipEventQuery(ev);
+                        if (q == hipSuccess) {
+                            advance(target);
+                            seen = true;
+                            break;
+                        }
+                        if (q != hipErrorNotReady) {
+                            (void)hipGetLastError();
+                            break;   // (the blocking wait below reports it)
+                        }
                         (void)hipGetLastError();
-                        break;   // (the blocking wait below reports it)
                     }
-                    (void)hipGetLastError();
                 }
-                if ((i & 255) == 255 && Clock::now() - t0 >= spin) break;
+                if ((i & 255) == 255 && Clock::now() - t0 >= spin) {
+                    // With an early launch still to make, keep following the
+                    // word up to the batch's estimated end (dozing through
+                    // most of a long batch), so calls that arrive meanwhile
+                    // are launched behind it; past that end by 100 us, or with
+                    // no early launch to make, sleep on the event.
+                    if (ahead_at_ns_.load(std::memory_order_relaxed) == INT64_MAX) break;
+                    const int64_t end = front_end_ns_.load(std::memory_order_relaxed), now = now_ns();
+                    if (now > end + 100000) break;
+                    if (end - now > 5000000) std::this_thread::sleep_for(std::chrono::nanoseconds(end - now - 2000000));
+                }
                 cpu_relax();
             }
             if (!seen && ev) {   // sleep until the GPU signals the event (behind the mark)
@@ -336,34 +433,49 @@ private:
             reap();
             lk.unlock();
             cv_done_.notify_all();
+            launch_some(kByWatcher);   // what waited for this batch
             lk.lock();
-            if (broken_.load(std::memory_order_acquire)) {   // nothing will complete: release everyone
-                for (SubmitReq* q : pending_) {
-                    q->rc = SHMR_EC_DEVICE_ERROR;
-                    q->done.store(1, std::memory_order_release);
-                }
-                pending_.clear();
-                while (!inflight_.empty()) inflight_.pop_front();
-                cv_done_.notify_all();
-            }
+            if (broken_.load(std::memory_order_acquire)) release_all(lk);
         }
+    }
+
+    // A broken queue: nothing will complete.  Every waiter returns through
+    // broken_ (finished / result); the lists are dropped without touching
+    // their requests, which their callers may already have freed.  mu_ held.
+    void release_all(std::unique_lock<std::mutex>& lk) {
+        lk.unlock();
+        while (launching_.exchange(true, std::memory_order_seq_cst)) std::this_thread::yield();
+        (void)inbox_.exchange(nullptr, std::memory_order_acq_rel);
+        pending_.clear();
+        queued_.store(0, std::memory_order_seq_cst);
+        launching_.store(false, std::memory_order_seq_cst);
+        lk.lock();
+        inflight_.clear();
+        publish_inflight();
+        cv_done_.notify_all();
+        cv_work_.wait(lk, [] { return false; });   // (the queue is dead: the watcher parks)
     }
 
     const int dev_;
     hipStream_t stream_ = nullptr;
     uint64_t* word_ = nullptr;    // completion mark (host view)
     uint64_t* dword_ = nullptr;   // ... its device address
-    std::mutex mu_;
+    std::atomic<SubmitReq*> inbox_{nullptr};   // pushed by submit(), drained by the launcher
+    std::atomic<int64_t> queued_{0};           // calls submitted and not yet launched
+    std::atomic<int64_t> first_arrival_ns_{0};
+    std::atomic<bool> launching_{false};
+    std::vector<SubmitReq*> pending_, take_;   // launcher only
+    std::vector<uint64_t> tab_;                // launcher only
+    std::vector<uint8_t> present_;             // launcher only
+    uint64_t launched_ = 0;                    // launcher only
+    std::mutex mu_;                            // inflight_, events_, the condition variables
     std::condition_variable cv_work_, cv_done_;
-    std::vector<SubmitReq*> pending_, take_;
     std::deque<Batch> inflight_;
+    std::atomic<int> inflight_n_{0};
+    std::atomic<int64_t> ahead_at_ns_{INT64_MAX};   // early launch behind the one batch in flight
+    std::atomic<int64_t> front_end_ns_{INT64_MAX};  // the oldest batch's estimated end
     std::vector<hipEvent_t> events_;
-    std::vector<uint64_t> tab_;
-    std::vector<uint8_t> present_;
-    uint64_t launched_ = 0;
-    bool launching_ = false;
     std::atomic<bool> broken_{false};
-    Clock::time_point first_arrival_{};
 };
 
 std::mutex g_queues_mu;
@@ -423,6 +535,7 @@ int set_submit_tuning(const std::string& key, int value, bool* known) {
     if (key == "coalesce_spin_us") return set(g_spin_us, kSpinDefault, 0, 10000000);
     if (key == "coalesce_watch_us") return set(g_watch_us, kWatchDefault, 0, 10000000);
     if (key == "coalesce_mark") return set(g_mark, 1, 0, 1);
+    if (key == "coalesce_lead_us") return set(g_lead_us, kLeadDefault, 0, 10000000);
     *known = false;
     return SHMR_EC_INVALID_ARGUMENT;
 }
@@ -437,6 +550,7 @@ int get_submit_tuning(const std::string& key, bool* known) {
     if (key == "coalesce_spin_us") return g_spin_us;
     if (key == "coalesce_watch_us") return g_watch_us;
     if (key == "coalesce_mark") return g_mark;
+    if (key == "coalesce_lead_us") return g_lead_us;
     *known = false;
     return SHMR_EC_INVALID_ARGUMENT;
 }

@@ -6,13 +6,14 @@
 // src/vfs/block.rs:427; load_block -> reconstruct at :560).  One launch per
 // 4 MiB block leaves the GPU launch-bound (a single-block RS(8,3) kernel is
 // ~6 us on the GPU for 0.9 us of HBM work), so per device ID the
-// library keeps one queue: a call whose inputs are ready submits its block's
-// shard row; a launch group is taken whenever fewer than `coalesce_depth`
-// batches are in flight on the queue's stream, so calls that arrive while one
-// is running (or, knob coalesce_us, within a window) merge into the next
-// launch -- every pending request of every codec, grouped per (codec, op,
-// length, data_only, memory kind), each group one pointer-table call (a slot
-// lattice runs the strided kernels, core::ptrs_launch).  Completion is in
+// library keeps one queue: a call whose inputs are ready pushes its block's
+// shard row onto a lock-free inbox; an idle queue launches at once, and calls
+// that arrive while a batch runs (or, knob coalesce_us, within a window)
+// merge into the next launch, which the queue's watcher thread issues shortly
+// before the running batch's estimated end (knob coalesce_lead_us) -- every
+// pending request of every codec, grouped per (codec, op, length, data_only,
+// memory kind), each group one pointer-table call (a slot lattice runs the
+// strided kernels, core::ptrs_launch).  Completion is in
 // launch order on the one stream: a mark kernel behind every batch stores its
 // sequence number into a pinned host word, on which the batch's callers spin
 // before they sleep; a watcher thread per queue wakes them and launches the
@@ -30,7 +31,7 @@ namespace shmr {
 namespace core {
 
 struct SubmitReq {
-    std::shared_ptr<Codec> codec;
+    const Codec* codec = nullptr;   // a registry codec (gf::get_codec: never freed)
     OpClass op = kEncode;
     bool data_only = false;
     bool host_mapped = false;       // row addresses are mapped host memory
@@ -44,6 +45,7 @@ struct SubmitReq {
     std::atomic<uint64_t> seq{0};
     std::atomic<int> done{0};
     int rc = SHMR_EC_OK;
+    SubmitReq* next = nullptr;      // the queue's lock-free inbox (submit.cpp)
 };
 
 // Queues r (validated by the caller: crate checks, non-NULL touched shards,
@@ -59,7 +61,11 @@ int wait(SubmitReq* r);
 // "coalesce_us" (window a launch from an idle queue waits for more calls),
 // "coalesce_max" (blocks per launch), "coalesce_spin_us" (a waiter spins on
 // the completion word this long before it sleeps), "coalesce_watch_us" (the
-// watcher spins this long before it blocks on the batch's event).
+// watcher spins this long before it blocks on the batch's event),
+// "coalesce_lead_us" (the watcher launches the calls that arrived while one
+// batch runs this long before that batch's estimated end, so the next batch
+// is queued behind it and the GPU does not idle between batches; 0: only at
+// its completion).
 bool coalesce_host();
 int set_submit_tuning(const std::string& key, int value, bool* known);
 int get_submit_tuning(const std::string& key, bool* known);

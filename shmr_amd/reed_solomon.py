@@ -749,7 +749,7 @@ def capture_reserve(bytes_: int, device: int = 0) -> None:
     _check(lib().shmr_ec_capture_reserve(int(device), int(bytes_)))
 
 
-QUEUE_COUNTERS = ("requests", "batches", "max_batch", "sleeps")
+QUEUE_COUNTERS = ("requests", "batches", "max_batch", "sleeps", "early")
 
 
 def queue_stats(device: int = 0) -> dict:

@@ -251,6 +251,60 @@ def test_started_calls_batch_and_wait_out_of_order(gpu):
     assert np.array_equal(view[:, :, :S].cpu().numpy(), got)
 
 
+@pytest.mark.parametrize("lead_us", [0, 1000000])
+def test_early_launch_knob(gpu, lead_us):
+    """coalesce_lead_us: 0 launches held-back calls only when the running batch
+    completes (no early launches counted); a lead longer than any batch makes
+    the watcher launch every call that arrives while one batch runs at once,
+    behind it on the stream.  Both exact (8 threads of started encodes of 16
+    MiB shards, waited in random order)."""
+    import torch
+    k, p, S, T, per = 4, 2, 1 << 24, 8, 3
+    t = k + p
+    rs = shmr_amd.ReedSolomon(k, p)
+    slab = shmr_amd.ShardSlab(T * per, t, S)
+    rng = np.random.default_rng(lead_us % 97)
+    data = rng.integers(0, 256, (T * per, k, 4096), dtype=np.uint8)
+    view = slab.tensor()
+    view[:, :k, :S] = torch.from_numpy(data).to(gpu).repeat(1, 1, S // 4096)
+    view[:, k:, :S] = 0xEE
+    torch.cuda.synchronize()
+    errors = []
+    barrier = threading.Barrier(T)
+
+    def worker(th):
+        try:
+            barrier.wait()
+            ops = [rs.encode_dev([slab.shard(th * per + j, i) for i in range(t)], start=True) for j in range(per)]
+            for j in np.random.default_rng(th).permutation(per):
+                ops[int(j)].wait()
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    shmr_amd.set_tuning(coalesce_lead_us=lead_us)
+    try:
+        assert shmr_amd.get_tuning("coalesce_lead_us") == lead_us
+        q0 = shmr_amd.queue_stats(0)
+        ths = [threading.Thread(target=worker, args=(i,)) for i in range(T)]
+        for x in ths:
+            x.start()
+        for x in ths:
+            x.join()
+        q1 = shmr_amd.queue_stats(0)
+    finally:
+        shmr_amd.set_tuning(coalesce_lead_us=-2)
+    assert shmr_amd.get_tuning("coalesce_lead_us") == 30
+    assert not errors, errors[:3]
+    assert q1["requests"] - q0["requests"] == T * per
+    if lead_us == 0:
+        assert q1["early"] == q0["early"]
+    got = view[:, k:, :4096].cpu().numpy()
+    for b in range(T * per):
+        assert np.array_equal(got[b], _parity(k, p, data[b])), b
+    # every column of a shard repeats the same 4 KiB: the whole parity row too
+    assert bool((view[:, k:, :S].reshape(T * per, p, S // 4096, 4096) == view[:, k:, None, :4096]).all())
+
+
 def test_validation_in_crate_order(gpu):
     import torch
     k, p, S = 4, 2, 4096

@@ -123,6 +123,26 @@ void enqueue_cost(shmr_ec_t* rs, uint8_t* slab, size_t blocks, hipStream_t s) {
     }
 }
 
+// CPU time the process's cgroup was throttled for (its CPU quota), in us;
+// UINT64_MAX where the file is missing.  (GPU boxes give a job a quota of
+// host cores: threads that spin can use it up.)
+uint64_t throttled_us() {
+    for (const char* path : {"/sys/fs/cgroup/cpu.stat", "/sys/fs/cgroup/cpu/cpu.stat", "/sys/fs/cgroup/cpu,cpuacct/cpu.stat"}) {
+        FILE* f = std::fopen(path, "r");
+        if (!f) continue;
+        char key[64];
+        unsigned long long v = 0;
+        uint64_t out = UINT64_MAX;
+        while (std::fscanf(f, "%63s %llu", key, &v) == 2) {
+            if (std::strcmp(key, "throttled_usec") == 0) out = v;
+            if (std::strcmp(key, "throttled_time") == 0) out = v / 1000;   // cgroup v1: ns
+        }
+        std::fclose(f);
+        if (out != UINT64_MAX) return out;
+    }
+    return UINT64_MAX;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -229,13 +249,15 @@ int main(int argc, char** argv) {
         {
             std::vector<hipStream_t> ss(static_cast<size_t>(threads));
             for (auto& s : ss) CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-            double best = 1e30;
+            double best = 1e30, best_submit = 0;
             bool ok = true;
+            const uint64_t thr0 = throttled_us();
             uint64_t q0[SHMR_EC_Q_COUNTERS] = {}, q1[SHMR_EC_Q_COUNTERS] = {};
             for (int r = 0; r < reps + 1; ++r) {
                 CHECK_HIP(hipMemset2D(slab + K * PITCH, BLOCK, 0, P * PITCH, blocks));   // parity cleared
                 CHECK_HIP(hipDeviceSynchronize());
                 std::vector<int> rc(size_t(threads), 0);
+                std::vector<std::chrono::steady_clock::time_point> sub_end{size_t(threads)};
                 // r06: the workers are started before the clock and released
                 // together (a rayon pool exists before the flush it serves);
                 // r05's figures included the thread creation
@@ -251,6 +273,7 @@ int main(int argc, char** argv) {
                                 if (encode_queued(rs, slab, b, wait_each ? nullptr : &op) != 0) rc[size_t(t)] = 1;
                                 if (op) ops.push_back(op);
                             }
+                            sub_end[size_t(t)] = std::chrono::steady_clock::now();
                             for (shmr_ec_op_t* op : ops)
                                 if (shmr_ec_op_wait(op) != 0) rc[size_t(t)] = 1;
                             return;
@@ -269,19 +292,29 @@ int main(int argc, char** argv) {
                 const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
                 (void)shmr_ec_queue_stats(0, q1, SHMR_EC_Q_COUNTERS);
                 for (int x : rc) ok = ok && x == 0;
-                if (r >= 1) best = std::min(best, sec);   // rep 0 warms the streams' state
+                double submit_s = 0;   // the last thread's submissions done (queue modes)
+                for (const auto& e : sub_end)
+                    if (md.queue) submit_s = std::max(submit_s, std::chrono::duration<double>(e - t0).count());
+                if (r >= 1 && sec < best) {   // rep 0 warms the streams' state
+                    best = sec;
+                    best_submit = submit_s;
+                }
             }
+            const uint64_t thr1 = throttled_us();
             const bool same = parity_of(slab, blocks) == want;
             const uint64_t nb = q1[SHMR_EC_Q_BATCHES] - q0[SHMR_EC_Q_BATCHES];
             std::printf("{\"mode\": \"per_block\", \"api\": \"%s\", \"knobs\": \"%s\", \"variant\": \"%s\", "
                         "\"wait_each_call\": %s, \"threads\": %d, \"blocks\": %zu, "
                         "\"GiBps\": %.1f, \"us_per_block\": %.2f, \"of_batch\": %.3f, \"ok\": %s, "
                         "\"parity_equals_batch\": %s, \"tune\": \"%s\", \"queue_batches_last_rep\": %llu, "
-                        "\"blocks_per_launch_last_rep\": %.2f}\n",
+                        "\"blocks_per_launch_last_rep\": %.2f, \"early_launches_last_rep\": %llu, "
+                        "\"submitted_by_us\": %.1f, \"cgroup_throttled_us\": %lld}\n",
                         md.queue ? "encode_dev (queue)" : "encode_batch_dev (stream)", label.c_str(), variant,
                         wait_each ? "true" : "false", threads, blocks, data_gib / best,
                         best / blocks * 1e6, best_batch / best, ok ? "true" : "false", same ? "true" : "false",
-                        std::getenv("SHMR_PB_TUNE") ? std::getenv("SHMR_PB_TUNE") : "", (unsigned long long)nb, nb ? double(blocks) / double(nb) : 0.0);
+                        std::getenv("SHMR_PB_TUNE") ? std::getenv("SHMR_PB_TUNE") : "", (unsigned long long)nb, nb ? double(blocks) / double(nb) : 0.0,
+                        (unsigned long long)(q1[SHMR_EC_Q_EARLY] - q0[SHMR_EC_Q_EARLY]), best_submit * 1e6,
+                        (thr0 == UINT64_MAX || thr1 == UINT64_MAX) ? -1LL : (long long)(thr1 - thr0));
             std::fflush(stdout);
             for (auto& s : ss) CHECK_HIP(hipStreamDestroy(s));
             if (!ok || !same) return 1;
