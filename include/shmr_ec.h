@@ -190,7 +190,7 @@ enum {
     SHMR_EC_Q_BATCHES = 1,    /* launch groups taken from the queue */
     SHMR_EC_Q_MAX_BATCH = 2,  /* the most blocks one launch group merged */
     SHMR_EC_Q_SLEEPS = 3,     /* waits that ended in a blocking event synchronize */
-    SHMR_EC_Q_EARLY = 4,      /* batches launched behind a running one, before its end (knob coalesce_lead_us) */
+    SHMR_EC_Q_EARLY = 4,      /* batches launched behind a running one before its end (knob coalesce_lead_us) */
     SHMR_EC_Q_COUNTERS = 5
 };
 int shmr_ec_queue_stats(int device, uint64_t* out, size_t n);
@@ -404,7 +404,8 @@ int shmr_ec_set_device(shmr_ec_t* rs, int device);
  * through the device's submission queue (above), merged with concurrent
  * calls, instead of one zero-copy launch per call; "coalesce_depth",
  * "coalesce_target", "coalesce_us", "coalesce_max" (blocks per launch, default
- * 1024), "coalesce_spin_us", "coalesce_watch_us" and "coalesce_lead_us": the queue (above).  "bounce_kib": pageable single-block calls whose
+ * 1024), "coalesce_spin_us", "coalesce_watch_us", "coalesce_lead_us" and "coalesce_idle_us" (default 1000:
+ * the watcher spins this long for calls after the queue goes idle, then sleeps): the queue (above).  "bounce_kib": pageable single-block calls whose
  * (k+p) x shard bytes fit in this many KiB go through one mapped bounce
  * buffer and a single zero-copy launch instead of per-shard DMA copies
  * (default 8192; 0 disables).  "mirror_zc" (0/1, default 1): pageable host

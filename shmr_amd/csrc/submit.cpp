@@ -1,14 +1,17 @@
 // Submission queue: concurrent per-block calls merged into batch launches (see
 // submit.hpp).
 //
-// Submission: a call pushes its request onto the queue's inbox, a lock-free
-// stack (one compare-exchange; r06 s13: 16 threads on one mutex convoyed, the
-// aggregate submission rate fell below one thread's).  A submitter launches
-// only when nothing is in flight (or `coalesce_depth` allows more, or
-// `coalesce_target` calls are pending); otherwise its call waits to merge.
-// One launcher at a time (the `launching_` flag): it drains the inbox, groups
-// the requests and enqueues them; after it drops the flag it looks again, so
-// a call pushed meanwhile is never left behind.
+// Submission: a call puts its request into the queue's inbox, a ring of
+// request pointers (one fetch_add; r06 s13: 16 threads on one mutex convoyed,
+// the aggregate submission rate fell below one thread's), and wakes the watcher
+// if it sleeps.  The callers' threads make no HIP call: the queue's watcher
+// thread is its one launcher (r06 s15-s23: a thread's first HIP calls cost
+// tens of microseconds, and new callers' first calls queued behind each
+// other in the runtime while every block waited).  It launches at once when
+// nothing is in flight (or `coalesce_depth` allows more, or `coalesce_target`
+// calls are pending, or a caller waits for a call not yet launched);
+// otherwise calls wait to merge.  A launch drains the inbox, groups the
+// requests and enqueues them.
 //
 // Completion: after a batch's kernels the queue's stream runs a one-wave mark
 // kernel that stores the batch's sequence number into a pinned host word
@@ -29,6 +32,8 @@
 #include <cstring>
 #include <deque>
 #include <map>
+#include <cstdio>
+#include <cstdlib>
 #include <mutex>
 #include <thread>
 #include <tuple>
@@ -43,7 +48,7 @@ namespace {
 using Clock = std::chrono::steady_clock;
 
 std::atomic<int> g_coalesce{0};      // host-buffer entry points on mapped memory through the queue
-std::atomic<int> g_depth{1};         // batches in flight a submitter may add to
+std::atomic<int> g_depth{1};         // batches in flight the watcher adds to at once
 std::atomic<int> g_target{64};       // ... or this many pending calls launch anyway
 std::atomic<int> g_window_us{0};     // an idle queue's launch waits this long for more calls
 std::atomic<int> g_max{1024};        // blocks per launch
@@ -51,20 +56,48 @@ std::atomic<int> g_spin_us{30};      // a waiter spins this long before it sleep
 std::atomic<int> g_watch_us{200};    // the watcher spins this long before it sleeps on the event
 std::atomic<int> g_mark{1};          // 1: a mark kernel advances the word; 0: the watcher does, from the event
 std::atomic<int> g_lead_us{30};      // the watcher's early launch, before the running batch's estimated end
+std::atomic<int> g_idle_us{1000};    // the watcher spins this long for calls on an idle queue before it sleeps
 constexpr int kDepthDefault = 1, kTargetDefault = 64, kWindowDefault = 0, kMaxDefault = 1024, kSpinDefault = 30,
-              kWatchDefault = 200, kLeadDefault = 30;
+              kWatchDefault = 200, kLeadDefault = 30, kIdleDefault = 1000;
 constexpr int kMaxInflight = 8;      // batches on the stream, whatever the target rule says
 // A batch's estimated GPU time: a launch's fixed cost plus its algorithmic
 // bytes at a nominal rate (device memory; mapped host memory crosses PCIe).
 constexpr int64_t kFixedNs = 5000;
-constexpr double kDevBytesPerNs = 6.4;    // 6.4 TB/s
-constexpr double kHostBytesPerNs = 50.0;                                     // 50 GB/s
+constexpr double kDevBytesPerNs = 6400.0;   // 6.4 TB/s = 6,400 bytes per ns
+constexpr double kHostBytesPerNs = 50.0;     // 50 GB/s = 50 bytes per ns
 
 constexpr int kMaxQueues = 64;   // device IDs (ec_core kMaxDevIds)
 enum { kReqs = 0, kBatches, kMaxBatch, kSleeps, kAhead, kStatCount };
 std::atomic<uint64_t> g_stats[kMaxQueues][kStatCount];
 
 inline void cpu_relax() { __builtin_ia32_pause(); }
+
+// Diagnostic event log (environment SHMR_QUEUE_TRACE=1; printed to stderr at
+// exit): launches (start, end, mode, blocks, batches in flight) and the
+// watcher's completions, microseconds from the first event.
+struct TraceEv {
+    int64_t t0, t1;
+    int kind, mode, n, f;
+};
+struct Trace {
+    bool on = std::getenv("SHMR_QUEUE_TRACE") != nullptr;
+    std::mutex mu;
+    std::vector<TraceEv> ev;
+    void add(int kind, int mode, int n, int f, int64_t t0, int64_t t1) {
+        if (!on) return;
+        std::lock_guard<std::mutex> lk(mu);
+        if (ev.size() < 200000) ev.push_back(TraceEv{t0, t1, kind, mode, n, f});
+    }
+    ~Trace() {
+        if (!on || ev.empty()) return;
+        const int64_t base = ev.front().t0;
+        for (const TraceEv& e : ev)
+            std::fprintf(stderr, "QTRACE %s mode=%d n=%d f=%d t0=%.1f t1=%.1f\n",
+                         e.kind == 0 ? "launch" : e.kind == 1 ? "reaped" : e.kind == 3 ? "phase" : "other", e.mode, e.n, e.f,
+                         double(e.t0 - base) / 1e3, double(e.t1 - base) / 1e3);
+    }
+};
+Trace g_trace;
 inline int64_t now_ns() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count();
 }
@@ -106,21 +139,31 @@ public:
         g_stats[dev_][kReqs].fetch_add(1, std::memory_order_relaxed);
         if (queued_.fetch_add(1, std::memory_order_seq_cst) == 0 && g_window_us.load(std::memory_order_relaxed) > 0)
             first_arrival_ns_.store(now_ns(), std::memory_order_relaxed);
-        SubmitReq* head = inbox_.load(std::memory_order_relaxed);
-        do {
-            r->next = head;
-        } while (!inbox_.compare_exchange_weak(head, r, std::memory_order_seq_cst, std::memory_order_relaxed));
-        launch_some(kBySubmitter);
+        const uint64_t t = tail_.fetch_add(1, std::memory_order_seq_cst);
+        while (t - head_pub_.load(std::memory_order_acquire) >= kRing) std::this_thread::yield();   // full (rare)
+        ring_[t & (kRing - 1)].store(r, std::memory_order_seq_cst);
+        wake_watcher();
     }
 
     int wait(SubmitReq* r) {
         // waited for before it was launched (held back to merge): nothing else
-        // may come to merge with it -- launch what is pending now (or, while
-        // another thread launches, wait for that launch and look again)
-        while (!launched(r)) {
-            launch_some(kForced);
-            if (launched(r)) break;
-            cpu_relax();
+        // may come to merge with it -- the watcher launches what is pending
+        // now; wait for that launch (briefly spinning, then asleep)
+        for (uint32_t i = 0; !launched(r); ++i) {
+            if (i == 0 || (i >= 64 && (i & 7) == 0)) {
+                force_.store(true, std::memory_order_seq_cst);
+                wake_watcher();
+            }
+            if (i < 64) {
+                cpu_relax();
+                continue;
+            }
+            forced_waiters_.fetch_add(1, std::memory_order_seq_cst);
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_done_.wait_for(lk, std::chrono::microseconds(500), [&] { return launched(r); });
+            }
+            forced_waiters_.fetch_sub(1, std::memory_order_seq_cst);
         }
         const auto t0 = Clock::now();
         const auto spin = std::chrono::microseconds(g_spin_us.load(std::memory_order_relaxed));
@@ -137,12 +180,22 @@ public:
     }
 
 private:
-    enum Mode { kBySubmitter, kForced, kByWatcher };
+    enum Mode { kForced, kByWatcher };
     struct Batch {
         uint64_t seq = 0;
         hipEvent_t ev = nullptr;
         int64_t est_end_ns = 0;
     };
+
+    // A caller's work for the watcher (a call pushed, a launch forced): wake
+    // it if it sleeps.  (sleeping_ is set before the watcher's last look
+    // under imu_, and read here after the caller's own store: one of the
+    // two sees the other.)
+    void wake_watcher() {
+        if (!sleeping_.load(std::memory_order_seq_cst)) return;
+        { std::lock_guard<std::mutex> lk(imu_); }
+        cv_work_.notify_one();
+    }
 
     uint64_t completed() const { return __atomic_load_n(word_, __ATOMIC_ACQUIRE); }
     // The host's own advance of the word (knob coalesce_mark=0; only the
@@ -163,8 +216,8 @@ private:
 
     // A finished request's status: its own, or DEVICE_ERROR when the queue
     // broke before its batch completed.
-    // (A request the queue still holds -- a launcher's, when the queue broke
-    // under it -- is returned only after that launcher let go: the caller
+    // (A request the queue still holds -- the launcher's, when the queue broke
+    // under it -- is returned only after the launcher let go: the caller
     // frees it next.)
     int result(const SubmitReq* r) const {
         if (r->done.load(std::memory_order_acquire)) return r->rc;
@@ -187,8 +240,11 @@ private:
         return mode == kByWatcher && f == 1 && now_ns() >= ahead_at_ns_.load(std::memory_order_relaxed);
     }
 
-    // Launches the pending calls while `wanted`: one launcher at a time; the
-    // others return (the launcher looks again after it drops the flag).
+    // Launches the pending calls while `wanted` (the watcher only: callers'
+    // threads make no HIP call -- r06 s15/s23: a thread's first HIP calls
+    // cost tens of microseconds, and 16-32 new threads' first calls queued
+    // behind each other in the runtime for up to 0.5 ms while every
+    // caller's block waited).  launching_ marks the launch in progress.
     void launch_some(Mode mode) {
         while (wanted(mode)) {
             if (launching_.exchange(true, std::memory_order_seq_cst)) return;
@@ -200,20 +256,37 @@ private:
                     std::this_thread::yield();
             }
             if (wanted(mode)) {
-                if (mode == kByWatcher && f == 1) g_stats[dev_][kAhead].fetch_add(1, std::memory_order_relaxed);
+                if (mode == kByWatcher && f == 1 &&
+                    queued_.load(std::memory_order_relaxed) < std::max(1, g_target.load(std::memory_order_relaxed)) &&
+                    g_depth.load(std::memory_order_relaxed) <= 1)   // (not the target or depth rule)
+                    g_stats[dev_][kAhead].fetch_add(1, std::memory_order_relaxed);
+                const int64_t ta = g_trace.on ? now_ns() : 0;
+                const int64_t qa = queued_.load(std::memory_order_relaxed);
                 launch_pending();
+                if (g_trace.on) g_trace.add(0, int(mode), int(qa), f, ta, now_ns());
             }
             launching_.store(false, std::memory_order_seq_cst);
-            if (mode == kForced) mode = kBySubmitter;   // one forced launch; then the usual rule
+            if (forced_waiters_.load(std::memory_order_seq_cst) > 0) {   // callers asleep in wait() for a launch
+                { std::lock_guard<std::mutex> lk(mu_); }
+                cv_done_.notify_all();
+            }
+            if (mode == kForced) mode = kByWatcher;   // one forced launch; then the usual rule
         }
     }
 
     // Takes up to coalesce_max pending calls and enqueues them.  launching_ held.
     void launch_pending() {
-        SubmitReq* h = inbox_.exchange(nullptr, std::memory_order_acq_rel);
-        const size_t first_new = pending_.size();
-        for (; h; h = h->next) pending_.push_back(h);
-        std::reverse(pending_.begin() + long(first_new), pending_.end());   // arrival order
+        // the inbox in arrival order, up to the first slot whose caller has
+        // taken its index but not yet stored (it comes with the next launch)
+        for (;;) {
+            std::atomic<SubmitReq*>& slot = ring_[head_ & (kRing - 1)];
+            SubmitReq* r = slot.load(std::memory_order_acquire);
+            if (!r) break;
+            slot.store(nullptr, std::memory_order_relaxed);
+            pending_.push_back(r);
+            ++head_;
+        }
+        head_pub_.store(head_, std::memory_order_release);
         if (pending_.empty()) return;
         const size_t maxn = size_t(std::max(1, g_max.load(std::memory_order_relaxed)));
         const size_t n = std::min(maxn, pending_.size());
@@ -229,7 +302,7 @@ private:
         }
         hipEvent_t ev = nullptr;   // (a blocking-sync event from the pool, or made by launch)
         {
-            std::lock_guard<std::mutex> lk(mu_);
+            std::lock_guard<std::mutex> lk(imu_);
             if (!events_.empty()) {
                 ev = events_.back();
                 events_.pop_back();
@@ -238,7 +311,7 @@ private:
         const bool queued = launch(take_, seq, &ev);
         const int64_t t = now_ns();
         {
-            std::lock_guard<std::mutex> lk(mu_);
+            std::lock_guard<std::mutex> lk(imu_);
             if (queued) {
                 const int64_t start = std::max(t, inflight_.empty() ? t : inflight_.back().est_end_ns);
                 inflight_.push_back(Batch{seq, ev, start + kFixedNs + int64_t(bytes_ns)});
@@ -249,13 +322,15 @@ private:
             }
         }
         take_.clear();
-        if (queued)
+        if (queued) {
             cv_work_.notify_one();
-        else
+        } else {
+            { std::lock_guard<std::mutex> lk(mu_); }
             cv_done_.notify_all();
+        }
     }
 
-    // inflight_ changed: its size and the watcher's early-launch time.  mu_ held.
+    // inflight_ changed: its size and the watcher's early-launch time.  imu_ held.
     void publish_inflight() {
         inflight_n_.store(int(inflight_.size()), std::memory_order_seq_cst);
         front_end_ns_.store(inflight_.empty() ? INT64_MAX : inflight_.front().est_end_ns, std::memory_order_relaxed);
@@ -265,7 +340,7 @@ private:
                            std::memory_order_relaxed);
     }
 
-    // Drops finished batches (their events back to the pool).  mu_ held.
+    // Drops finished batches (their events back to the pool).  imu_ held.
     void reap() {
         const uint64_t c = completed();
         bool changed = false;
@@ -282,6 +357,7 @@ private:
     // A group's error is its requests' status.  false: nothing will mark the
     // batch (every status is final; the stream is drained).
     bool launch(std::vector<SubmitReq*>& reqs, uint64_t seq, hipEvent_t* ev) {
+        const int64_t tl0 = g_trace.on ? now_ns() : 0;
         RelaxedCapture relaxed;
         DeviceScope scope(dev_);
         if (!scope.ok()) {
@@ -294,6 +370,7 @@ private:
             groups[Key{q->codec, int(q->op), q->data_only, q->host_mapped, q->len}].push_back(q);
             q->seq.store(seq, std::memory_order_release);   // the mark for seq comes after its kernels
         }
+        if (g_trace.on) g_trace.add(3, 0, int(reqs.size()), 0, tl0, now_ns());
         for (auto& g : groups) {
             std::vector<SubmitReq*>& v = g.second;
             Codec& c = *const_cast<Codec*>(v[0]->codec);
@@ -317,6 +394,7 @@ private:
             if (rc)
                 for (SubmitReq* q : v) q->rc = rc;
         }
+        if (g_trace.on) g_trace.add(3, 1, int(reqs.size()), 0, tl0, now_ns());
         g_stats[dev_][kBatches].fetch_add(1, std::memory_order_relaxed);
         uint64_t m = g_stats[dev_][kMaxBatch].load(std::memory_order_relaxed);
         while (reqs.size() > m && !g_stats[dev_][kMaxBatch].compare_exchange_weak(m, reqs.size())) {
@@ -364,19 +442,55 @@ private:
         return true;
     }
 
-    // The watcher: follows the oldest batch in flight -- the host word, then
-    // (after coalesce_watch_us, and past the early-launch time while calls
-    // wait) hipEventSynchronize on its event; an error there means the device
-    // failed: the queue is broken and every waiter returns DEVICE_ERROR --
-    // launches the waiting calls at the early-launch time and at completion,
-    // and wakes the sleeping callers.
+    // Launches what is due: everything pending when a caller forced it,
+    // otherwise what `wanted` allows.
+    void launch_due() {
+        if (force_.exchange(false, std::memory_order_seq_cst))
+            launch_some(kForced);
+        else if (wanted(kByWatcher))
+            launch_some(kByWatcher);
+    }
+
+    // The watcher, the queue's one launcher: launches what is due, follows
+    // the oldest batch in flight -- the host word, then (after
+    // coalesce_watch_us, and past the early-launch time while calls could
+    // still arrive) hipEventSynchronize on its event; an error there means
+    // the device failed: the queue is broken and every waiter returns
+    // DEVICE_ERROR -- wakes the sleeping callers when it completes, and with
+    // nothing in flight spins coalesce_idle_us for calls before it sleeps.
     void watch() {
         RelaxedCapture relaxed;
-        std::unique_lock<std::mutex> lk(mu_);
+        std::unique_lock<std::mutex> lk(imu_);
+        lk.unlock();
         for (;;) {
-            cv_work_.wait(lk, [&] { return !inflight_.empty() || broken_.load(std::memory_order_acquire); });
+            launch_due();
+            lk.lock();
             if (broken_.load(std::memory_order_acquire)) {
                 release_all(lk);
+                continue;
+            }
+            if (inflight_.empty()) {   // idle: spin for calls, then sleep
+                lk.unlock();
+                const auto t0 = Clock::now();
+                const auto idle = std::chrono::microseconds(g_idle_us.load(std::memory_order_relaxed));
+                bool work = false;
+                for (uint32_t i = 0;; ++i) {
+                    if (queued_.load(std::memory_order_seq_cst) > 0 || force_.load(std::memory_order_seq_cst)) {
+                        work = true;
+                        break;
+                    }
+                    if ((i & 255) == 255 && Clock::now() - t0 >= idle) break;
+                    cpu_relax();
+                }
+                if (work) continue;
+                lk.lock();
+                sleeping_.store(true, std::memory_order_seq_cst);
+                cv_work_.wait(lk, [&] {
+                    return queued_.load(std::memory_order_seq_cst) > 0 || force_.load(std::memory_order_seq_cst) ||
+                           !inflight_.empty() || broken_.load(std::memory_order_acquire);
+                });
+                sleeping_.store(false, std::memory_order_seq_cst);
+                lk.unlock();
                 continue;
             }
             const uint64_t target = inflight_.front().seq;
@@ -391,7 +505,7 @@ private:
                     break;
                 }
                 if ((i & 15) == 15) {
-                    if (wanted(kByWatcher)) launch_some(kByWatcher);   // the early launch
+                    launch_due();   // the early launch, the target rule, forced launches
                     if (ev && !g_mark.load(std::memory_order_relaxed)) {   // no mark kernel: poll the event
                         const hipError_t q = hipEventQuery(ev);
                         if (q == hipSuccess) {
@@ -414,7 +528,7 @@ private:
                     // no early launch to make, sleep on the event.
                     if (ahead_at_ns_.load(std::memory_order_relaxed) == INT64_MAX) break;
                     const int64_t end = front_end_ns_.load(std::memory_order_relaxed), now = now_ns();
-                    if (now > end + 100000) break;
+                    if (end == INT64_MAX || now > end + 100000) break;
                     if (end - now > 5000000) std::this_thread::sleep_for(std::chrono::nanoseconds(end - now - 2000000));
                 }
                 cpu_relax();
@@ -431,28 +545,33 @@ private:
             }
             lk.lock();
             reap();
+            if (g_trace.on) g_trace.add(1, seen ? 1 : 0, int(target), int(inflight_.size()), now_ns(), now_ns());
             lk.unlock();
+            launch_due();   // what waited for this batch (before waking the sleepers: the GPU first)
+            { std::lock_guard<std::mutex> g(mu_); }   // (no caller between its check and its sleep)
             cv_done_.notify_all();
-            launch_some(kByWatcher);   // what waited for this batch
-            lk.lock();
-            if (broken_.load(std::memory_order_acquire)) release_all(lk);
         }
     }
 
     // A broken queue: nothing will complete.  Every waiter returns through
     // broken_ (finished / result); the lists are dropped without touching
-    // their requests, which their callers may already have freed.  mu_ held.
+    // their requests, which their callers may already have freed.  imu_ held.
     void release_all(std::unique_lock<std::mutex>& lk) {
         lk.unlock();
         while (launching_.exchange(true, std::memory_order_seq_cst)) std::this_thread::yield();
-        (void)inbox_.exchange(nullptr, std::memory_order_acq_rel);
+        for (auto& slot : ring_) slot.store(nullptr, std::memory_order_relaxed);
+        head_ = tail_.load(std::memory_order_seq_cst);
+        head_pub_.store(head_, std::memory_order_release);
         pending_.clear();
         queued_.store(0, std::memory_order_seq_cst);
         launching_.store(false, std::memory_order_seq_cst);
         lk.lock();
         inflight_.clear();
         publish_inflight();
+        lk.unlock();
+        { std::lock_guard<std::mutex> g(mu_); }
         cv_done_.notify_all();
+        lk.lock();
         cv_work_.wait(lk, [] { return false; });   // (the queue is dead: the watcher parks)
     }
 
@@ -460,18 +579,37 @@ private:
     hipStream_t stream_ = nullptr;
     uint64_t* word_ = nullptr;    // completion mark (host view)
     uint64_t* dword_ = nullptr;   // ... its device address
-    std::atomic<SubmitReq*> inbox_{nullptr};   // pushed by submit(), drained by the launcher
-    std::atomic<int64_t> queued_{0};           // calls submitted and not yet launched
+    // The shared atomics each on a cache line of their own, apart from the
+    // launcher's private state (r06 s19: callers hammering a line the
+    // launcher also used slowed its launches several-fold).
+    // The inbox: a ring of request pointers.  A caller takes an index
+    // (fetch_add) and stores its request there; the launcher reads the slots
+    // in order -- independent loads from one array (r06 s25: walking a
+    // linked list of requests made by other threads' cores cost ~0.25 us of
+    // dependent cache misses per request, 57 us for a 215-block batch).
+    static constexpr uint64_t kRing = 1u << 16;
+    std::vector<std::atomic<SubmitReq*>> ring_ = std::vector<std::atomic<SubmitReq*>>(kRing);
+    alignas(64) std::atomic<uint64_t> tail_{0};            // next index a caller takes
+    alignas(64) std::atomic<uint64_t> head_pub_{0};        // the launcher's head, for the full check
+    uint64_t head_ = 0;                                    // launcher only
+    alignas(64) std::atomic<int64_t> queued_{0};           // calls submitted and not yet launched
+    alignas(64) std::atomic<bool> launching_{false};
+    alignas(64) std::atomic<int> forced_waiters_{0};       // wait() callers asleep until a launch ends
+    alignas(64) std::atomic<bool> force_{false};           // a caller waits for a call not yet launched
+    alignas(64) std::atomic<bool> sleeping_{false};        // the watcher sleeps on cv_work_
     std::atomic<int64_t> first_arrival_ns_{0};
-    std::atomic<bool> launching_{false};
-    std::vector<SubmitReq*> pending_, take_;   // launcher only
+    alignas(64) std::vector<SubmitReq*> pending_, take_;   // launcher only
     std::vector<uint64_t> tab_;                // launcher only
     std::vector<uint8_t> present_;             // launcher only
     uint64_t launched_ = 0;                    // launcher only
-    std::mutex mu_;                            // inflight_, events_, the condition variables
+    // Two locks: callers asleep in wait() (cv_done_) never stand in the
+    // launcher's way to inflight_ (r06 s22: a notify_all woke 16-32 sleepers
+    // whose turns at one mutex delayed launches by 100-400 us).
+    alignas(64) std::mutex mu_;                // cv_done_: callers asleep until a batch completes or a launch ends
+    alignas(64) std::mutex imu_;               // inflight_, events_, cv_work_ (launcher and watcher)
     std::condition_variable cv_work_, cv_done_;
     std::deque<Batch> inflight_;
-    std::atomic<int> inflight_n_{0};
+    alignas(64) std::atomic<int> inflight_n_{0};
     std::atomic<int64_t> ahead_at_ns_{INT64_MAX};   // early launch behind the one batch in flight
     std::atomic<int64_t> front_end_ns_{INT64_MAX};  // the oldest batch's estimated end
     std::vector<hipEvent_t> events_;
@@ -536,6 +674,7 @@ int set_submit_tuning(const std::string& key, int value, bool* known) {
     if (key == "coalesce_watch_us") return set(g_watch_us, kWatchDefault, 0, 10000000);
     if (key == "coalesce_mark") return set(g_mark, 1, 0, 1);
     if (key == "coalesce_lead_us") return set(g_lead_us, kLeadDefault, 0, 10000000);
+    if (key == "coalesce_idle_us") return set(g_idle_us, kIdleDefault, 0, 10000000);
     *known = false;
     return SHMR_EC_INVALID_ARGUMENT;
 }
@@ -551,6 +690,7 @@ int get_submit_tuning(const std::string& key, bool* known) {
     if (key == "coalesce_watch_us") return g_watch_us;
     if (key == "coalesce_mark") return g_mark;
     if (key == "coalesce_lead_us") return g_lead_us;
+    if (key == "coalesce_idle_us") return g_idle_us;
     *known = false;
     return SHMR_EC_INVALID_ARGUMENT;
 }

@@ -7,17 +7,16 @@
 // 4 MiB block leaves the GPU launch-bound (a single-block RS(8,3) kernel is
 // ~6 us on the GPU for 0.9 us of HBM work), so per device ID the
 // library keeps one queue: a call whose inputs are ready pushes its block's
-// shard row onto a lock-free inbox; an idle queue launches at once, and calls
-// that arrive while a batch runs (or, knob coalesce_us, within a window)
-// merge into the next launch, which the queue's watcher thread issues shortly
-// before the running batch's estimated end (knob coalesce_lead_us) -- every
-// pending request of every codec, grouped per (codec, op, length, data_only,
-// memory kind), each group one pointer-table call (a slot lattice runs the
-// strided kernels, core::ptrs_launch).  Completion is in
-// launch order on the one stream: a mark kernel behind every batch stores its
-// sequence number into a pinned host word, on which the batch's callers spin
-// before they sleep; a watcher thread per queue wakes them and launches the
-// calls held back for merging.
+// shard row into a lock-free inbox; the queue's watcher thread, its one
+// launcher, launches at once when nothing runs, and calls that arrive while a
+// batch runs (or, knob coalesce_us, within a window) merge into the next
+// launch, which it issues shortly before the running batch's estimated end
+// (knob coalesce_lead_us) -- every pending request of every codec, grouped per
+// (codec, op, length, data_only, memory kind), each group one pointer-table
+// call (a slot lattice runs the strided kernels, core::ptrs_launch).
+// Completion is in launch order on the one stream: a mark kernel behind every
+// batch stores its sequence number into a pinned host word, on which the
+// batch's callers spin before they sleep; the watcher wakes the sleepers.
 #pragma once
 
 #include <atomic>
@@ -45,7 +44,6 @@ struct SubmitReq {
     std::atomic<uint64_t> seq{0};
     std::atomic<int> done{0};
     int rc = SHMR_EC_OK;
-    SubmitReq* next = nullptr;      // the queue's lock-free inbox (submit.cpp)
 };
 
 // Queues r (validated by the caller: crate checks, non-NULL touched shards,
