@@ -79,6 +79,31 @@ def test_alloc_shards_placement_and_free(gpu):
     assert L.shmr_ec_device_free_shards(0, arr[0]) == -100
 
 
+def _needs_plan_list(present, k_max_segs=32):
+    """Mirror of ptrs.cpp lattice_needs_plan_list for blocks on slots 0..B-1:
+    several erasure patterns of one absent count whose blocks fall into more
+    arithmetic runs than the kernel arguments hold send a rebuild to the table
+    kernels (no grid call counted)."""
+    by_pattern = {}
+    for b, row in enumerate(np.asarray(present)):
+        by_pattern.setdefault(bytes(row), []).append(b)
+    by_m = {}
+    for pat, slots in by_pattern.items():
+        m = sum(1 for x in pat if not x)
+        runs, i = 0, 0
+        while i < len(slots):
+            e = i + 1
+            st = slots[e] - slots[i] if e < len(slots) else 1
+            while e < len(slots) and slots[e] - slots[e - 1] == st:
+                e += 1
+            runs += 1
+            i = e
+        c = by_m.setdefault(m, [0, 0])
+        c[0] += 1
+        c[1] += runs
+    return any(n > 1 and r > k_max_segs for n, r in by_m.values())
+
+
 @pytest.mark.parametrize("k,p,S,B", [(8, 3, 65536, 9), (10, 4, 3 * 8192 + 2458, 5), (4, 2, 4096 * 5, 33),
                                      (1, 1, 17, 4)])
 @pytest.mark.parametrize("joint", [True, False])
@@ -164,7 +189,7 @@ def test_grid_reconstruct_in_place(gpu, k, p, S, B, mixed, data_only):
     rc = rs._L.shmr_ec_reconstruct_ptrs_dev(rs._h, tab, pr.ctypes.data_as(_u8p), B, S, int(data_only), 0, _stream())
     assert rc == 0, shmr_amd.Error(rc).name
     torch.cuda.synchronize()
-    assert _stats()["ptr_table_grids"] == st0["ptr_table_grids"] + 1
+    assert _stats()["ptr_table_grids"] == st0["ptr_table_grids"] + (0 if _needs_plan_list(present) else 1)
     want = cw.copy()
     if data_only:
         keep_parity = (present == 0)
@@ -216,7 +241,8 @@ def test_grid_reconstruct_fresh_buffers(gpu, k, p, S, B, erasures, data_only):
     rc = rs._L.shmr_ec_reconstruct_ptrs_dev(rs._h, tab, pr.ctypes.data_as(_u8p), B, S, int(data_only), 0, _stream())
     assert rc == 0, shmr_amd.Error(rc).name
     torch.cuda.synchronize()
-    assert _stats()["ptr_table_grids"] == st0["ptr_table_grids"] + 1
+    # (mixed patterns in more runs than the kernel arguments hold: the table kernels)
+    assert _stats()["ptr_table_grids"] == st0["ptr_table_grids"] + (0 if _needs_plan_list(present) else 1)
     o = oview.cpu().numpy()
     for b in range(B):
         idx = np.flatnonzero(written[b])
