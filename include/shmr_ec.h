@@ -417,7 +417,13 @@ int shmr_ec_set_device(shmr_ec_t* rs, int device);
  * shards in place, or rebuilt shard j of block b at out + b * out_block_pitch +
  * j * out_shard_pitch) -- runs through the strided kernels of the *_batch_dev
  * calls with no table (same bytes; SHMR_EC_DEV_PTR_TABLE_GRIDS counts them);
- * 0 always takes the table kernels.
+ * 0 always takes the table kernels.  A table whose blocks sit on a slot
+ * lattice (a slab or a pool, in any order, with holes) runs the strided
+ * kernels over its slots when they form one arithmetic run or up to 32 runs
+ * (segment launches); beyond that the table kernels run, measured faster than
+ * an uploaded slot list ("lattice_list" (0/1, default 0): 1 takes the list).
+ * Rebuilds with several erasure patterns in more runs than that take the
+ * table kernels too.
  * "ptrs_direct" (default 16): zero-copy launches of at most this many 4 KiB
  * tiles read their shard-pointer table from pinned host memory in place
  * instead of uploading it first (0: always upload).  "sync_spin_us"

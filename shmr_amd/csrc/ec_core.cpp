@@ -72,6 +72,11 @@ std::atomic<int> g_slots_list{0};
 // is two dependent loads away), 1 = one single-plan launch set per pattern over
 // its blocks (launch_slots: a run, segment runs or a block list)
 std::atomic<int> g_pattern_launches{0};
+// Lattice tables whose slots need the uploaded block list (more than 32
+// arithmetic runs, or several runs where segment launches do not apply):
+// 0 = the table kernels instead (measured faster: profiles/r06 s1, s3, s14,
+// ptrs_ab pool_holed vs pool_holed_tab), 1 = the strided kernels over the list
+std::atomic<int> g_lattice_list{0};
 
 // The launch policy itself is kern::policy_variant (gf_apply.hpp): constexpr,
 // so the product library compiles exactly the kernels it can select.  Its
@@ -161,6 +166,11 @@ int set_tuning(const char* key, int value) {
     }
     if (k == "pattern_launches") {   // not per op class
         g_pattern_launches = value == kAuto ? 0 : (value != 0);
+        return SHMR_EC_OK;
+    }
+    if (k == "lattice_list") {   // not per op class
+        if (value != kAuto && value != 0 && value != 1) return SHMR_EC_INVALID_ARGUMENT;
+        g_lattice_list = value == kAuto ? 0 : value;
         return SHMR_EC_OK;
     }
     if (k == "slots_list") {   // not per op class; tools build only
@@ -270,6 +280,7 @@ int get_tuning(const char* key) {
     if (k == "sync_spin_us") return g_sync_spin;
     if (k == "alias_devices") return g_alias_devices;
     if (k == "slots_list") return g_slots_list;
+    if (k == "lattice_list") return g_lattice_list;
     if (k == "pattern_launches") return g_pattern_launches;
     if (k == "uvec") return g_uvec;
     if (k == "chunks") return T.u;
@@ -399,6 +410,19 @@ bool mirror_zero_copy() { return g_mirror_zc.load() != 0; }
 uint64_t ptrs_direct_max() { return uint64_t(g_ptrs_direct.load()); }
 
 bool ptrs_grid() { return g_ptrs_grid.load() != 0; }
+
+bool slots_launch_fits(OpClass op, unsigned k, const Layout& L, const uint64_t* slots, uint64_t n) {
+    if (g_lattice_list.load(std::memory_order_relaxed)) return true;
+    uint64_t runs = 0;
+    for (uint64_t i = 0; i < n;) {   // (launch_slots' run split)
+        uint64_t e = i + 1;
+        const uint64_t st = e < n ? slots[e] - slots[i] : 1;
+        while (e < n && slots[e] - slots[e - 1] == st) ++e;
+        if (++runs > kern::kMaxSegs) return false;
+        i = e;
+    }
+    return runs <= 1 || segs_supported(op, k, L.host_mapped, L.d_ptrs != nullptr, L.compact);
+}
 
 hipError_t sync_stream(hipStream_t stream) {
     const int spin = g_sync_spin.load();
@@ -1122,7 +1146,9 @@ int launch_slots(Plan& plan, int dev, const Layout& L, const uint64_t* slots, ui
     }
     if (fits && segs_supported(op, plan.k, L.host_mapped, L.d_ptrs != nullptr, L.compact)) {
         const uint8_t* dp = nullptr;
-        const int rc = plan_on_device(plan, dev, stream, L.compact, &dp);
+        int rc = device_init(dev, stream);
+        if (rc) return rc;
+        rc = plan_on_device(plan, dev, stream, L.compact, &dp);
         if (rc) return rc;
         for (auto& sg : segs) sg.plan = dp;
         BlockSet bs;
@@ -1154,6 +1180,10 @@ int launch_slots(Plan& plan, int dev, const Layout& L, const uint64_t* slots, ui
 
 int encode_on_device(Codec& c, int dev, const Layout& L, uint64_t nblocks, uint64_t len, hipStream_t stream,
                      const uint64_t* slots) {
+    // (first: segment launches upload the plan before launch_set would init
+    // the device -- r06 s30, a pool encode as a process's first call)
+    const int rc = device_init(dev, stream);
+    if (rc) return rc;
     count_device(dev, kDevBlocksEncoded, nblocks);
     if (slots) return launch_slots(*c.encode_plan(), dev, L, slots, nblocks, len, stream, kEncode);
     BlockSet bs;

@@ -244,6 +244,11 @@ struct BlockSet {
 int launch_set(Plan& shape, int dev, const Layout& L, const BlockSet& bs, uint64_t len, hipStream_t stream,
                OpClass op);
 
+// Whether a lattice launch over these (ascending) slots runs without the
+// uploaded block list: one arithmetic run, or segment runs (knob
+// "lattice_list" = 1: always true -- the list is used).
+bool slots_launch_fits(OpClass op, unsigned k, const Layout& L, const uint64_t* slots, uint64_t n);
+
 // Encode nblocks blocks laid out per `L` (plan = the codec's parity rows).
 // slots (r06, nullable): batch block j is layout block slots[j] (ascending,
 // distinct, < 2^32) -- a slot lattice (ptr_grid.hpp) of a pool or of merged

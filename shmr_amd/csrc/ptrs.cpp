@@ -169,7 +169,8 @@ int ptrs_launch(Codec& c, const uint64_t* tab, const uint8_t* present, size_t nb
     if (ptrs_grid()) {
         LatticeForm F;
         if (lattice_form(k, t, tab, present, nblocks, data_only, op, host_mapped, &F) &&
-            !(op == kDecode && lattice_needs_plan_list(t, present, F))) {
+            !(op == kDecode && lattice_needs_plan_list(t, present, F)) &&
+            slots_launch_fits(op, k, F.L, F.slots.data(), F.slots.size())) {
             int rc;
             if (op == kEncode) {
                 rc = encode_on_device(c, device, F.L, F.rows.size(), len, stream, F.slots.data());

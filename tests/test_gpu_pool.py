@@ -6,8 +6,9 @@ The reference's Block Cache takes and drops one block's buffers at a time
 slab and takes them back singly; after churn the live blocks of a flush sit in
 any order with holes.  Their pointer tables lie on the slab's slot lattice
 (ptr_grid.hpp), so *_ptrs_dev and the submission queue run the strided
-kernels over the slots (counter ptr_table_grids): one run, segment runs, or
-an uploaded block list.  Every byte must equal the oracle's and nothing
+kernels over the slots (counter ptr_table_grids): one run or up to 32
+segment runs; beyond that the table kernels (measured faster than an uploaded
+slot list; knob lattice_list).  Every byte must equal the oracle's and nothing
 outside the blocks' shards may change."""
 import ctypes
 
@@ -31,6 +32,22 @@ def _parity(k, p, data):
 def _tab(rows):
     arr = np.ascontiguousarray(np.asarray(rows, dtype=np.uint64).reshape(-1))
     return arr, arr.ctypes.data_as(ctypes.POINTER(_u8p))
+
+
+def _fits_args(slots):
+    """Mirror of ec_core slots_launch_fits on device pitch layouts: the slots
+    (ascending) form at most 32 arithmetic runs -- otherwise the table kernels
+    run (knob lattice_list, default 0)."""
+    slots = sorted(int(x) for x in slots)
+    runs, i = 0, 0
+    while i < len(slots):
+        e = i + 1
+        st = slots[e] - slots[i] if e < len(slots) else 1
+        while e < len(slots) and slots[e] - slots[e - 1] == st:
+            e += 1
+        runs += 1
+        i = e
+    return runs <= 32
 
 
 def _stream():
@@ -95,7 +112,8 @@ def test_pool_churn_encode_and_rebuild(gpu, k, p, S):
         keep, tab = _tab(rows)
         assert rs._L.shmr_ec_encode_ptrs_dev(rs._h, tab, B, S, 0, _stream()) == 0
         torch.cuda.synchronize()
-        assert shmr_amd.device_stats(0)["ptr_table_grids"] == g0 + 1
+        enc = 1 if _fits_args([(int(r[0]) - base) // (t * P) for r in rows]) else 0
+        assert shmr_amd.device_stats(0)["ptr_table_grids"] == g0 + enc
         want = _parity(k, p, data)
         full = np.concatenate([data, want], axis=1)
         for b in range(B):
@@ -110,8 +128,8 @@ def test_pool_churn_encode_and_rebuild(gpu, k, p, S):
         assert rs._L.shmr_ec_reconstruct_ptrs_dev(rs._h, tab, _ptr(present), B, S, 0, 0, _stream()) == 0
         torch.cuda.synchronize()
         # (mixed patterns in more runs than the kernel arguments hold take the
-        # table kernels: ptrs.cpp lattice_needs_plan_list)
-        assert shmr_amd.device_stats(0)["ptr_table_grids"] in (g0 + 1, g0 + 2)
+        # table kernels: ptrs.cpp lattice_needs_plan_list, slots_launch_fits)
+        assert shmr_amd.device_stats(0)["ptr_table_grids"] in (g0 + enc, g0 + enc + 1)
         for b in range(B):
             for i in range(t):
                 assert np.array_equal(pool.shard(rows[b], i).cpu().numpy(), full[b, i]), (rnd, b, i)
@@ -184,3 +202,34 @@ def test_pool_failed_disk_rebuild_on_the_lattice(gpu):
     for b in range(B):
         for i in range(t):
             assert np.array_equal(pool.shard(rows[b], i).cpu().numpy(), full[b, i]), (b, i)
+
+
+def test_pool_lattice_encode_as_first_call(gpu):
+    """A process whose first compute call is a pool encode over segment runs
+    (r06 s30: the segment launch uploaded its plan before the device state
+    existed and returned INVALID_ARGUMENT)."""
+    import os
+    import subprocess
+    import sys
+    code = r'''
+import ctypes, numpy as np, torch, shmr_amd
+from shmr_amd.reed_solomon import _u8p
+k, p, S = 8, 3, 65536
+rs = shmr_amd.ReedSolomon(k, p)
+pool = shmr_amd.ShardPool(k + p, S, 16)
+blocks = [pool.alloc() for _ in range(16)]
+for j in (13, 9, 4, 1):
+    pool.free(blocks.pop(j))
+tab = np.ascontiguousarray(np.stack(blocks).reshape(-1))
+sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+g0 = shmr_amd.device_stats(0)["ptr_table_grids"]
+rc = rs._L.shmr_ec_encode_ptrs_dev(rs._h, tab.ctypes.data_as(ctypes.POINTER(_u8p)), len(blocks), S, 0, sp)
+torch.cuda.synchronize()
+print(rc, shmr_amd.device_stats(0)["ptr_table_grids"] - g0)
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env,
+                         cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.split()[-2:] == ["0", "1"], out.stdout

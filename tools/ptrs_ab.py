@@ -29,7 +29,10 @@ can get:
   pool_holed     r06: a pool after churn: B + B/4 slots, a random quarter freed,
                  the B live blocks in shuffled order (lattice runs -> segment runs
                  or a block list); _tab: the same with ptrs_grid=0; _pl (rebuilds):
-                 one launch set per erasure pattern (knob pattern_launches)
+                 one launch set per erasure pattern (knob pattern_launches); _list:
+                 knob lattice_list=1 (a block list where runs do not fit the kernel
+                 arguments; default: the table kernels)
+  pool_few       r06: B + 16 slots, 16 freed (at most 17 runs: segment launches)
   joint_padNk    r06, encode: one torch slab, block b's k + p shards at b * (t*P + N KiB)
                  + i * P (the pool's slot layout, with N KiB between slots)
 
@@ -93,10 +96,12 @@ def main():
         keep.append(arr)
         return arr.ctypes.data_as(ctypes.POINTER(_u8p))
 
-    def ptrs_run(tab, grid=True):
+    def ptrs_run(tab, grid=True, use_list=False):
         def f():
             if not grid:
                 shmr_amd.set_tuning(ptrs_grid=0)
+            if use_list:
+                shmr_amd.set_tuning(lattice_list=1)
             try:
                 if er == 0:
                     return rs._L.shmr_ec_encode_ptrs_dev(rs._h, tab, B, S, 0, sp)
@@ -104,6 +109,8 @@ def main():
             finally:
                 if not grid:
                     shmr_amd.set_tuning(ptrs_grid=-2)
+                if use_list:
+                    shmr_amd.set_tuning(lattice_list=-2)
         return f
 
     def rebuilt_into(addrs, out_addr):
@@ -178,7 +185,7 @@ def main():
     # order -- a Block Cache after churn.  Encodes write parity into the block's
     # own slot; rebuilds write the lost shard in place.  _tab: ptrs_grid=0.
     prng = np.random.default_rng(17)
-    for name, extra in (("pool_dense", 0), ("pool_holed", B // 4)):
+    for name, extra in (("pool_dense", 0), ("pool_holed", B // 4), ("pool_few", 16)):
         pool = shmr_amd.ShardPool(t, S, B + extra)
         blocks = [pool.alloc() for _ in range(B + extra)]
         for j in sorted(prng.choice(B + extra, size=extra, replace=False).tolist(), reverse=True):
@@ -192,6 +199,7 @@ def main():
         assert rs._L.shmr_ec_encode_ptrs_dev(rs._h, ptab, B, S, 0, sp) == 0
         runs[name] = ptrs_run(ptab)
         runs[name + "_tab"] = ptrs_run(ptab, grid=False)
+        runs[name + "_list"] = ptrs_run(ptab, use_list=True)
         if er:   # the rebuild's patterns as one launch set each (knob pattern_launches)
             def pl(f=ptrs_run(ptab)):
                 shmr_amd.set_tuning(pattern_launches=1)
