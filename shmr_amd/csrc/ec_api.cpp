@@ -521,8 +521,7 @@ std::unique_ptr<core::SubmitReq> make_req(shmr_ec_t* rs, core::OpClass op, bool 
     r->host_mapped = host_mapped;
     r->len = len;
     r->dev = dev;
-    r->row = std::move(row);
-    if (present) r->present.assign(present, present + r->row.size());
+    r->set_row(row.data(), present, unsigned(row.size()));   // (after len and host_mapped: its time estimate)
     return r;
 }
 

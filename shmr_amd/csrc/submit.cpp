@@ -295,11 +295,7 @@ private:
         queued_.fetch_sub(int64_t(n), std::memory_order_seq_cst);
         const uint64_t seq = ++launched_;
         double bytes_ns = 0;   // the batch's estimated GPU time
-        for (const SubmitReq* q : take_) {
-            size_t touched = 0;
-            for (uint64_t a : q->row) touched += a != 0;
-            bytes_ns += double(touched) * double(q->len) / (q->host_mapped ? kHostBytesPerNs : kDevBytesPerNs);
-        }
+        for (const SubmitReq* q : take_) bytes_ns += q->est_ns;
         hipEvent_t ev = nullptr;   // (a blocking-sync event from the pool, or made by launch)
         {
             std::lock_guard<std::mutex> lk(imu_);
@@ -377,10 +373,10 @@ private:
             const unsigned t = c.k() + c.p();
             const size_t n = v.size();
             tab_.resize(n * t);
-            for (size_t b = 0; b < n; ++b) std::memcpy(&tab_[b * t], v[b]->row.data(), t * sizeof(uint64_t));
+            for (size_t b = 0; b < n; ++b) std::memcpy(&tab_[b * t], v[b]->row_data(), t * sizeof(uint64_t));
             if (v[0]->op == kDecode) {
                 present_.resize(n * t);
-                for (size_t b = 0; b < n; ++b) std::memcpy(&present_[b * t], v[b]->present.data(), t);
+                for (size_t b = 0; b < n; ++b) std::memcpy(&present_[b * t], v[b]->present_data(), t);
             }
             int rc;
             try {
@@ -639,6 +635,27 @@ Queue* queue_for(int dev, int* rc) {
 }
 
 }  // namespace
+
+void SubmitReq::set_row(const uint64_t* r, const uint8_t* pr, unsigned t) {
+    total = t;
+    uint64_t* dst = row_inline;
+    uint8_t* pdst = present_inline;
+    if (t > kInline) {
+        row.resize(t);
+        dst = row.data();
+        if (pr) {
+            present.resize(t);
+            pdst = present.data();
+        }
+    }
+    size_t touched = 0;
+    for (unsigned i = 0; i < t; ++i) {
+        dst[i] = r[i];
+        touched += r[i] != 0;
+    }
+    if (pr) std::memcpy(pdst, pr, t);
+    est_ns = double(touched) * double(len) / (host_mapped ? kHostBytesPerNs : kDevBytesPerNs);
+}
 
 int submit(SubmitReq* r) {
     int rc = SHMR_EC_OK;

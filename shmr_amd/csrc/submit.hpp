@@ -36,8 +36,20 @@ struct SubmitReq {
     bool host_mapped = false;       // row addresses are mapped host memory
     uint64_t len = 0;
     int dev = 0;
-    std::vector<uint64_t> row;      // total device addresses, shard index order (0: not touched)
-    std::vector<uint8_t> present;   // reconstruct: total flags
+    // The block's row -- total device addresses in shard index order (0: not
+    // touched) -- and, for a reconstruct, its presence flags: in the request
+    // itself up to kInline shards (the launcher reads one object per request,
+    // no second cache miss), else in the vectors.  set_row() fills them.
+    static constexpr unsigned kInline = 24;
+    unsigned total = 0;
+    double est_ns = 0;              // the block's estimated GPU time (bytes at a nominal rate)
+    uint64_t row_inline[kInline];
+    uint8_t present_inline[kInline];
+    std::vector<uint64_t> row;
+    std::vector<uint8_t> present;
+    const uint64_t* row_data() const { return total <= kInline ? row_inline : row.data(); }
+    const uint8_t* present_data() const { return total <= kInline ? present_inline : present.data(); }
+    void set_row(const uint64_t* r, const uint8_t* pr, unsigned t);
     // completion: the batch's sequence number (its completion mark), set
     // when the request is launched; done = 1 when its status is final without
     // a mark (a failed launch)
