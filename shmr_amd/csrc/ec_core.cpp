@@ -1654,7 +1654,11 @@ Staging* StagingPool::acquire(int dev, size_t bytes, int* rc) {
     if (!s) {
         s = new Staging;
         s->dev = dev;
-        if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+        // (greatest priority like the library's other streams: a stream of
+        // its own among the hardware queues, not one a held caller stream may
+        // share -- r06 s33, tests/test_gpu_hol.py)
+        DeviceScope scope(dev);
+        if (!scope.ok() || create_priority_stream(&s->stream) != hipSuccess) {
             (void)hipGetLastError();
             delete s;
             *rc = SHMR_EC_DEVICE_ERROR;

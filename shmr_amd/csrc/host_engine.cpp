@@ -135,7 +135,7 @@ struct DevicePipe {
         RelaxedCapture relaxed;
         for (auto& s : sets) {
             if (!s.stream) {
-                if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
+                if (create_priority_stream(&s.stream) != hipSuccess ||   // (as the library's other streams)
                     hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) {
                     (void)hipGetLastError();
                     return SHMR_EC_DEVICE_ERROR;
