@@ -65,10 +65,16 @@ bool lattice_form(unsigned k, unsigned t, const uint64_t* tab, const uint8_t* pr
     // index - k (encode: the parity rows), at their rank q among the block's
     // rebuilt shards (a compact output); every touched shard at its index
     // (rebuilt in place)
-    std::vector<RowEntry> ein, eout, eall;
+    // (epres, rebuilds: every present shard of the row -- they sit on the
+    // same lattice as the ones read, and pin its shard pitch when each row
+    // reads only one, k = 1)
+    std::vector<RowEntry> ein, eout, eall, epres;
     ein.reserve(n * k);
     eout.reserve(n * (t - k));
-    if (op == kDecode) eall.reserve(n * t);
+    if (op == kDecode) {
+        eall.reserve(n * t);
+        epres.reserve(n * t);
+    }
     unsigned in[256], out[256], ni = 0, no = 0;
     for (size_t b = 0; b < n; ++b) {
         touched_into(k, t, op, data_only, op == kEncode ? nullptr : present + b * t, in, &ni, out, &no);
@@ -84,6 +90,9 @@ bool lattice_form(unsigned k, unsigned t, const uint64_t* tab, const uint8_t* pr
                 const unsigned i = (y >= no || (x < ni && in[x] < out[y])) ? in[x++] : out[y++];
                 eall.push_back({r, i, row[i]});
             }
+            const uint8_t* pr = present + b * t;
+            for (unsigned i = 0; i < t; ++i)
+                if (pr[i] && row[i]) epres.push_back({r, i, row[i]});   // (queue rows: 0 where not read)
         }
     }
     if (rows.empty()) return false;
@@ -105,8 +114,11 @@ bool lattice_form(unsigned k, unsigned t, const uint64_t* tab, const uint8_t* pr
         // present shards on one lattice, rebuilt shards (q-th of the block) on
         // another: a compact output (device memory only)
         if (host_mapped) return false;
-        if (!grid::row_anchors(ein, nr, &sp_in, &ain) || !grid::fit_slots(ain, &gi, &slots)) return false;
-        if (!grid::row_anchors(eout, nr, &sp_out, &aout) || !grid::fit_with_slots(aout, slots, &go)) return false;
+        auto fit = [&](const std::vector<RowEntry>& e) {
+            return grid::row_anchors(e, nr, &sp_in, &ain) && grid::fit_slots(ain, &gi, &slots) &&
+                   grid::row_anchors(eout, nr, &sp_out, &aout) && grid::fit_with_slots(aout, slots, &go);
+        };
+        if (!fit(epres) && !fit(ein)) return false;
         L = Layout{reinterpret_cast<const uint8_t*>(uintptr_t(gi.base)), reinterpret_cast<uint8_t*>(uintptr_t(go.base)),
                    gi.bpitch, sp_in, go.bpitch, sp_out, 0};
         L.compact = true;
