@@ -91,6 +91,7 @@ struct Trace {
     ~Trace() {
         if (!on || ev.empty()) return;
         const int64_t base = ev.front().t0;
+        std::fprintf(stderr, "QTRACE base_ns=%lld\n", (long long)base);
         for (const TraceEv& e : ev)
             std::fprintf(stderr, "QTRACE %s mode=%d n=%d f=%d t0=%.1f t1=%.1f\n",
                          e.kind == 0 ? "launch" : e.kind == 1 ? "reaped" : e.kind == 3 ? "phase" : "other", e.mode, e.n, e.f,

@@ -287,6 +287,9 @@ int main(int argc, char** argv) {
                     });
                 (void)shmr_ec_queue_stats(0, q0, SHMR_EC_Q_COUNTERS);
                 const auto t0 = std::chrono::steady_clock::now();
+                if (std::getenv("SHMR_PB_GO"))   // (steady-clock ns: lines up with SHMR_QUEUE_TRACE's base_ns)
+                    std::fprintf(stderr, "PBGO threads=%d rep=%d ns=%lld\n", threads, r,
+                                 (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(t0.time_since_epoch()).count());
                 go.store(1, std::memory_order_release);
                 for (auto& th : ts) th.join();
                 const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
