@@ -232,7 +232,7 @@ int shmr_ec_describe_variant(int decode, uint32_t data_shards, uint32_t rows, ch
     for (const auto& kv : {std::make_pair(v.glds, " glds=1"), std::make_pair(v.serial, " serial=1"),
                            std::make_pair(v.sc1_store, " sc1_store=1"), std::make_pair(v.realign, " realign=1"),
                            std::make_pair(v.peel, " peel=1"), std::make_pair(v.wave_run, " wave_run=1"),
-                           std::make_pair(v.st_align, " st_align=1"), std::make_pair(v.xcd, " xcd=1")}) {
+                           std::make_pair(v.st_align, " st_align=1"), std::make_pair(v.xcd, " xcd=1"), std::make_pair(v.pair, " pair=1")}) {
         const size_t n = std::strlen(buf);
         if (kv.first && n + 1 < len) std::snprintf(buf + n, len - n, "%s", kv.second);
     }

@@ -44,6 +44,7 @@ struct Tuning {
     std::atomic<int> wave_run{kAuto};
     std::atomic<int> st_align{kAuto};
     std::atomic<int> xcd{kAuto};
+    std::atomic<int> pair{kAuto};
 };
 Tuning g_tune[2];   // [kEncode], [kDecode]
 std::atomic<int> g_bounce_kib{kBounceKibDefault};
@@ -205,7 +206,7 @@ int set_tuning(const char* key, int value) {
             {"grid", -1},      {"diag", 0},        {"threads", 256},    {"depth", kAuto},   {"wgs_per_cu", kAuto},
             {"occ", kAuto},    {"early", kAuto},   {"spre", kAuto},     {"fuse_tail", kAuto},
             {"glds", kAuto},   {"serial", kAuto},   {"sc1_store", kAuto}, {"realign", kAuto}, {"peel", kAuto}, {"wave_run", kAuto}, {"st_align", kAuto},
-            {"xcd", kAuto}};
+            {"xcd", kAuto},    {"pair", kAuto}};
         const auto it = kDefaults.find(k);
         return (it != kDefaults.end() && it->second == value) ? SHMR_EC_OK : SHMR_EC_INVALID_ARGUMENT;
     }
@@ -260,6 +261,8 @@ int set_tuning(const char* key, int value) {
             T.st_align = value == kAuto ? kAuto : (value != 0);
         } else if (k == "xcd") {
             T.xcd = value == kAuto ? kAuto : (value != 0);
+        } else if (k == "pair") {
+            T.pair = value == kAuto ? kAuto : (value != 0);
         } else {
             return SHMR_EC_INVALID_ARGUMENT;
         }
@@ -304,6 +307,7 @@ int get_tuning(const char* key) {
     if (k == "wave_run") return T.wave_run;
     if (k == "st_align") return T.st_align;
     if (k == "xcd") return T.xcd;
+    if (k == "pair") return T.pair;
     return SHMR_EC_INVALID_ARGUMENT;
 }
 
@@ -329,6 +333,7 @@ kern::Variant select_variant(OpClass op, const kern::LaunchShape& s) {
     if (T.sc1_store.load() != kAuto) v.sc1_store = T.sc1_store.load() != 0;
     if (T.peel.load() != kAuto) v.peel = T.peel.load() != 0;
     if (T.xcd.load() != kAuto) v.xcd = T.xcd.load() != 0;
+    if (T.pair.load() != kAuto) v.pair = T.pair.load() != 0;
     if (T.wave_run.load() != kAuto)
         v.wave_run = T.wave_run.load() != 0;
     else

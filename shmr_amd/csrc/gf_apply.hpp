@@ -118,6 +118,10 @@ constexpr int kPeel = 1 << 25;
 constexpr int kWaveRun = 1 << 26;
 constexpr int kStAlign = 1 << 27;   // tools: misaligned output rows stored aligned (DPP-shifted)
 constexpr int kXcd = 1 << 28;       // tools: XCD-grouped tile order
+// tools: two neighbouring tiles per workgroup (one workgroup per pair): the
+// second tile of a block finds the block's pointer-table row in the scalar
+// cache its first tile filled
+constexpr int kPair = 1 << 29;
 // Bits 12-15: occupancy target in waves per SIMD (0 = compiler's choice);
 // the register allocator must then fit 512 / target VGPRs.
 constexpr int kOccShift = 12;
@@ -147,6 +151,7 @@ struct Variant {
     bool wave_run = false;   // U > 1 slots in wave-contiguous runs
     bool st_align = false;   // misaligned output rows: aligned stores realigned across lanes (tools)
     bool xcd = false;        // XCD-grouped tile order: neighbouring tiles on one XCD's L2 (tools)
+    bool pair = false;       // two neighbouring tiles per workgroup (tools)
 };
 
 // Template flags of a variant (its instantiation; wgs_per_cu is a launch
@@ -159,7 +164,7 @@ constexpr int variant_flags(const Variant& v) {
            (v.spre ? kSPre : 0) | (v.fuse_tail ? kFuse : 0) | (v.ptrs ? kPtrs : 0) | (v.segs ? kSegs : 0) |
            (v.glds ? kGlds : 0) | (v.serial ? kSerial : 0) | (v.sc1_store ? kSc1Store : 0) |
            (v.realign ? kRealign : 0) | (v.peel ? kPeel : 0) | (v.wave_run ? kWaveRun : 0) |
-           (v.st_align ? kStAlign : 0) | (v.xcd ? kXcd : 0);
+           (v.st_align ? kStAlign : 0) | (v.xcd ? kXcd : 0) | (v.pair ? kPair : 0);
 }
 
 // ---- launch policy -----------------------------------------------------------

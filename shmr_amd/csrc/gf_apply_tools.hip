@@ -9,6 +9,9 @@
 //  * the DPP realigning-load tile for misaligned shards (realign_tile):
 //    -2.7 / -2.7 points against the unaligned vector path on
 //    the reference's packed RS(10,4) buffer;
+//  * tile pairs per workgroup on the table kernels (kPair: the second tile
+//    finds its block's pointer-table row in the scalar cache): -2.0 to -10.3
+//    points (profiles/r06/s39);
 //  * ring depths 1/3/5/9, 128/512-lane workgroups, occupancy targets and the
 //    other knob combinations of the instantiation list below.
 #include <hip/hip_runtime.h>
@@ -514,7 +517,13 @@ __device__ __forceinline__ void store_run_aligned(uint8_t* p, const u32x4 (&v)[U
     X(1, kNtLoad | kSc1Store | kDepth2 | kSPre | kSegs) \
     X(1, kNtLoad | kSc1Store | kDepth2 | kSPre | kSegs | kFuse) \
     X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kSerial | kPeel | kWaveRun) \
-    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial | kPeel | kWaveRun)
+    X(2, kNtLoad | kNtStore | kDepth2 | kEarly | kSerial | kPeel | kWaveRun) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kPtrs | kPair) \
+    X(1, kNtLoad | kNtStore | kDepth2 | kEarly | kFuse | kPtrs | kPair) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kPtrs | kPeel | kPair) \
+    X(1, kNtLoad | kSc1Store | kDepth2 | kEarly | kFuse | kPtrs | kPeel | kPair) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kPtrs | kWaveRun | kPair) \
+    X(2, kNtLoad | kNtStore | kDepth2 | kFuse | kPtrs | kWaveRun | kPair)
 
 // The round-3 product list (every row count), so the tools build can still
 // A/B the r03 policy against the current one.

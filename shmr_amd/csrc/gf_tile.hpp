@@ -664,10 +664,18 @@ __device__ __forceinline__ TileRef tile_ref(const ApplyArgs& a, uint64_t tile) {
     return TileRef{j, tile - j * tpb, false};
 }
 
-// First grid tile of this workgroup (kXcd: XCD-grouped, one workgroup per tile).
+// Neighbouring tiles a workgroup takes per grid step (kPair: 2).
+template <int F>
+__device__ __host__ constexpr uint64_t tiles_per_wg() {
+    return (F & kPair) != 0 ? 2 : 1;
+}
+
+// First grid tile of this workgroup (kXcd: XCD-grouped, one workgroup per
+// tile; kPair: tile pairs 2w, 2w + 1, grid-strided over the pairs).
 template <int F>
 __device__ __forceinline__ uint64_t first_tile(const ApplyArgs& a) {
     uint64_t w = blockIdx.x;
+    if constexpr ((F & kPair) != 0) return w * 2;
     if constexpr ((F & kXcd) != 0) {
         if (uint64_t(gridDim.x) == a.ntiles) {
             const uint64_t q = a.ntiles >> 3;
@@ -675,6 +683,12 @@ __device__ __forceinline__ uint64_t first_tile(const ApplyArgs& a) {
         }
     }
     return w;
+}
+
+template <int F>
+__device__ __forceinline__ uint64_t next_tile(uint64_t tile) {
+    if constexpr ((F & kPair) != 0) return (tile & 1) ? tile + uint64_t(gridDim.x) * 2 - 1 : tile + 1;
+    return tile + gridDim.x;
 }
 
 // The second __launch_bounds__ argument is amdgpu_waves_per_eu (minimum).
@@ -688,7 +702,7 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
     if constexpr ((F & (kEarly | kSPre)) != 0) {
         const uint64_t tb = uint64_t(TH) * 16 * U;
         bool first = true;
-        for (uint64_t tile = first_tile<F>(a); tile < a.ntiles; tile += gridDim.x) {
+        for (uint64_t tile = first_tile<F>(a); tile < a.ntiles; tile = next_tile<F>(tile)) {
             const TileRef tr = tile_ref<F>(a, tile);
             const uint64_t j = tr.j, cc = tr.cc;
             uint64_t blk;
@@ -733,7 +747,7 @@ __global__ __launch_bounds__(threads_of<F>(), occ_of<F>() ? occ_of<F>() : 1) voi
         __syncthreads();
     }
     const uint64_t tb = uint64_t(TH) * 16 * U;
-    for (uint64_t tile = first_tile<F>(a); tile < a.ntiles; tile += gridDim.x) {
+    for (uint64_t tile = first_tile<F>(a); tile < a.ntiles; tile = next_tile<F>(tile)) {
         const TileRef tr = tile_ref<F>(a, tile);
         const uint64_t j = tr.j, cc = tr.cc;
         const uint8_t* plan = a.plan;
@@ -774,8 +788,9 @@ hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStr
         if (e != hipSuccess) return e;
     }
     uint64_t grid;
+    const uint64_t units = (a.ntiles + tiles_per_wg<F>() - 1) / tiles_per_wg<F>();   // kPair: tile pairs
     if (grid_cap < 0) {
-        grid = a.ntiles;                      // one workgroup per tile
+        grid = units;                         // one workgroup per tile (pair)
         if (grid > 0x7fffffffull) grid = 0x7fffffffull;
     } else {
         int dev = 0;
@@ -791,10 +806,10 @@ hipError_t launch_one(const ApplyArgs& a, const Variant& v, int grid_cap, hipStr
         if (grid_cap > 0 && uint64_t(grid_cap) < maxg) maxg = uint64_t(grid_cap);
         // Balanced persistent grid: every workgroup gets ceil(ntiles / maxg)
         // or one fewer tile, so the launch has no straggler round.
-        const uint64_t per = (a.ntiles + maxg - 1) / maxg;
-        grid = (a.ntiles + per - 1) / per;
+        const uint64_t per = (units + maxg - 1) / maxg;
+        grid = (units + per - 1) / per;
     }
-    if (grid > a.ntiles) grid = a.ntiles;
+    if (grid > units) grid = units;
     if (grid == 0) return hipSuccess;
     // Launched by name, never through the function-pointer variable `kern`: in
     // host code a kernel's "address" is its kernel handle (a data object), and
