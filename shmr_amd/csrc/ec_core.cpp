@@ -656,6 +656,23 @@ bool own_stream(hipStream_t s) {
     return g_own_streams->count(s) != 0;
 }
 
+hipError_t grow_scratch(uint8_t** p, size_t* cap, size_t bytes, bool host) {
+    static std::mutex mu;
+    static auto* kept = new std::vector<std::pair<void*, bool>>;   // leaked: outlives static teardown
+    const size_t want = std::max(bytes, *cap * 2);
+    void* q = nullptr;
+    const hipError_t e = host ? hipHostMalloc(&q, want, hipHostMallocMapped | hipHostMallocPortable)
+                              : hipMalloc(&q, want);
+    if (e != hipSuccess) return e;
+    if (*p) {
+        std::lock_guard<std::mutex> lock(mu);
+        kept->emplace_back(*p, host);
+    }
+    *p = static_cast<uint8_t*>(q);
+    *cap = want;
+    return hipSuccess;
+}
+
 hipError_t create_priority_stream(hipStream_t* s) {
     int least = 0, greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) {
@@ -1673,16 +1690,13 @@ Staging* StagingPool::acquire(int dev, size_t bytes, int* rc) {
         count_device(dev, kDevStagingStreams);
     }
     if (s->cap < bytes) {
-        if (s->dbuf && hipFree(s->dbuf) != hipSuccess) (void)hipGetLastError();
-        s->dbuf = nullptr;
-        s->cap = 0;
-        if (hipMalloc(reinterpret_cast<void**>(&s->dbuf), bytes) != hipSuccess) {
+        DeviceScope scope(dev);
+        if (!scope.ok() || grow_scratch(&s->dbuf, &s->cap, bytes, false) != hipSuccess) {
             (void)hipGetLastError();
             release(s);
             *rc = SHMR_EC_OUT_OF_MEMORY;
             return nullptr;
         }
-        s->cap = bytes;
     }
     *rc = SHMR_EC_OK;
     return s;

@@ -342,6 +342,14 @@ int record_mirrored(int dev, hipStream_t stream, hipEvent_t on_caller, hipEvent_
 // its queue; the library's own queue, mirror and private streams sit in the
 // high-priority pool instead (tests/test_gpu_hol.py).  Current device.
 hipError_t create_priority_stream(hipStream_t* s);
+// Grows a reusable scratch buffer (device memory, or mapped pinned host
+// memory with `host`) to at least `bytes`, doubling, without freeing the old
+// one: hipFree / hipHostFree synchronize the whole device, so a caller stream
+// held by a host-released wait would hold this call (r06 s40,
+// tests/test_gpu_hol.py).  The old buffer is kept for the process's life
+// (doubling bounds what is kept to the final size); its caller has drained
+// the work that used it.  *p / *cap unchanged on failure.
+hipError_t grow_scratch(uint8_t** p, size_t* cap, size_t bytes, bool host);
 // Streams the library creates (registered once, never destroyed).
 void register_own_stream(hipStream_t s);
 bool own_stream(hipStream_t s);

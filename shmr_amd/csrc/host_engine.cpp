@@ -143,27 +143,18 @@ struct DevicePipe {
                 register_own_stream(s.stream);
                 count_device(dev, kDevStagingStreams);
             }
-            if (s.dcap < dbytes) {
-                if (s.dbuf && hipFree(s.dbuf) != hipSuccess) (void)hipGetLastError();
-                s.dbuf = nullptr;
-                s.dcap = 0;
-                if (hipMalloc(reinterpret_cast<void**>(&s.dbuf), dbytes) != hipSuccess) {
-                    (void)hipGetLastError();
-                    return SHMR_EC_OUT_OF_MEMORY;
-                }
-                s.dcap = dbytes;
+            // (grown without a free: a hipFree would wait for every stream of
+            // the device, a held caller stream included)
+            if (s.dcap < dbytes && grow_scratch(&s.dbuf, &s.dcap, dbytes, false) != hipSuccess) {
+                (void)hipGetLastError();
+                return SHMR_EC_OUT_OF_MEMORY;
             }
             if (s.hcap < hbytes) {
-                if (s.hbuf && hipHostFree(s.hbuf) != hipSuccess) (void)hipGetLastError();
-                s.hbuf = nullptr;
-                s.hcap = 0;
-                s.hbuf_unified = false;
-                if (hipHostMalloc(reinterpret_cast<void**>(&s.hbuf), hbytes,
-                                  hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) {
+                if (grow_scratch(&s.hbuf, &s.hcap, hbytes, true) != hipSuccess) {
                     (void)hipGetLastError();
                     return SHMR_EC_OUT_OF_MEMORY;
                 }
-                s.hcap = hbytes;
+                s.hbuf_unified = false;
                 void* d = nullptr;
                 s.hbuf_unified = hipHostGetDevicePointer(&d, s.hbuf, 0) == hipSuccess && d == s.hbuf;
                 if (!s.hbuf_unified) (void)hipGetLastError();

@@ -7,7 +7,9 @@ host-released wait.  tools/hol_held.py holds stream A with
 hipStreamWaitValue32 (released by the host after 1 s) behind library work
 that uploads a new plan and takes upload-ring slots, while thread B runs
 library calls on stream B that need the same plan and cycle every ring slot,
-plus the submission queue and a mapped host-buffer call.  Since r06 the
+plus the submission queue and host-buffer calls (mapped and pageable) whose
+scratch buffers grow during the hold -- grown without a free, since hipFree
+waits for every stream of the device (r06 s40).  Since r06 the
 library keeps a caller stream's readiness mirrors on a mirror stream of its
 own, re-uploads a plan another stream still has in flight, and takes a ring
 slot whose last reader has finished: none of B's steps may wait for A's

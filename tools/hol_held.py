@@ -7,8 +7,11 @@ with library work queued behind the wait that takes a new erasure plan (its
 first upload is on A) and upload-ring slots.  Meanwhile thread B, on stream B,
 runs: a plain torch kernel (the runtime baseline: B's hardware queue may be
 shared with A's), device-resident calls that need the same plan, pointer-table
-calls that cycle every ring slot, the per-block queue call, and a host-buffer
-call.  The word is released after --hold seconds.  Each of B's steps reports
+calls that cycle every ring slot, the per-block queue call, and host-buffer
+calls (mapped, and pageable through the staging pipe) larger than the ones made
+before the hold, so their scratch buffers grow during it (r06 s40: a growth
+that freed the old buffer -- hipFree waits for every stream of the device --
+was held back by A).  The word is released after --hold seconds.  Each of B's steps reports
 when it completed, relative to the hold; a step that completes only after the
 release was held back by A.
 
@@ -54,6 +57,11 @@ def run(hold: float = 1.0) -> dict:
     pa, pb = ctypes.c_void_p(sa.cuda_stream), ctypes.c_void_p(sb.cuda_stream)
     slab = torch.randint(0, 256, (2, B, t, S), dtype=torch.uint8, device=dev, generator=g)
     torch.cuda.synchronize()
+    # small host-buffer calls before the hold: the library's scratch for them
+    # exists and must grow for the larger calls made during it
+    small = shmr_amd.PinnedBuffer(t * 4096)
+    rs.encode([small.array.reshape(t, 4096)[i] for i in range(t)])
+    rs.encode([np.zeros(4096, np.uint8) for _ in range(t)])
     # pattern never used before: its plan's first upload goes on A
     present = np.ones((B, t), np.uint8)
     present[:, [1, 9]] = 0
@@ -106,6 +114,9 @@ def run(hold: float = 1.0) -> dict:
             h = host.array.reshape(t, S)
             rs.encode([h[i] for i in range(t)])
             mark("host_mapped_encode")
+            SP = 4 << 20
+            rs.encode([np.full(SP, i, np.uint8) if i < k else np.zeros(SP, np.uint8) for i in range(t)])
+            mark("host_pageable_encode")
             del y
         except Exception as e:  # noqa: BLE001
             steps["error"] = repr(e)
