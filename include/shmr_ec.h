@@ -338,7 +338,12 @@ int shmr_ec_host_unregister(void* p);
  * Measured on MI355X: contiguous VRAM lifts the XOR-only replica of the
  * RS(8,3) access pattern over 2,048 blocks (11 GiB) from 76 % to 78.5 % of
  * HBM peak, but the GF kernel itself runs the same on both (78.8 % at 2,048
- * blocks, 79.7 % at 512).  Free with shmr_ec_device_free on the same device. */
+ * blocks, 79.7 % at 512).  Free with shmr_ec_device_free on the same device.
+ * The frees here (shmr_ec_device_free, shmr_ec_device_free_shards,
+ * shmr_ec_pool_destroy, shmr_ec_host_free) are hipFree / hipHostFree: each
+ * waits for the work of every stream of the device, a caller stream held by a
+ * wait included.  The compute calls grow their own scratch without a free
+ * (r06 s40). */
 int shmr_ec_device_alloc(int device, size_t bytes, int contiguous, void** out);
 int shmr_ec_device_free(int device, void* p);
 
