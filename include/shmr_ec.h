@@ -343,7 +343,8 @@ int shmr_ec_host_unregister(void* p);
  * shmr_ec_pool_destroy, shmr_ec_host_free) are hipFree / hipHostFree: each
  * waits for the work of every stream of the device, a caller stream held by a
  * wait included.  The compute calls grow their own scratch without a free
- * (r06 s40). */
+ * (r06 s40); only the pinned bounce pool of pageable host calls frees, and only
+ * a buffer returned while 32 others lie idle. */
 int shmr_ec_device_alloc(int device, size_t bytes, int contiguous, void** out);
 int shmr_ec_device_free(int device, void* p);
 
